@@ -1,0 +1,52 @@
+"""Lock-step G-learner gossip on the CPU -- TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+One round per learner g, as the reference's README loop runs it (README.md:18-29):
+``update_send(loss)`` (adapters/pytorch.py:42-53 -> dpwa.py:104-123) publishes a copy of
+the parameters plus ``{clock, loss}``, draws the Bernoulli gate; the training step
+changes the parameters; ``update_wait(loss)`` (pytorch.py:55-68 -> dpwa.py:125-156)
+fetches one peer's published snapshot chosen by TxThread (conn.py:224-317), computes
+the factor/clock and averages.  "Lock-step" = every learner publishes round r before
+any fetch of round r is served, which is the schedule the GPU gossip group runs.
+"""
+import numpy as np
+
+from .lerp import lerp_f32
+from .policy import OracleLearner
+
+
+def simulate(names, init, deltas, send_loss, wait_loss, method, value, threshold, fetch_probability,
+             seeds, lerp=lerp_f32):
+    G, n = init.shape
+    T = deltas.shape[0]
+    learners = [OracleLearner(names[g], [x for x in names if x != names[g]], fetch_probability,
+                              method, value, threshold, seeds[g]) for g in range(G)]
+    params = init.copy()
+    out_params = np.zeros((T, G, n), init.dtype)
+    clocks = np.zeros((T, G))
+    factors = np.zeros((T, G))
+    fetching = np.zeros((T, G), bool)
+    picks = [[None] * G for _ in range(T)]
+    for r in range(T):
+        states, snaps = [], []
+        for g in range(G):
+            states.append(learners[g].update_send(send_loss[r][g]))
+            snaps.append(params[g].copy())
+            fetching[r, g] = learners[g].fetching
+        for g in range(G):
+            params[g] = np.add(params[g], deltas[r, g], dtype=params.dtype)
+        for g in range(G):
+            L = learners[g]
+            state, payload, attempts = None, None, []
+            if L.fetching:
+                idx = {nm: i for i, nm in enumerate(names)}
+                state, payload, attempts = L.fetch(
+                    lambda peer: "ok",
+                    lambda peer: ("payload", states[idx[peer]], snaps[idx[peer]]))
+            averaged, factor = L.update_wait(wait_loss[r][g], state, payload is not None)
+            if averaged:
+                params[g] = lerp(params[g], payload, factor)
+            picks[r][g] = [a["peer"] for a in attempts]
+            factors[r, g] = factor
+            clocks[r, g] = L.clock
+            out_params[r, g] = params[g]
+    return {"params": out_params, "clocks": clocks, "factors": factors, "fetching": fetching, "picks": picks}

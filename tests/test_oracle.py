@@ -1,0 +1,137 @@
+"""Pins the CPU oracle (oracle/) against the golden fixtures produced by running the
+reference (tests/golden/make_golden.py).  CPU only."""
+import json
+
+import numpy as np
+import pytest
+
+from oracle import gossip as ogossip
+from oracle import lerp as olerp
+from oracle import policy as opolicy
+from tests.helpers import AttemptReplay, hexf, load_json, load_npz, num
+
+
+def test_lerp_f32_numpy_matches_reference_adapter():
+    z = load_npz("lerp_f32.npz")
+    for f, out in zip(z["factors"], z["out"]):
+        got = olerp.lerp_f32(z["param"], z["peer"], float(f))
+        assert olerp.bits_equal(got, out), f
+
+
+def test_lerp_f32_c_matches_reference_adapter():
+    z = load_npz("lerp_f32.npz")
+    for f, out in zip(z["factors"], z["out"]):
+        p = z["param"].copy()
+        olerp.c_lerp_f32_(p, z["peer"].copy(), float(f))
+        assert olerp.bits_equal(p, out), f
+
+
+def test_lerp_f32_fma_would_not_match():
+    """The fixtures contain near-cancellation pairs on which a fused multiply-add differs:
+    guards against a restatement (or kernel) that silently contracts."""
+    z = load_npz("lerp_f32.npz")
+    f = 1.0 / 3.0
+    a, b = olerp.coefficients(f)
+    p = z["param"].astype(np.float64)
+    t = z["peer"].astype(np.float64)
+    with np.errstate(all="ignore"):
+        fused = (a * t + np.float32(b * z["param"]).astype(np.float64)).astype(np.float32)
+    out = z["out"][list(z["factors"]).index(f)]
+    assert not olerp.bits_equal(fused, out)
+    del p
+
+
+def test_lerp_bf16_matches_torch_eager():
+    z = load_npz("lerp_bf16.npz")
+    for f, out in zip(z["factors"], z["out"]):
+        assert olerp.bits_equal(olerp.lerp_bf16(z["param"], z["peer"], float(f)), out), f
+        p = z["param"].copy()
+        olerp.c_lerp_bf16_(p, z["peer"].copy(), float(f))
+        assert olerp.bits_equal(p, out), f
+
+
+def test_factor_c_matches_python_restatement():
+    lib = olerp.clib()
+    import ctypes
+    rng = np.random.default_rng(3)
+    for _ in range(2000):
+        m = int(rng.integers(0, 3))
+        vals = rng.uniform(0, 3, 5)
+        args = (m, float(vals[0] / 3), float(rng.choice([0.0, 0.5, 1.0])), float(vals[1]),
+                float(vals[2]), float(vals[3]), float(vals[4]))
+        fo, co = ctypes.c_double(), ctypes.c_double()
+        rc = lib.dpwa_oracle_factor(*args, ctypes.byref(fo), ctypes.byref(co))
+        f, c = opolicy.factor_and_clock(["constant", "clock", "loss"][m], args[1], args[2], args[3], args[4],
+                                        args[5], args[6])
+        assert rc == 0 and fo.value == f and co.value == c
+
+
+def test_policy_traces_match_reference():
+    data = load_json("policy.json")
+    assert len(data["cases"]) == 40
+    for case in data["cases"]:
+        L = opolicy.OracleLearner("w2", ["w1", "w3"], case["fetch_probability"], case["interpolation"],
+                                  case["value"], case["divergence_threshold"], case["seed"])
+        for r in case["rounds"]:
+            st = L.update_send(num(r["send_loss"]))
+            assert L.fetching == r["fetching"]
+            assert st["clock"] == r["pub_clock"] and st["loss"] == num(r["pub_loss"])
+            peer = {"clock": num(r["peer_clock"]), "loss": num(r["peer_loss"])}
+            if r["raises"]:
+                with pytest.raises(ZeroDivisionError):
+                    L.update_wait(num(r["wait_loss"]), peer, r["has_payload"])
+                L.fetching = False
+            else:
+                averaged, factor = L.update_wait(num(r["wait_loss"]), peer, r["has_payload"])
+                assert averaged == r["averaged"]
+                assert float(factor) == hexf(r["factor_hex"])
+            assert float(L.clock) == hexf(r["clock_hex"])
+
+
+def test_peer_selection_matches_reference_txthread():
+    data = load_json("peer_select.json")
+    assert len(data["cases"]) == 48
+    for case in data["cases"]:
+        L = opolicy.OracleLearner(case["me"], case["peers"], case["fetch_probability"], "clock", None, 0.0,
+                                  case["seed"])
+        for r in case["rounds"]:
+            L.update_send(1.0)
+            assert L.fetching == r["fetching"]
+            state, payload = None, None
+            if L.fetching:
+                rep = AttemptReplay(r["attempts"])
+                state, payload, attempts = L.fetch(rep.connect, rep.request)
+                assert rep.done()
+                assert [a["peer"] for a in attempts] == [a["peer"] for a in r["attempts"]]
+            else:
+                assert r["attempts"] == []
+            averaged, factor = L.update_wait(1.0, state, payload is not None)
+            assert averaged == r["data"]
+            assert float(factor) == hexf(r["factor_hex"])
+            assert float(L.clock) == hexf(r["clock_hex"])
+            assert L.scores(case["peers"]) == r["scores"]
+
+
+def test_gossip_trajectories_match_reference():
+    meta = load_json("gossip.json")
+    z = load_npz("gossip.npz")
+    for case in meta["cases"]:
+        k = case["key"]
+        res = ogossip.simulate(case["names"], z[k + "_init"], z[k + "_deltas"], case["send_loss"],
+                               case["wait_loss"], case["interpolation"], case["value"],
+                               case["divergence_threshold"], case["fetch_probability"], case["seeds"])
+        assert res["picks"] == case["picks"], k
+        assert np.array_equal(res["fetching"], z[k + "_fetching"]), k
+        assert np.array_equal(res["factors"], z[k + "_factors"]), k
+        assert np.array_equal(res["clocks"], z[k + "_clocks"]), k
+        assert olerp.bits_equal(res["params"], z[k + "_params"]), k
+
+
+def test_fixture_files_are_data_only():
+    """Fixtures are inputs/outputs (json/npz), never reference source."""
+    import os
+    from tests.helpers import GOLDEN
+    for fn in os.listdir(GOLDEN):
+        assert fn.endswith((".json", ".npz", ".py", ".md")), fn
+        if fn.endswith(".json"):
+            json.load(open(os.path.join(GOLDEN, fn)))
