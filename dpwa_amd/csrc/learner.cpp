@@ -1,0 +1,506 @@
+// learner.cpp -- the per-node runtime behind DpwaConnection (dpwa/dpwa.py:54-156) on MI355X.
+//
+// The reference keeps, per node, an RxThread that serves the latest (state, payload)
+// under a lock (conn.py:51-172) and a TxThread that fetches one peer's (state, payload)
+// over TCP (conn.py:197-334).  Here a node (learner) owns, on its GPU:
+//   slots    two snapshot slots [header 256 B | payload] -- RxThread.state/payload,
+//            double-buffered so a publish never overwrites the slot a peer may be reading
+//   staging  one slot-sized buffer receiving a peer's snapshot -- TxThread.peer_payload
+//   ctl      the device clock and the averaging coefficients (dpwa_coef)
+// and a side stream on which fetches (xGMI pulls for peers on other GPUs) overlap the
+// training step.  Nothing here synchronises the host with the device except the explicit
+// read/write helpers.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <set>
+#include <unistd.h>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+}  // namespace
+
+namespace dpwa {
+
+int set_error(int code, const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+}  // namespace dpwa
+
+using namespace dpwa;
+
+#define HIP_TRY(expr)                                                                                  \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            return set_error(DPWA_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+constexpr size_t kHeader = sizeof(dpwa_header);
+static_assert(sizeof(dpwa_header) == 256, "dpwa_header must be 256 bytes");
+constexpr uint64_t kIpcMagic = 0x445057414950430aULL;  // "DPWAIPC\n"
+
+struct IpcBlob {
+    hipIpcMemHandle_t handle;   // 64 B
+    uint64_t magic;
+    int64_t slot_stride;
+    int64_t n;
+    int32_t dtype;
+    int32_t device;
+    int32_t pid;
+    int32_t reserved;
+};
+static_assert(sizeof(IpcBlob) <= DPWA_IPC_HANDLE_BYTES, "IPC blob too large");
+
+struct Ctl {            // device control block
+    double clock;
+    double pad0;
+    dpwa_coef coef;
+};
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Registry of live learners, so a learner never dereferences a destroyed local peer.
+std::mutex g_reg_mu;
+std::set<dpwa_learner *> g_live;
+
+class DeviceGuard {
+public:
+    explicit DeviceGuard(int dev)
+    {
+        (void)hipGetDevice(&prev_);
+        if (prev_ != dev) (void)hipSetDevice(dev);
+        dev_ = dev;
+    }
+    ~DeviceGuard()
+    {
+        if (prev_ != dev_) (void)hipSetDevice(prev_);
+    }
+
+private:
+    int prev_ = 0, dev_ = 0;
+};
+
+}  // namespace
+
+struct Endpoint {
+    int kind = 0;                    // 1 local learner, 2 IPC-mapped
+    dpwa_learner *local = nullptr;
+    char *base = nullptr;            // slot 0 in this process's address space
+    int device = -1;
+    int64_t slot_stride = 0;
+    int64_t n = 0;
+    int32_t dtype = 0;
+};
+
+struct dpwa_learner {
+    int device = 0;
+    int64_t n = 0;
+    int32_t dtype = DPWA_F32;
+    dpwa_interp cfg{};
+    size_t payload_bytes = 0;
+    size_t slot_stride = 0;
+    char *slots = nullptr;          // 2 slots
+    char *staging = nullptr;        // 1 slot
+    Ctl *ctl = nullptr;
+    uint64_t version = 0;
+    bool exported = false;
+    hipStream_t side = nullptr;
+    hipEvent_t ev_published[2] = {nullptr, nullptr};
+    hipEvent_t ev_issue = nullptr;      // fetch may start (recorded on the caller's stream)
+    hipEvent_t ev_fetched = nullptr;    // fetch landed (recorded on the side stream)
+    hipEvent_t ev_consumed = nullptr;   // this learner finished reading its fetch source
+    hipEvent_t ev_factor = nullptr;     // last factor computation done
+    // fetch state
+    const char *src = nullptr;          // header of the snapshot to average with
+    bool src_copied = false;
+    bool have_fetch = false;
+    bool have_factor = false;
+    dpwa_learner *src_owner = nullptr;  // local peer whose slot is being read (reader tracking)
+    int src_slot = -1;
+    std::unordered_map<int, Endpoint> peers;
+    // learners (local) that read our slot k and must be waited for before rewriting it
+    std::mutex readers_mu;
+    std::vector<dpwa_learner *> readers[2];
+    int32_t *host_status = nullptr;     // pinned mirror of coef.status for non-blocking polls
+    int32_t *host_status_dev = nullptr; // its device-side address
+};
+
+static bool is_live(dpwa_learner *l)
+{
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    return g_live.count(l) != 0;
+}
+
+extern "C" {
+
+const char *dpwa_last_error(void) { return g_last_error.c_str(); }
+
+int dpwa_abi_version(void) { return DPWA_ABI_VERSION; }
+
+int dpwa_lerp_f32(float *param, const float *peer, int64_t n, const dpwa_coef *coef_dev, dpwa_stream_t stream)
+{
+    if (n < 0 || (n > 0 && (!param || !peer || !coef_dev))) return set_error(DPWA_ERR_ARG, "dpwa_lerp_f32: bad arguments");
+    HIP_TRY(launch_lerp(DPWA_F32, param, peer, n, coef_dev, 0.f, 0.f, (hipStream_t)stream));
+    return DPWA_OK;
+}
+
+int dpwa_lerp_bf16(uint16_t *param, const uint16_t *peer, int64_t n, const dpwa_coef *coef_dev,
+                   dpwa_stream_t stream)
+{
+    if (n < 0 || (n > 0 && (!param || !peer || !coef_dev))) return set_error(DPWA_ERR_ARG, "dpwa_lerp_bf16: bad arguments");
+    HIP_TRY(launch_lerp(DPWA_BF16, param, peer, n, coef_dev, 0.f, 0.f, (hipStream_t)stream));
+    return DPWA_OK;
+}
+
+int dpwa_lerp_f32_host(float *param, const float *peer, int64_t n, double factor, dpwa_stream_t stream)
+{
+    if (n < 0 || (n > 0 && (!param || !peer))) return set_error(DPWA_ERR_ARG, "dpwa_lerp_f32_host: bad arguments");
+    HIP_TRY(launch_lerp(DPWA_F32, param, peer, n, nullptr, (float)factor, (float)(1.0 - factor), (hipStream_t)stream));
+    return DPWA_OK;
+}
+
+int dpwa_lerp_bf16_host(uint16_t *param, const uint16_t *peer, int64_t n, double factor, dpwa_stream_t stream)
+{
+    if (n < 0 || (n > 0 && (!param || !peer))) return set_error(DPWA_ERR_ARG, "dpwa_lerp_bf16_host: bad arguments");
+    HIP_TRY(launch_lerp(DPWA_BF16, param, peer, n, nullptr, (float)factor, (float)(1.0 - factor), (hipStream_t)stream));
+    return DPWA_OK;
+}
+
+int dpwa_factor(const dpwa_interp *cfg, double *clock_dev, const dpwa_header *peer_header_dev, double loss,
+                const double *loss_dev, dpwa_coef *coef_dev, dpwa_stream_t stream)
+{
+    if (!cfg || !clock_dev || !peer_header_dev || !coef_dev) return set_error(DPWA_ERR_ARG, "dpwa_factor: NULL argument");
+    if (cfg->method < 0 || cfg->method > 2) return set_error(DPWA_ERR_ARG, "dpwa_factor: unknown method %d", cfg->method);
+    HIP_TRY(launch_factor(*cfg, clock_dev, peer_header_dev, loss, loss_dev, coef_dev, nullptr, (hipStream_t)stream));
+    return DPWA_OK;
+}
+
+int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype, const dpwa_interp *cfg)
+{
+    if (!out || n < 0 || !cfg || dtype_size(dtype) == 0) return set_error(DPWA_ERR_ARG, "dpwa_learner_create: bad arguments");
+    if (cfg->method < 0 || cfg->method > 2) return set_error(DPWA_ERR_ARG, "dpwa_learner_create: unknown method");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return set_error(DPWA_ERR_ARG, "dpwa_learner_create: device %d of %d", device, ndev);
+    DeviceGuard dg(device);
+    dpwa_learner *l = new (std::nothrow) dpwa_learner();
+    if (!l) return set_error(DPWA_ERR_NOMEM, "dpwa_learner_create: out of memory");
+    l->device = device;
+    l->n = n;
+    l->dtype = dtype;
+    l->cfg = *cfg;
+    l->payload_bytes = (size_t)n * dtype_size(dtype);
+    l->slot_stride = kHeader + round_up(l->payload_bytes, 256);
+    hipError_t e = hipSuccess;
+    do {
+        if ((e = hipMalloc(&l->slots, 2 * l->slot_stride)) != hipSuccess) break;
+        if ((e = hipMalloc(&l->staging, l->slot_stride)) != hipSuccess) break;
+        if ((e = hipMalloc(&l->ctl, sizeof(Ctl))) != hipSuccess) break;
+        if ((e = hipMemset(l->slots, 0, kHeader)) != hipSuccess) break;
+        if ((e = hipMemset(l->slots + l->slot_stride, 0, kHeader)) != hipSuccess) break;
+        if ((e = hipMemset(l->staging, 0, kHeader)) != hipSuccess) break;
+        if ((e = hipMemset(l->ctl, 0, sizeof(Ctl))) != hipSuccess) break;
+        if ((e = hipStreamCreateWithFlags(&l->side, hipStreamNonBlocking)) != hipSuccess) break;
+        for (auto &ev : l->ev_published)
+            if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) break;
+        if (e != hipSuccess) break;
+        if ((e = hipEventCreateWithFlags(&l->ev_issue, hipEventDisableTiming)) != hipSuccess) break;
+        if ((e = hipEventCreateWithFlags(&l->ev_fetched, hipEventDisableTiming)) != hipSuccess) break;
+        if ((e = hipEventCreateWithFlags(&l->ev_consumed, hipEventDisableTiming)) != hipSuccess) break;
+        if ((e = hipEventCreateWithFlags(&l->ev_factor, hipEventDisableTiming)) != hipSuccess) break;
+        if ((e = hipHostMalloc((void **)&l->host_status, sizeof(int32_t), hipHostMallocMapped)) != hipSuccess) break;
+        *l->host_status = 0;
+        if ((e = hipHostGetDevicePointer((void **)&l->host_status_dev, l->host_status, 0)) != hipSuccess) break;
+        if ((e = hipDeviceSynchronize()) != hipSuccess) break;
+    } while (0);
+    if (e != hipSuccess) {
+        int rc = set_error(DPWA_ERR_HIP, "dpwa_learner_create: %s (slot %zu bytes)", hipGetErrorString(e), l->slot_stride);
+        dpwa_learner_destroy(l);
+        return rc;
+    }
+    {
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        g_live.insert(l);
+    }
+    *out = l;
+    return DPWA_OK;
+}
+
+int dpwa_learner_destroy(dpwa_learner *l)
+{
+    if (!l) return DPWA_OK;
+    {
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        g_live.erase(l);
+        for (dpwa_learner *o : g_live) {   // forget `l` as a reader of anyone's slot
+            std::lock_guard<std::mutex> r(o->readers_mu);
+            for (auto &v : o->readers) v.erase(std::remove(v.begin(), v.end(), l), v.end());
+        }
+    }
+    DeviceGuard dg(l->device);
+    (void)hipDeviceSynchronize();
+    for (auto &kv : l->peers)
+        if (kv.second.kind == 2 && kv.second.base) (void)hipIpcCloseMemHandle(kv.second.base);
+    if (l->side) (void)hipStreamDestroy(l->side);
+    for (auto ev : l->ev_published)
+        if (ev) (void)hipEventDestroy(ev);
+    if (l->ev_issue) (void)hipEventDestroy(l->ev_issue);
+    if (l->ev_fetched) (void)hipEventDestroy(l->ev_fetched);
+    if (l->ev_consumed) (void)hipEventDestroy(l->ev_consumed);
+    if (l->ev_factor) (void)hipEventDestroy(l->ev_factor);
+    if (l->host_status) (void)hipHostFree(l->host_status);
+    if (l->slots) (void)hipFree(l->slots);
+    if (l->staging) (void)hipFree(l->staging);
+    if (l->ctl) (void)hipFree(l->ctl);
+    delete l;
+    return DPWA_OK;
+}
+
+int dpwa_learner_publish(dpwa_learner *l, const void *flat, double loss, const double *loss_dev, dpwa_stream_t stream)
+{
+    if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_publish: NULL argument");
+    DeviceGuard dg(l->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int k = (int)(l->version % 2);   // slot of publish number version+1
+    // Local learners that read slot k (two publishes ago) must have finished.
+    {
+        std::lock_guard<std::mutex> g(l->readers_mu);
+        for (dpwa_learner *r : l->readers[k]) HIP_TRY(hipStreamWaitEvent(s, r->ev_consumed, 0));
+        l->readers[k].clear();
+    }
+    char *slot = l->slots + (size_t)k * l->slot_stride;
+    HIP_TRY(launch_publish(slot, flat, (int64_t)l->payload_bytes, l->n, l->dtype, &l->ctl->clock, loss, loss_dev,
+                           l->version + 1, l->exported, s));
+    HIP_TRY(hipEventRecord(l->ev_published[k], s));
+    l->version++;
+    return DPWA_OK;
+}
+
+int dpwa_learner_version(const dpwa_learner *l, uint64_t *version)
+{
+    if (!l || !version) return set_error(DPWA_ERR_ARG, "dpwa_learner_version: NULL argument");
+    *version = l->version;
+    return DPWA_OK;
+}
+
+int dpwa_learner_attach_local(dpwa_learner *l, int peer_id, dpwa_learner *peer)
+{
+    if (!l || !peer || peer == l) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_local: bad peer");
+    if (peer->n != l->n || peer->dtype != l->dtype)
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_local: peer holds %lld elements of dtype %d, this learner %lld of %d",
+                         (long long)peer->n, peer->dtype, (long long)l->n, l->dtype);
+    if (peer->device != l->device) {
+        DeviceGuard dg(l->device);
+        int can = 0;
+        HIP_TRY(hipDeviceCanAccessPeer(&can, l->device, peer->device));
+        if (!can) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_local: device %d cannot access device %d", l->device, peer->device);
+        hipError_t e = hipDeviceEnablePeerAccess(peer->device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+            return set_error(DPWA_ERR_HIP, "hipDeviceEnablePeerAccess: %s", hipGetErrorString(e));
+        (void)hipGetLastError();
+    }
+    Endpoint ep;
+    ep.kind = 1;
+    ep.local = peer;
+    ep.base = peer->slots;
+    ep.device = peer->device;
+    ep.slot_stride = (int64_t)peer->slot_stride;
+    ep.n = peer->n;
+    ep.dtype = peer->dtype;
+    l->peers[peer_id] = ep;
+    return DPWA_OK;
+}
+
+int dpwa_learner_ipc_handle(dpwa_learner *l, void *handle_out, int64_t handle_len)
+{
+    if (!l || !handle_out || handle_len < (int64_t)sizeof(IpcBlob))
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_ipc_handle: need %zu bytes", sizeof(IpcBlob));
+    DeviceGuard dg(l->device);
+    IpcBlob b;
+    memset(&b, 0, sizeof(b));
+    HIP_TRY(hipIpcGetMemHandle(&b.handle, l->slots));
+    b.magic = kIpcMagic;
+    b.slot_stride = (int64_t)l->slot_stride;
+    b.n = l->n;
+    b.dtype = l->dtype;
+    b.device = l->device;
+    b.pid = (int32_t)getpid();
+    memset(handle_out, 0, (size_t)handle_len);
+    memcpy(handle_out, &b, sizeof(b));
+    l->exported = true;   // from now on publishes release at system scope
+    return DPWA_OK;
+}
+
+int dpwa_learner_attach_ipc(dpwa_learner *l, int peer_id, const void *handle, int64_t handle_len)
+{
+    if (!l || !handle || handle_len < (int64_t)sizeof(IpcBlob)) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_ipc: bad handle");
+    IpcBlob b;
+    memcpy(&b, handle, sizeof(b));
+    if (b.magic != kIpcMagic) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_ipc: not a dpwa handle");
+    if (b.n != l->n || b.dtype != l->dtype)
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_ipc: peer holds %lld elements of dtype %d, this learner %lld of %d",
+                         (long long)b.n, b.dtype, (long long)l->n, l->dtype);
+    DeviceGuard dg(l->device);
+    void *ptr = nullptr;
+    HIP_TRY(hipIpcOpenMemHandle(&ptr, b.handle, hipIpcMemLazyEnablePeerAccess));
+    auto it = l->peers.find(peer_id);
+    if (it != l->peers.end() && it->second.kind == 2 && it->second.base) (void)hipIpcCloseMemHandle(it->second.base);
+    Endpoint ep;
+    ep.kind = 2;
+    ep.base = (char *)ptr;
+    ep.device = b.device;
+    ep.slot_stride = b.slot_stride;
+    ep.n = b.n;
+    ep.dtype = b.dtype;
+    l->peers[peer_id] = ep;
+    return DPWA_OK;
+}
+
+int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int zero_copy, dpwa_stream_t stream)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_fetch: NULL learner");
+    auto it = l->peers.find(peer_id);
+    if (it == l->peers.end()) return set_error(DPWA_ERR_ARG, "dpwa_learner_fetch: peer %d not attached", peer_id);
+    if (peer_version == 0) return set_error(DPWA_ERR_STATE, "dpwa_learner_fetch: peer %d has not published", peer_id);
+    Endpoint &ep = it->second;
+    if (ep.kind == 1 && !is_live(ep.local)) return set_error(DPWA_ERR_STATE, "dpwa_learner_fetch: peer %d was destroyed", peer_id);
+    DeviceGuard dg(l->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int k = (int)((peer_version - 1) % 2);
+    const char *peer_slot = ep.base + (size_t)k * (size_t)ep.slot_stride;
+    if (ep.kind == 1) {
+        // RAW: the peer's publish of that slot must be complete before anyone reads it.
+        HIP_TRY(hipStreamWaitEvent(s, ep.local->ev_published[k], 0));
+        std::lock_guard<std::mutex> g(ep.local->readers_mu);
+        auto &rv = ep.local->readers[k];
+        if (std::find(rv.begin(), rv.end(), l) == rv.end()) rv.push_back(l);
+    }
+    if (zero_copy && ep.kind == 1 && ep.device == l->device) {
+        l->src = peer_slot;             // read in place; stream order covers the rest
+        l->src_copied = false;
+    } else {
+        HIP_TRY(hipEventRecord(l->ev_issue, s));
+        HIP_TRY(hipStreamWaitEvent(l->side, l->ev_issue, 0));
+        // WAR on our own staging buffer: the previous average must have consumed it.
+        HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
+        HIP_TRY(hipMemcpyAsync(l->staging, peer_slot, kHeader + l->payload_bytes, hipMemcpyDefault, l->side));
+        HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
+        l->src = l->staging;
+        l->src_copied = true;
+    }
+    l->src_owner = ep.kind == 1 ? ep.local : nullptr;
+    l->src_slot = k;
+    l->have_fetch = true;
+    return DPWA_OK;
+}
+
+int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dpwa_stream_t stream)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_factor: NULL learner");
+    if (!l->have_fetch) return set_error(DPWA_ERR_STATE, "dpwa_learner_factor: no fetch in flight");
+    DeviceGuard dg(l->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
+    HIP_TRY(launch_factor(l->cfg, &l->ctl->clock, (const dpwa_header *)l->src, loss, loss_dev, &l->ctl->coef,
+                          l->host_status_dev, s));
+    HIP_TRY(hipEventRecord(l->ev_factor, s));
+    l->have_factor = true;
+    return DPWA_OK;
+}
+
+int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream)
+{
+    if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_lerp: NULL argument");
+    if (!l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_lerp: no factor computed for this fetch");
+    DeviceGuard dg(l->device);
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(launch_lerp(l->dtype, flat, l->src + kHeader, l->n, &l->ctl->coef, 0.f, 0.f, s));
+    HIP_TRY(hipEventRecord(l->ev_consumed, s));
+    l->have_fetch = false;
+    l->have_factor = false;
+    l->src = nullptr;
+    return DPWA_OK;
+}
+
+int dpwa_learner_average(dpwa_learner *l, void *flat, double loss, const double *loss_dev, dpwa_stream_t stream)
+{
+    int rc = dpwa_learner_factor(l, loss, loss_dev, stream);
+    if (rc) return rc;
+    return dpwa_learner_lerp(l, flat, stream);
+}
+
+int dpwa_learner_pointers(dpwa_learner *l, double **clock_dev, dpwa_coef **coef_dev, dpwa_header **staging_header_dev,
+                          void **staging_payload_dev)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_pointers: NULL learner");
+    if (clock_dev) *clock_dev = &l->ctl->clock;
+    if (coef_dev) *coef_dev = &l->ctl->coef;
+    if (staging_header_dev) *staging_header_dev = (dpwa_header *)l->staging;
+    if (staging_payload_dev) *staging_payload_dev = l->staging + kHeader;
+    return DPWA_OK;
+}
+
+int dpwa_learner_read_clock(dpwa_learner *l, double *clock)
+{
+    if (!l || !clock) return set_error(DPWA_ERR_ARG, "dpwa_learner_read_clock: NULL argument");
+    DeviceGuard dg(l->device);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(clock, &l->ctl->clock, sizeof(double), hipMemcpyDeviceToHost));
+    return DPWA_OK;
+}
+
+int dpwa_learner_write_clock(dpwa_learner *l, double clock)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_write_clock: NULL learner");
+    DeviceGuard dg(l->device);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&l->ctl->clock, &clock, sizeof(double), hipMemcpyHostToDevice));
+    return DPWA_OK;
+}
+
+int dpwa_learner_read_coef(dpwa_learner *l, dpwa_coef *coef)
+{
+    if (!l || !coef) return set_error(DPWA_ERR_ARG, "dpwa_learner_read_coef: NULL argument");
+    DeviceGuard dg(l->device);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(coef, &l->ctl->coef, sizeof(dpwa_coef), hipMemcpyDeviceToHost));
+    return DPWA_OK;
+}
+
+int dpwa_learner_poll_status(dpwa_learner *l, int *done, int32_t *status)
+{
+    if (!l || !done || !status) return set_error(DPWA_ERR_ARG, "dpwa_learner_poll_status: NULL argument");
+    DeviceGuard dg(l->device);
+    hipError_t e = hipEventQuery(l->ev_factor);
+    if (e != hipSuccess && e != hipErrorNotReady) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(e));
+    *done = e == hipSuccess ? 1 : 0;
+    // Sticky word: the factor kernel writes only non-OK statuses; reading clears it.
+    volatile int32_t *w = l->host_status;
+    *status = *w;
+    if (*status != DPWA_STATUS_OK) *w = DPWA_STATUS_OK;
+    return DPWA_OK;
+}
+
+}  // extern "C"

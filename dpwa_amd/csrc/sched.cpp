@@ -1,0 +1,338 @@
+// sched.cpp -- host-side gossip scheduler: the reference TxThread's peer choice and flow
+// control (dpwa/conn.py:178-317) and DpwaConnection's Bernoulli fetch gate
+// (dpwa/dpwa.py:101-102, 118-123), driven by an MT19937 that reproduces CPython 3.10's
+// `random` module draw for draw (Modules/_randommodule.c + Lib/random.py), so a learner
+// seeded like `random.seed(seed)` picks exactly the peers the reference picks.
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <random>
+#include <vector>
+
+#include "common.hpp"
+
+namespace dpwa {
+
+// CPython's MT19937 (_randommodule.c): init_genrand / init_by_array / genrand_uint32.
+class PyMT {
+public:
+    static constexpr int N = 624;
+    static constexpr int M = 397;
+
+    void seed_by_array(const uint32_t *key, size_t key_len)
+    {
+        uint32_t zero = 0;
+        if (key_len == 0) {  // random.seed(0): keyused = 1, key[0] = 0
+            key = &zero;
+            key_len = 1;
+        }
+        init_genrand(19650218U);
+        size_t i = 1, j = 0;
+        size_t k = (N > key_len ? N : key_len);
+        for (; k; k--) {
+            mt_[i] = (mt_[i] ^ ((mt_[i - 1] ^ (mt_[i - 1] >> 30)) * 1664525U)) + key[j] + (uint32_t)j;
+            i++;
+            j++;
+            if (i >= (size_t)N) {
+                mt_[0] = mt_[N - 1];
+                i = 1;
+            }
+            if (j >= key_len) j = 0;
+        }
+        for (k = N - 1; k; k--) {
+            mt_[i] = (mt_[i] ^ ((mt_[i - 1] ^ (mt_[i - 1] >> 30)) * 1566083941U)) - (uint32_t)i;
+            i++;
+            if (i >= (size_t)N) {
+                mt_[0] = mt_[N - 1];
+                i = 1;
+            }
+        }
+        mt_[0] = 0x80000000U;
+    }
+
+    uint32_t next_u32()
+    {
+        static const uint32_t mag01[2] = {0x0U, 0x9908b0dfU};
+        uint32_t y;
+        if (idx_ >= N) {
+            int kk;
+            for (kk = 0; kk < N - M; kk++) {
+                y = (mt_[kk] & 0x80000000U) | (mt_[kk + 1] & 0x7fffffffU);
+                mt_[kk] = mt_[kk + M] ^ (y >> 1) ^ mag01[y & 0x1U];
+            }
+            for (; kk < N - 1; kk++) {
+                y = (mt_[kk] & 0x80000000U) | (mt_[kk + 1] & 0x7fffffffU);
+                mt_[kk] = mt_[kk + (M - N)] ^ (y >> 1) ^ mag01[y & 0x1U];
+            }
+            y = (mt_[N - 1] & 0x80000000U) | (mt_[0] & 0x7fffffffU);
+            mt_[N - 1] = mt_[M - 1] ^ (y >> 1) ^ mag01[y & 0x1U];
+            idx_ = 0;
+        }
+        y = mt_[idx_++];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680U;
+        y ^= (y << 15) & 0xefc60000U;
+        y ^= (y >> 18);
+        return y;
+    }
+
+    // random.random(): 53-bit double from two words (random_random)
+    double random()
+    {
+        uint32_t a = next_u32() >> 5, b = next_u32() >> 6;
+        return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
+    }
+
+    // random.getrandbits(k), 0 <= k <= 32 (random_getrandbits fast path)
+    uint32_t getrandbits(int k)
+    {
+        if (k == 0) return 0;
+        return next_u32() >> (32 - k);
+    }
+
+    // Random._randbelow_with_getrandbits(n) (Lib/random.py, CPython 3.10), n < 2**32
+    uint64_t randbelow(uint64_t n)
+    {
+        if (n == 0) return 0;
+        int k = 0;
+        for (uint64_t t = n; t; t >>= 1) k++;  // n.bit_length()
+        uint64_t r = getrandbits(k);
+        while (r >= n) r = getrandbits(k);
+        return r;
+    }
+
+    // random.randint(a, b) == randrange(a, b + 1) == a + _randbelow(b - a + 1)
+    int64_t randint(int64_t a, int64_t b) { return a + (int64_t)randbelow((uint64_t)(b - a + 1)); }
+
+private:
+    void init_genrand(uint32_t s)
+    {
+        mt_[0] = s;
+        for (int i = 1; i < N; i++) mt_[i] = (1812433253U * (mt_[i - 1] ^ (mt_[i - 1] >> 30)) + (uint32_t)i);
+        idx_ = N;
+    }
+
+    uint32_t mt_[N];
+    int idx_ = N + 1;
+};
+
+// conn.py:178-181
+constexpr int kFlowMin = 10;
+constexpr int kFlowMax = 1000;
+constexpr int kFlowInc = 10;
+constexpr int kFlowDec = 100;
+
+struct PeerEntry {
+    int score = kFlowMax;      // WorkerConn.flow_control_score (conn.py:190)
+    bool connected = false;    // lazy connection (conn.py:193)
+    bool live = true;          // false after remove_peer (conn.py:215-222)
+};
+
+}  // namespace dpwa
+
+struct dpwa_sched {
+    dpwa::PyMT rng;
+    double fetch_probability = 1.0;
+    std::vector<dpwa::PeerEntry> peers;   // insertion order == YAML order minus self
+    std::vector<int64_t> draw;            // scratch: scores of this pick
+};
+
+using namespace dpwa;
+
+extern "C" {
+
+int dpwa_sched_create(dpwa_sched **out, int n_peers, const uint32_t *seed_key, int key_len,
+                      double fetch_probability)
+{
+    if (!out || n_peers < 0) return set_error(DPWA_ERR_ARG, "dpwa_sched_create: bad arguments");
+    if (key_len > 0 && !seed_key) return set_error(DPWA_ERR_ARG, "dpwa_sched_create: seed_key is NULL");
+    dpwa_sched *s = new (std::nothrow) dpwa_sched();
+    if (!s) return set_error(DPWA_ERR_NOMEM, "dpwa_sched_create: out of memory");
+    if (key_len < 0) {  // random.seed(None): OS entropy
+        std::random_device rd;
+        std::vector<uint32_t> key(PyMT::N);
+        for (auto &k : key) k = rd();
+        s->rng.seed_by_array(key.data(), key.size());
+    } else {
+        s->rng.seed_by_array(seed_key, (size_t)key_len);
+    }
+    s->fetch_probability = fetch_probability;
+    s->peers.assign((size_t)n_peers, PeerEntry());
+    *out = s;
+    return DPWA_OK;
+}
+
+int dpwa_sched_destroy(dpwa_sched *s)
+{
+    delete s;
+    return DPWA_OK;
+}
+
+int dpwa_sched_bernoulli(dpwa_sched *s, int *fetching)
+{
+    if (!s || !fetching) return set_error(DPWA_ERR_ARG, "dpwa_sched_bernoulli: NULL argument");
+    *fetching = s->rng.random() < s->fetch_probability ? 1 : 0;
+    return DPWA_OK;
+}
+
+int dpwa_sched_pick(dpwa_sched *s, int *peer, int *connected)
+{
+    if (!s || !peer || !connected) return set_error(DPWA_ERR_ARG, "dpwa_sched_pick: NULL argument");
+    // conn.py:227-229: one randint(10, 1000) per live peer, in insertion order
+    int64_t best = -1;
+    int n_best = 0;
+    s->draw.assign(s->peers.size(), -1);
+    for (size_t k = 0; k < s->peers.size(); ++k) {
+        if (!s->peers[k].live) continue;
+        int64_t v = s->peers[k].score + s->rng.randint(kFlowMin, kFlowMax);
+        s->draw[k] = v;
+        if (v > best) {
+            best = v;
+            n_best = 1;
+        } else if (v == best) {
+            n_best++;
+        }
+    }
+    if (n_best == 0) {  // conn.py:231-233: no peers
+        *peer = -1;
+        *connected = 0;
+        return DPWA_OK;
+    }
+    // conn.py:238-239: ties in insertion order, chosen by randint(0, k-1) (always drawn)
+    int64_t which = s->rng.randint(0, n_best - 1);
+    for (size_t k = 0; k < s->peers.size(); ++k) {
+        if (s->draw[k] == best) {
+            if (which == 0) {
+                *peer = (int)k;
+                *connected = s->peers[k].connected ? 1 : 0;
+                return DPWA_OK;
+            }
+            which--;
+        }
+    }
+    return set_error(DPWA_ERR_STATE, "dpwa_sched_pick: internal error");
+}
+
+int dpwa_sched_report(dpwa_sched *s, int peer, int outcome, int *round_done, int *got_data)
+{
+    if (!s || !round_done || !got_data || peer < 0 || (size_t)peer >= s->peers.size() || !s->peers[peer].live)
+        return set_error(DPWA_ERR_ARG, "dpwa_sched_report: bad peer");
+    PeerEntry &p = s->peers[peer];
+    *round_done = 0;
+    *got_data = 0;
+    switch (outcome) {
+    case DPWA_CONNECT_OK:
+        p.connected = true;
+        break;
+    case DPWA_CONNECT_REFUSED:   // conn.py:253-256
+        p.score = p.score - kFlowDec > kFlowMin ? p.score - kFlowDec : kFlowMin;
+        *round_done = 1;
+        break;
+    case DPWA_CONNECT_ERROR:     // conn.py:257-260
+        p.live = false;
+        p.connected = false;
+        *round_done = 1;
+        break;
+    case DPWA_REPLY_PAYLOAD:     // conn.py:301-302
+        p.score = p.score + kFlowInc < kFlowMax ? p.score + kFlowInc : kFlowMax;
+        *round_done = 1;
+        *got_data = 1;
+        break;
+    case DPWA_REPLY_EMPTY:
+        p.score = p.score + kFlowInc < kFlowMax ? p.score + kFlowInc : kFlowMax;
+        break;
+    case DPWA_REPLY_TIMEOUT:     // conn.py:304-309
+        p.score = p.score - kFlowDec > kFlowMin ? p.score - kFlowDec : kFlowMin;
+        p.connected = false;
+        break;
+    case DPWA_REPLY_ERROR:       // conn.py:311-313
+        p.live = false;
+        p.connected = false;
+        break;
+    default:
+        return set_error(DPWA_ERR_ARG, "dpwa_sched_report: unknown outcome");
+    }
+    return DPWA_OK;
+}
+
+int dpwa_sched_fetch(dpwa_sched *s, const int32_t *peer_status, int max_attempts, int *peer_out,
+                     int *attempts_out)
+{
+    if (!s || !peer_status || !peer_out || !attempts_out || max_attempts <= 0)
+        return set_error(DPWA_ERR_ARG, "dpwa_sched_fetch: bad arguments");
+    *peer_out = -1;
+    int attempts = 0;
+    while (attempts < max_attempts) {
+        int peer, connected, done = 0, data = 0;
+        int rc = dpwa_sched_pick(s, &peer, &connected);
+        if (rc) return rc;
+        if (peer < 0) break;
+        attempts++;
+        const int32_t st = peer_status[peer];
+        if (!connected) {
+            int c = DPWA_CONNECT_OK;
+            if (st == DPWA_PEER_DOWN) c = DPWA_CONNECT_REFUSED;
+            else if (st == DPWA_PEER_DEAD) c = DPWA_CONNECT_ERROR;
+            if ((rc = dpwa_sched_report(s, peer, c, &done, &data))) return rc;
+            if (done) break;
+        }
+        int r;
+        switch (st) {
+        case DPWA_PEER_READY: r = DPWA_REPLY_PAYLOAD; break;
+        case DPWA_PEER_NO_STATE: r = DPWA_REPLY_EMPTY; break;
+        case DPWA_PEER_SLOW: r = DPWA_REPLY_TIMEOUT; break;
+        default: r = DPWA_REPLY_ERROR; break;   // DOWN while connected (reset) or DEAD
+        }
+        if ((rc = dpwa_sched_report(s, peer, r, &done, &data))) return rc;
+        if (data) {
+            *peer_out = peer;
+            break;
+        }
+        if (done) break;
+    }
+    *attempts_out = attempts;
+    return DPWA_OK;
+}
+
+int dpwa_sched_score(const dpwa_sched *s, int peer, int *score)
+{
+    if (!s || !score || peer < 0 || (size_t)peer >= s->peers.size())
+        return set_error(DPWA_ERR_ARG, "dpwa_sched_score: bad peer");
+    *score = s->peers[peer].live ? s->peers[peer].score : -1;
+    return DPWA_OK;
+}
+
+int dpwa_sched_remove(dpwa_sched *s, int peer)
+{
+    if (!s || peer < 0 || (size_t)peer >= s->peers.size() || !s->peers[peer].live)
+        return set_error(DPWA_ERR_ARG, "dpwa_sched_remove: bad peer");
+    s->peers[peer].live = false;
+    s->peers[peer].connected = false;
+    return DPWA_OK;
+}
+
+int dpwa_sched_n_live(const dpwa_sched *s, int *n_live)
+{
+    if (!s || !n_live) return set_error(DPWA_ERR_ARG, "dpwa_sched_n_live: NULL argument");
+    int n = 0;
+    for (const auto &p : s->peers) n += p.live ? 1 : 0;
+    *n_live = n;
+    return DPWA_OK;
+}
+
+int dpwa_sched_random(dpwa_sched *s, double *out)
+{
+    if (!s || !out) return set_error(DPWA_ERR_ARG, "dpwa_sched_random: NULL argument");
+    *out = s->rng.random();
+    return DPWA_OK;
+}
+
+int dpwa_sched_randint(dpwa_sched *s, int64_t a, int64_t b, int64_t *out)
+{
+    if (!s || !out || b < a || (uint64_t)(b - a) >= 0xffffffffULL)
+        return set_error(DPWA_ERR_ARG, "dpwa_sched_randint: bad range");
+    *out = s->rng.randint(a, b);
+    return DPWA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+"""Python handle of one device-resident learner (dpwa_learner in include/dpwa_hip.h).
+
+A learner owns two snapshot slots, a staging buffer and the device clock/coefficient
+block on its GPU; this class only forwards torch tensors and streams to the C ABI.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+DTYPES = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}
+
+
+def loss_args(loss, device):
+    """(host double, device pointer or None, keep-alive) for a loss given as a number or a
+    device tensor (a device tensor is read by the kernels without a host sync)."""
+    if isinstance(loss, torch.Tensor):
+        if loss.device.type == "cuda":
+            t = loss.detach().to(device=device, dtype=torch.float64).reshape(())
+            return 0.0, ctypes.c_void_p(t.data_ptr()), t
+        return float(loss.item()), None, None
+    return float(loss), None, None
+
+
+class Learner:
+    def __init__(self, device, numel, dtype, interp_cfg):
+        if dtype not in DTYPES:
+            raise TypeError("dpwa averages float32 or bfloat16 parameters, got %s" % dtype)
+        self.device = torch.device(device)
+        self.numel = int(numel)
+        self.dtype = dtype
+        self._h = ctypes.c_void_p()
+        cfg = interp_cfg
+        _lib.call("dpwa_learner_create", ctypes.byref(self._h), self.device.index, self.numel, DTYPES[dtype],
+                  ctypes.byref(cfg))
+        clock, coef, sh, sp = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.call("dpwa_learner_pointers", self._h, ctypes.byref(clock), ctypes.byref(coef), ctypes.byref(sh),
+                  ctypes.byref(sp))
+        self.clock_ptr, self.coef_ptr = clock.value, coef.value
+        self.staging_header_ptr, self.staging_payload_ptr = sh.value, sp.value
+        self._keep = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h is not None and self._h.value and _lib._lib is not None:
+            _lib._lib.dpwa_learner_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, t):
+        if not isinstance(t, torch.Tensor) or t.device != self.device or t.dtype != self.dtype:
+            raise ValueError("expected a %s tensor on %s" % (self.dtype, self.device))
+        if not t.is_contiguous() or t.numel() != self.numel:
+            raise ValueError("expected a contiguous tensor of %d elements, got %s" % (self.numel, tuple(t.shape)))
+
+    def publish(self, flat, loss, stream=None):
+        self._check(flat)
+        h, d, keep = loss_args(loss, self.device)
+        self._keep = keep
+        _lib.call("dpwa_learner_publish", self._h, ctypes.c_void_p(flat.data_ptr()), h, d, _lib.stream_handle(stream))
+
+    @property
+    def version(self):
+        v = ctypes.c_uint64()
+        _lib.call("dpwa_learner_version", self._h, ctypes.byref(v))
+        return v.value
+
+    def attach_local(self, peer_id, other):
+        _lib.call("dpwa_learner_attach_local", self._h, peer_id, other.handle)
+
+    def ipc_handle(self):
+        buf = ctypes.create_string_buffer(_lib.IPC_HANDLE_BYTES)
+        _lib.call("dpwa_learner_ipc_handle", self._h, buf, _lib.IPC_HANDLE_BYTES)
+        return buf.raw
+
+    def attach_ipc(self, peer_id, handle):
+        buf = ctypes.create_string_buffer(bytes(handle), _lib.IPC_HANDLE_BYTES)
+        _lib.call("dpwa_learner_attach_ipc", self._h, peer_id, buf, _lib.IPC_HANDLE_BYTES)
+
+    def fetch(self, peer_id, peer_version, zero_copy=True, stream=None):
+        _lib.call("dpwa_learner_fetch", self._h, peer_id, peer_version, 1 if zero_copy else 0,
+                  _lib.stream_handle(stream))
+
+    def factor(self, loss, stream=None):
+        h, d, keep = loss_args(loss, self.device)
+        self._keep = keep
+        _lib.call("dpwa_learner_factor", self._h, h, d, _lib.stream_handle(stream))
+
+    def lerp(self, flat, stream=None):
+        self._check(flat)
+        _lib.call("dpwa_learner_lerp", self._h, ctypes.c_void_p(flat.data_ptr()), _lib.stream_handle(stream))
+
+    def average(self, flat, loss, stream=None):
+        self._check(flat)
+        h, d, keep = loss_args(loss, self.device)
+        self._keep = keep
+        _lib.call("dpwa_learner_average", self._h, ctypes.c_void_p(flat.data_ptr()), h, d,
+                  _lib.stream_handle(stream))
+
+    def read_clock(self):
+        c = ctypes.c_double()
+        _lib.call("dpwa_learner_read_clock", self._h, ctypes.byref(c))
+        return c.value
+
+    def write_clock(self, value):
+        _lib.call("dpwa_learner_write_clock", self._h, float(value))
+
+    def read_coef(self):
+        c = _lib.Coef()
+        _lib.call("dpwa_learner_read_coef", self._h, ctypes.byref(c))
+        return c
+
+    def poll_status(self):
+        done, st = ctypes.c_int(), ctypes.c_int32()
+        _lib.call("dpwa_learner_poll_status", self._h, ctypes.byref(done), ctypes.byref(st))
+        return bool(done.value), st.value

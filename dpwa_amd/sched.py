@@ -1,0 +1,94 @@
+"""Host-side gossip scheduler: the reference TxThread's peer choice and flow control
+(dpwa/conn.py:178-317) and the Bernoulli gate (dpwa/dpwa.py:101-102), implemented in C++
+(dpwa_amd/csrc/sched.cpp) over a CPython-exact MT19937.
+
+``Scheduler(n_peers, seed, p)`` draws exactly what a reference process that called
+``random.seed(seed)`` draws, in the same order: ``random()`` for the gate, then per pick
+one ``randint(10, 1000)`` per live peer plus the tie-break ``randint(0, k-1)``.
+"""
+import ctypes
+
+from . import _lib
+
+OUTCOMES = {
+    "connect_ok": _lib.CONNECT_OK, "refused": _lib.CONNECT_REFUSED, "connect_error": _lib.CONNECT_ERROR,
+    "payload": _lib.REPLY_PAYLOAD, "empty": _lib.REPLY_EMPTY, "timeout": _lib.REPLY_TIMEOUT,
+    "error": _lib.REPLY_ERROR,
+}
+
+
+def seed_key(seed):
+    """32-bit little-endian words of abs(seed), as CPython's random.seed(int) splits it."""
+    n = abs(int(seed))
+    words = []
+    while n:
+        words.append(n & 0xFFFFFFFF)
+        n >>= 32
+    return words   # [] == seed 0 (key [0])
+
+
+class Scheduler:
+    def __init__(self, n_peers, seed=None, fetch_probability=1.0):
+        self._h = ctypes.c_void_p()
+        if seed is None:
+            _lib.call("dpwa_sched_create", ctypes.byref(self._h), n_peers, None, -1, float(fetch_probability))
+        else:
+            key = seed_key(seed)
+            arr = (ctypes.c_uint32 * max(1, len(key)))(*key)
+            _lib.call("dpwa_sched_create", ctypes.byref(self._h), n_peers, arr, len(key), float(fetch_probability))
+        self.n_peers = n_peers
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and h.value and _lib._lib is not None:
+            _lib._lib.dpwa_sched_destroy(h)
+            self._h = None
+
+    def bernoulli(self):
+        out = ctypes.c_int()
+        _lib.call("dpwa_sched_bernoulli", self._h, ctypes.byref(out))
+        return bool(out.value)
+
+    def pick(self):
+        """Returns (peer index or -1, connected)."""
+        peer, conn = ctypes.c_int(), ctypes.c_int()
+        _lib.call("dpwa_sched_pick", self._h, ctypes.byref(peer), ctypes.byref(conn))
+        return peer.value, bool(conn.value)
+
+    def report(self, peer, outcome):
+        """Returns (round_done, got_data)."""
+        if isinstance(outcome, str):
+            outcome = OUTCOMES[outcome]
+        done, data = ctypes.c_int(), ctypes.c_int()
+        _lib.call("dpwa_sched_report", self._h, peer, outcome, ctypes.byref(done), ctypes.byref(data))
+        return bool(done.value), bool(data.value)
+
+    def fetch(self, peer_status, max_attempts=1000):
+        """Whole TxThread fetch loop against a static per-peer status list; returns (peer, attempts)."""
+        arr = (ctypes.c_int32 * max(1, len(peer_status)))(*peer_status)
+        peer, att = ctypes.c_int(), ctypes.c_int()
+        _lib.call("dpwa_sched_fetch", self._h, arr, max_attempts, ctypes.byref(peer), ctypes.byref(att))
+        return peer.value, att.value
+
+    def score(self, peer):
+        out = ctypes.c_int()
+        _lib.call("dpwa_sched_score", self._h, peer, ctypes.byref(out))
+        return None if out.value < 0 else out.value
+
+    def scores(self):
+        return [self.score(k) for k in range(self.n_peers)]
+
+    def n_live(self):
+        out = ctypes.c_int()
+        _lib.call("dpwa_sched_n_live", self._h, ctypes.byref(out))
+        return out.value
+
+    def random(self):
+        out = ctypes.c_double()
+        _lib.call("dpwa_sched_random", self._h, ctypes.byref(out))
+        return out.value
+
+    def randint(self, a, b):
+        out = ctypes.c_int64()
+        _lib.call("dpwa_sched_randint", self._h, a, b, ctypes.byref(out))
+        return out.value

@@ -1,0 +1,225 @@
+/*
+ * dpwa_hip.h -- C ABI of libdpwa_hip.so, the MI355X-native pairwise-averaging hot path.
+ *
+ * The reference (zenghanfu/dpwa) is pure Python; its hot path is the adapter/connection
+ * seam below, which this library replaces.  Every entry point names the reference
+ * interface it stands in for.  A maintainer binds it with ctypes;
+ * dpwa_amd/_lib.py is that binding.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Device pointers are HIP device addresses on the
+ *    learner's GPU; `dpwa_stream_t` is a hipStream_t (NULL = the legacy default stream).
+ *  - Every function returns DPWA_OK (0) or a negative DPWA_ERR_*; the message of the
+ *    last failure on the calling thread is available from dpwa_last_error().
+ *  - The library never allocates or frees caller memory.  Learner-owned snapshot and
+ *    staging buffers are allocated at dpwa_learner_create() with hipMalloc.
+ *  - No host synchronisation happens inside publish / fetch / average: the factor is
+ *    computed on the device from the (clock, loss) state and handed to the lerp through
+ *    device memory (dpwa_coef), so a whole round can be enqueued without a sync.
+ *  - There is no CPU fallback: without a HIP device the compute entry points fail.
+ */
+#ifndef DPWA_HIP_H
+#define DPWA_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPWA_ABI_VERSION 1
+
+#define DPWA_OK 0
+#define DPWA_ERR_ARG (-1)     /* bad argument (API misuse)                          */
+#define DPWA_ERR_HIP (-2)     /* a HIP runtime call failed                          */
+#define DPWA_ERR_STATE (-3)   /* call out of order (e.g. average without a fetch)   */
+#define DPWA_ERR_NOMEM (-4)
+
+/* element types of the flat parameter buffer */
+#define DPWA_F32 0            /* the reference's only type: TYPE_CONVERSION, pytorch.py:11-14 */
+#define DPWA_BF16 1           /* extension: torch-eager bf16 rounding, no reference path      */
+
+/* interpolation methods: INTERPOLATION_METHODS, dpwa/dpwa.py:11-15 */
+#define DPWA_INTERP_CONSTANT 0   /* interpolation.py:8-15  factor = value                       */
+#define DPWA_INTERP_CLOCK 1      /* interpolation.py:18-24 factor = peer_clock/(clock+peer_clock) */
+#define DPWA_INTERP_LOSS 2       /* interpolation.py:27-33 factor = loss/(loss+peer_loss)         */
+
+/* status written into dpwa_coef.status by the factor kernel */
+#define DPWA_STATUS_OK 0
+#define DPWA_STATUS_ZERO_DIVISION 1   /* the reference raises ZeroDivisionError (dpwa.py:143) */
+
+typedef void *dpwa_stream_t;
+
+/* The published `state` of one learner (dpwa.py:115 `{'clock', 'loss'}`), stored as the
+ * first 256 bytes of every snapshot slot so that state and parameters travel together
+ * exactly as RxThread sends them together (conn.py:110). */
+typedef struct dpwa_header {
+    double clock;        /* publisher's clock after `clock += 1` (dpwa.py:112)           */
+    double loss;         /* loss given to update_send (dpwa.py:115)                      */
+    uint64_t version;    /* publishes so far; 0 = never published (have_state, conn.py:60) */
+    int64_t n;           /* payload elements                                              */
+    int32_t dtype;       /* DPWA_F32 / DPWA_BF16                                          */
+    int32_t reserved0;
+    uint8_t pad[216];
+} dpwa_header;
+
+/* Averaging coefficients, produced on the device by the factor kernel (dpwa.py:143-150)
+ * and consumed by the lerp (pytorch.py:68). */
+typedef struct dpwa_coef {
+    double factor;       /* interpolation factor after divergence scaling (dpwa.py:143-147) */
+    double new_clock;    /* factor*peer_clock + (1-factor)*clock (dpwa.py:150)              */
+    float a;             /* f32(factor)        -- torch casts the scalar to fp32            */
+    float b;             /* f32(1.0 - factor)  -- `1 - factor` is a Python double           */
+    int32_t status;      /* DPWA_STATUS_*; non-zero makes the lerp a no-op                  */
+    int32_t reserved;
+} dpwa_coef;
+
+/* Interpolation configuration (DpwaConfiguration.get_interpolation / get_divergence_threshold,
+ * dpwa.py:40-51). */
+typedef struct dpwa_interp {
+    int32_t method;               /* DPWA_INTERP_*                                 */
+    int32_t reserved;
+    double value;                 /* constant value (ConstantInterpolation)        */
+    double divergence_threshold;  /* 0 disables (README.md:62)                     */
+} dpwa_interp;
+
+const char *dpwa_last_error(void);
+int dpwa_abi_version(void);
+
+/* ------------------------------------------------------------------------------------
+ * Stateless kernels (the fused replacements of the ATen mul/mul/add behind pytorch.py:68)
+ * ------------------------------------------------------------------------------------ */
+
+/* param[i] = f32(f32(a*peer[i]) + f32(b*param[i])) with (a, b) read from coef_dev on the
+ * device (no host sync).  Replaces the per-tensor loop dpwa/adapters/pytorch.py:66-68 with
+ * one launch over the flat buffer.  In place; param and peer may not overlap. */
+int dpwa_lerp_f32(float *param, const float *peer, int64_t n, const dpwa_coef *coef_dev,
+                  dpwa_stream_t stream);
+/* bf16 form: bf16(bf16(a*peer) + bf16(b*param)), RNE (torch-eager bf16). */
+int dpwa_lerp_bf16(uint16_t *param, const uint16_t *peer, int64_t n, const dpwa_coef *coef_dev,
+                   dpwa_stream_t stream);
+/* Same kernels with the factor given by the host, as pytorch.py:68 receives it. */
+int dpwa_lerp_f32_host(float *param, const float *peer, int64_t n, double factor, dpwa_stream_t stream);
+int dpwa_lerp_bf16_host(uint16_t *param, const uint16_t *peer, int64_t n, double factor,
+                        dpwa_stream_t stream);
+
+/* Factor + clock on the device (dpwa.py:139-155 + interpolation.py): reads *clock_dev and the
+ * peer's header, writes *coef_dev and, unless the status is an error, *clock_dev = new_clock.
+ * `loss` is used when loss_dev is NULL, else *loss_dev (a device float64). */
+int dpwa_factor(const dpwa_interp *cfg, double *clock_dev, const dpwa_header *peer_header_dev, double loss,
+                const double *loss_dev, dpwa_coef *coef_dev, dpwa_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Learner runtime: one per gossip node.  Owns two snapshot slots (double-buffered
+ * RxThread.set_current_state, conn.py:73-79), a staging buffer (the fetched
+ * TxThread.peer_payload, conn.py:298), the device clock and the coefficient block.
+ * ------------------------------------------------------------------------------------ */
+typedef struct dpwa_learner dpwa_learner;
+
+int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype, const dpwa_interp *cfg);
+int dpwa_learner_destroy(dpwa_learner *l);
+
+/* update_send's publish half (dpwa.py:111-116 + pytorch.py:49-53): clock += 1 on the device,
+ * copy the n-element flat buffer into the next snapshot slot with header {clock, loss,
+ * version}.  Stream-ordered after prior work on `stream`. */
+int dpwa_learner_publish(dpwa_learner *l, const void *flat, double loss, const double *loss_dev,
+                         dpwa_stream_t stream);
+/* Number of publishes so far (host counter, no sync). */
+int dpwa_learner_version(const dpwa_learner *l, uint64_t *version);
+
+/* Peers.  `peer_id` is the caller's index of that peer (e.g. its node index).
+ * attach_local: the peer learner lives in this process (any device).
+ * ipc_handle / attach_ipc: the peer lives in another process; its snapshot allocation is
+ * exported with hipIpcGetMemHandle (handle_len = DPWA_IPC_HANDLE_BYTES). */
+#define DPWA_IPC_HANDLE_BYTES 128
+int dpwa_learner_attach_local(dpwa_learner *l, int peer_id, dpwa_learner *peer);
+int dpwa_learner_ipc_handle(dpwa_learner *l, void *handle_out, int64_t handle_len);
+int dpwa_learner_attach_ipc(dpwa_learner *l, int peer_id, const void *handle, int64_t handle_len);
+
+/* The fetch (TxThread request -> reply, conn.py:297-298): pull peer `peer_id`'s snapshot of
+ * publish number `peer_version` (1-based) into this learner's staging buffer on the
+ * learner's side stream, after all work already enqueued on `stream`.  For a peer on the
+ * same device with zero_copy != 0 no bytes move: the average reads the peer's slot in place.
+ * Slot reuse is protected for local peers by events; for IPC peers by the caller's
+ * lock-step barrier (a slot is rewritten two publishes later). */
+int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int zero_copy,
+                       dpwa_stream_t stream);
+
+/* update_wait's averaging (dpwa.py:133-155 + pytorch.py:64-68): make `stream` wait for the
+ * fetch, compute factor/clock on the device, then lerp the n-element flat buffer in place. */
+int dpwa_learner_average(dpwa_learner *l, void *flat, double loss, const double *loss_dev,
+                         dpwa_stream_t stream);
+
+/* Split form of dpwa_learner_average for the DpwaConnection / adapter seam:
+ * factor only (update_wait's return value), then lerp with the learner's coefficients. */
+int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dpwa_stream_t stream);
+int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream);
+
+/* Device pointers of the learner's blocks (for zero-copy views from the host side). */
+int dpwa_learner_pointers(dpwa_learner *l, double **clock_dev, dpwa_coef **coef_dev,
+                          dpwa_header **staging_header_dev, void **staging_payload_dev);
+/* Synchronous reads for inspection (these DO synchronise with the learner's device). */
+int dpwa_learner_read_clock(dpwa_learner *l, double *clock);
+int dpwa_learner_write_clock(dpwa_learner *l, double clock);
+int dpwa_learner_read_coef(dpwa_learner *l, dpwa_coef *coef);
+/* Non-blocking status check: *done = 1 when the last factor computation has completed;
+ * *status = the first non-OK DPWA_STATUS_* any factor computation reported since the last
+ * poll (a sticky pinned host word, cleared by this call), else DPWA_STATUS_OK. */
+int dpwa_learner_poll_status(dpwa_learner *l, int *done, int32_t *status);
+
+/* ------------------------------------------------------------------------------------
+ * Host scheduler: TxThread's peer choice and flow control (conn.py:178-317) plus the
+ * Bernoulli fetch gate (dpwa.py:101-102), over a CPython-exact MT19937 so that a learner
+ * seeded like `random.seed(seed)` draws the reference's exact sequence.
+ * ------------------------------------------------------------------------------------ */
+typedef struct dpwa_sched dpwa_sched;
+
+/* outcomes reported back for a picked peer (conn.py:245-313) */
+#define DPWA_CONNECT_OK 0        /* lazy connect succeeded                       conn.py:247-251 */
+#define DPWA_CONNECT_REFUSED 1   /* ConnectionRefusedError: score -= 100, round ends  conn.py:253-256 */
+#define DPWA_CONNECT_ERROR 2     /* other error: peer removed, round ends        conn.py:257-260 */
+#define DPWA_REPLY_PAYLOAD 3     /* reply with data: score += 10, round ends      conn.py:301-302 */
+#define DPWA_REPLY_EMPTY 4       /* peer had no state: score += 10, pick again    conn.py:301-302 */
+#define DPWA_REPLY_TIMEOUT 5     /* socket.timeout: score -= 100, reconnect, again conn.py:304-309 */
+#define DPWA_REPLY_ERROR 6       /* other error: peer removed, pick again         conn.py:311-313 */
+
+/* static peer status for dpwa_sched_fetch (what the transport knows about each peer) */
+#define DPWA_PEER_READY 0        /* up and has published                          */
+#define DPWA_PEER_NO_STATE 1     /* up, nothing published yet -> empty reply       */
+#define DPWA_PEER_DOWN 2         /* not up: refused when not connected, error if it was */
+#define DPWA_PEER_SLOW 3         /* times out                                     */
+#define DPWA_PEER_DEAD 4         /* unrecoverable: removed                        */
+
+/* seed_key: 32-bit little-endian words of abs(seed) as CPython's random.seed(int) splits
+ * it (key_len 0 means seed 0); key_len < 0 seeds from OS entropy (random.seed(None)). */
+int dpwa_sched_create(dpwa_sched **out, int n_peers, const uint32_t *seed_key, int key_len,
+                      double fetch_probability);
+int dpwa_sched_destroy(dpwa_sched *s);
+/* dpwa.py:101-102 / 118: *fetching = random() < fetch_probability */
+int dpwa_sched_bernoulli(dpwa_sched *s, int *fetching);
+/* conn.py:224-240: score each live peer + randint(10,1000) in insertion order, argmax,
+ * tie-break randint(0, k-1).  *peer = -1 when no peers remain. *connected tells whether
+ * the caller must report a CONNECT_* outcome before the REPLY_* one. */
+int dpwa_sched_pick(dpwa_sched *s, int *peer, int *connected);
+/* Applies an outcome for the picked peer; *round_done / *got_data say how the fetch loop
+ * (conn.py:286-313) continues. */
+int dpwa_sched_report(dpwa_sched *s, int peer, int outcome, int *round_done, int *got_data);
+/* The whole fetch loop for one queue item (conn.py:277-315) against a static per-peer
+ * status array; stops after max_attempts picks (the reference would spin forever when
+ * every peer times out).  *peer_out = the peer that delivered data, or -1. */
+int dpwa_sched_fetch(dpwa_sched *s, const int32_t *peer_status, int max_attempts, int *peer_out,
+                     int *attempts_out);
+/* flow_control_score of a peer (conn.py:190); -1 once removed */
+int dpwa_sched_score(const dpwa_sched *s, int peer, int *score);
+/* DpwaConnection.remove_peer (dpwa.py:98-99 -> conn.py:215-222): drop a peer for good. */
+int dpwa_sched_remove(dpwa_sched *s, int peer);
+int dpwa_sched_n_live(const dpwa_sched *s, int *n_live);
+/* raw CPython-equivalent draws, for tests: random.random(), random.randint(a, b) */
+int dpwa_sched_random(dpwa_sched *s, double *out);
+int dpwa_sched_randint(dpwa_sched *s, int64_t a, int64_t b, int64_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DPWA_HIP_H */
