@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""bench.py -- gossip-round throughput of the MI355X pairwise-averaging hot path.
+
+A *step* is one lock-step gossip round of every learner in the job through the drop-in
+API: ``update_send`` (device clock += 1, snapshot publish, Bernoulli gate, peer choice,
+pull) then ``update_wait`` + ``average`` (device factor/clock, fused in-place lerp).
+
+Workload (BASELINE.json configs[1]): a synthetic 11,173,962-element fp32 parameter
+vector (ResNet-18 size) per learner, N(0,1) data, constant interpolation 0.5,
+fetch_probability 1.
+  * ``--gpus 1``: two learners co-resident on cuda:0 (the minimal non-degenerate gossip:
+    each averages with the other's snapshot, read in place from HBM).
+  * ``--gpus N`` (torchrun): one learner per GPU; peers' snapshots are mapped with
+    hipIpcOpenMemHandle and pulled over xGMI on each learner's side stream; every round is
+    lock-step behind an RCCL barrier.  Per-GPU work is fixed -> "scaling": "weak".
+
+``value`` = algorithmic averaged bytes (3 * numel * sizeof(dtype) per completed
+averaging) summed over all learners / the max-over-ranks wall time of the
+K timed steps.  ``roofline`` prices the lerp kernel alone from HIP events recorded around
+every lerp launch on the stream it runs on.  ``cpu_baseline`` times the C oracle's
+restatement of the same round (publish copy + averaging) on one host core.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+RESNET18_NUMEL = 11_173_962    # examples/pytorch-cifar/models/resnet.py ResNet18
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--numel", type=int, default=RESNET18_NUMEL)
+    ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32")
+    ap.add_argument("--interpolation", choices=["constant", "clock", "loss"], default="constant")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+                    help="PMC traffic summary (rocprofv3 FETCH_SIZE/WRITE_SIZE passes) to report")
+    return ap.parse_args()
+
+
+def write_config(path, names, interp):
+    lines = ["- nodes:"] + ["  - {name: %s, host: 127.0.0.1, port: %d}" % (n, 45000 + i)
+                            for i, n in enumerate(names)]
+    lines += ["- fetch_probability: 1", "- timeout_ms: 2500", "- interpolation: %s" % interp,
+              "- divergence_threshold: 0", "- constant: { value: 0.5 }", "- clock: 0", "- loss: 0"]
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def cpu_baseline(numel, seconds):
+    """The C oracle (oracle/dpwa_oracle.c) running the same round on one host core:
+    publish copy (2*N*4 bytes) + averaging (3*N*4 bytes); reported like `value`."""
+    from oracle import lerp as olerp
+    lib = olerp.clib()
+    rng = np.random.default_rng(0)
+    param = rng.standard_normal(numel).astype(np.float32)
+    peer = rng.standard_normal(numel).astype(np.float32)
+    slot = np.empty_like(param)
+    rounds = 0
+    t0 = time.perf_counter()
+    while True:
+        lib.dpwa_oracle_publish(slot.ctypes.data, param.ctypes.data, param.nbytes)
+        lib.dpwa_oracle_lerp_f32(param.ctypes.data, peer.ctypes.data, numel, 0.5)
+        rounds += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": rounds * 3 * numel * 4 / el / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "%d rounds of publish-copy + fp32 lerp over %d elements (C oracle, -O3, 1 thread, %.1f s)"
+                      % (rounds, numel, el),
+            "ms_per_round": 1e3 * el / rounds}
+
+
+def cold_kernel(numel, dtype, device, launches=40):
+    """Lerp alone over rotating buffers (> 512 MiB between reuses: no Infinity-Cache hits)."""
+    from dpwa_amd import _lib
+    esize = 4 if dtype == torch.float32 else 2
+    pairs = max(4, int(np.ceil(1.2e9 / (2 * numel * esize))))
+    bufs = [(torch.randn(numel, device=device).to(dtype), torch.randn(numel, device=device).to(dtype))
+            for _ in range(pairs)]
+    fn = "dpwa_lerp_f32_host" if dtype == torch.float32 else "dpwa_lerp_bf16_host"
+    s = _lib.stream_handle(None)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    for i in range(launches + pairs):
+        p, q = bufs[i % pairs]
+        j = i - pairs
+        if j >= 0:
+            evs[j][0].record()
+        _lib.call(fn, ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(q.data_ptr()), numel, 0.5, s)
+        if j >= 0:
+            evs[j][1].record()
+    torch.cuda.synchronize()
+    ms = np.array([a.elapsed_time(b) for a, b in evs])
+    del bufs
+    torch.cuda.empty_cache()
+    return 3 * numel * esize / (ms.mean() * 1e-3) / 1e9, float(ms.mean() * 1e3), pairs
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d (launch N>1 with torch.distributed.run)" % (args.gpus, world))
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from dpwa_amd import DpwaConnection
+    from dpwa_amd.group import LocalGroup
+
+    dtype = torch.float32 if args.dtype == "f32" else torch.bfloat16
+    esize = 4 if dtype == torch.float32 else 2
+    tmp = tempfile.mkdtemp(prefix="dpwa_bench_")
+    cfg = os.path.join(tmp, "bench.yaml")
+    if world == 1:
+        names = ["w1", "w2"]
+        write_config(cfg, names, args.interpolation)
+        group = LocalGroup()
+        mine = [(names[0], 0), (names[1], 1)]
+    else:
+        names = ["w%d" % (r + 1) for r in range(world)]
+        write_config(cfg, names, args.interpolation)
+        group = None
+        mine = [(names[rank], rank)]
+    learners = []
+    for name, seed in mine:
+        g = torch.Generator(device=device).manual_seed(seed)
+        flat = torch.randn(args.numel, device=device, generator=g, dtype=torch.float32).to(dtype)
+        conn = DpwaConnection(name, cfg, seed=1000 + seed, group=group)
+        learners.append((conn, flat))
+
+    stream = torch.cuda.current_stream(device)
+    loss = 1.0
+    lerp_events = []
+
+    def step(timed):
+        done = 0
+        for conn, flat in learners:
+            conn.update_send(flat, loss)
+        for conn, flat in learners:
+            payload, _ = conn.update_wait(loss)
+            if payload is not None:
+                if timed:
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(stream)
+                    conn.average(flat, stream)
+                    b.record(stream)
+                    lerp_events.append((a, b))
+                else:
+                    conn.average(flat, stream)
+                done += 1
+        return done
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    averaged = 0
+    for _ in range(args.steps):
+        averaged += step(True)
+    torch.cuda.synchronize()
+    host_enqueue_done = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    lerp_ms = np.array([a.elapsed_time(b) for a, b in lerp_events]) if lerp_events else np.array([np.nan])
+    stats = torch.tensor([elapsed, float(averaged), float(len(learners) * args.steps)], dtype=torch.float64,
+                         device=device)
+    if world > 1:
+        tmax = stats[0:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        sums = stats[1:].clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax.item())
+        averaged, rounds = float(sums[0].item()), float(sums[1].item())
+    else:
+        averaged, rounds = float(averaged), float(len(learners) * args.steps)
+
+    unit_bytes = 3 * args.numel * esize
+    if rank == 0:
+        value = averaged * unit_bytes / elapsed / 1e9
+        lerp_us = float(np.nanmean(lerp_ms) * 1e3)
+        achieved = unit_bytes / (lerp_us * 1e-6) / 1e9
+        traffic = None
+        traffic_src = None
+        if os.path.exists(args.traffic):
+            with open(args.traffic) as f:
+                tr = json.load(f)
+            if tr.get("numel") == args.numel and tr.get("dtype") == args.dtype and tr.get("gpus", 1) == world:
+                traffic = tr.get("hbm_bytes_per_launch")
+                traffic_src = os.path.relpath(args.traffic, ROOT)
+        out = {
+            "metric": "pairwise-average GB/s (% HBM peak) + gossip rounds/s",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if dtype == torch.float32 else "bf16",
+            "data": "synthetic N(0,1) flat parameter vectors (no dataset needed)",
+            "config": {
+                "workload": ("configs[1]: synthetic %d-element %s vector per learner (ResNet-18 size), "
+                             "%s interpolation, fetch_probability 1, lock-step gossip rounds"
+                             % (args.numel, args.dtype, args.interpolation)),
+                "learners": int(rounds / args.steps),
+                "learners_per_gpu": len(learners),
+                "numel": args.numel,
+                "transport": "in-place HBM read (co-resident peer)" if world == 1 else
+                             "hipIpc-mapped slot pulled over xGMI on a side stream",
+                "parallelism": "gossip x%d" % int(rounds / args.steps),
+            },
+            "gossip_rounds_per_s": round(rounds / elapsed, 1),
+            "gossip_rounds_per_s_per_learner": round(rounds / elapsed / (rounds / args.steps), 1),
+            "averagings": int(averaged),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "dpwa::k_lerp_%s" % args.dtype,
+                "bytes_per_launch": unit_bytes,
+                "avg_launch_us": round(lerp_us, 2),
+                "launches_timed": len(lerp_events),
+                "traffic_source": traffic_src,
+            },
+            "host_enqueue_ms_per_step": round(1e3 * (host_enqueue_done - t0) / args.steps, 4),
+        }
+        if world == 1 and not args.no_cold:
+            gbs, us, pairs = cold_kernel(args.numel, dtype, device)
+            out["roofline"]["cold_cache"] = {"achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                             "avg_launch_us": round(us, 2), "rotating_buffer_pairs": pairs}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.numel, args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    for conn, _ in learners:
+        conn.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,68 @@
+"""Worker process for the multi-process gossip tests (spawned; one rank per process).
+
+Each rank runs one DpwaConnection on its node; the group is chosen exactly as in
+production (torch.distributed initialised, world size == number of nodes -> DistGroup).
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def inputs(world, n, T, seed=0):
+    rng = np.random.default_rng(seed)
+    init = rng.standard_normal((world, n)).astype(np.float32)
+    deltas = (0.01 * rng.standard_normal((T, world, n))).astype(np.float32)
+    send = [[float(2 * np.exp(-r / 4) + 0.05 * rng.random()) for _ in range(world)] for r in range(T)]
+    wait = [[float(2 * np.exp(-(r + .5) / 4) + 0.05 * rng.random()) for _ in range(world)] for r in range(T)]
+    return init, deltas, send, wait
+
+
+def write_cfg(path, names, fp, interp, thr):
+    lines = ["- nodes:"] + ["  - {name: %s, host: 127.0.0.1, port: %d}" % (nm, 45500 + i)
+                            for i, nm in enumerate(names)]
+    lines += ["- fetch_probability: %r" % fp, "- timeout_ms: 2500", "- interpolation: %s" % interp,
+              "- divergence_threshold: %r" % thr, "- constant: { value: 0.5 }", "- clock: 0", "- loss: 0"]
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of_rank):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    dev = torch.device("cuda", device_of_rank(rank) if callable(device_of_rank) else device_of_rank)
+    torch.cuda.set_device(dev)
+    from dpwa_amd import DpwaConnection
+    from dpwa_amd.group import DistGroup
+    init, deltas, send, wait = inputs(world, n, T)
+    names = ["r%d" % i for i in range(world)]
+    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank)
+    assert isinstance(conn._group, DistGroup)
+    flat = torch.from_numpy(init[rank]).to(dev)
+    params = np.zeros((T, n), np.float32)
+    clocks = np.zeros(T)
+    peers = []
+    for r in range(T):
+        conn.update_send(flat, send[r][rank])
+        flat.add_(torch.from_numpy(deltas[r, rank]).to(dev))
+        payload, factor = conn.update_wait(wait[r][rank])
+        if payload is not None:
+            conn.average(flat)
+            peers.append(payload.peer)
+        else:
+            peers.append(None)
+        params[r] = flat.cpu().numpy()
+        clocks[r] = conn.clock
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=params, clocks=clocks,
+             peers=np.array([p or "" for p in peers]))
+    torch.cuda.synchronize()
+    dist.barrier()
+    conn.close()
+    dist.destroy_process_group()

@@ -1,0 +1,200 @@
+"""End-to-end parity of the drop-in API on one GPU: G learners in one process
+(LocalGroup) replay the reference's own lock-step gossip trajectories
+(tests/golden/gossip.*, produced by running the reference adapter + connection +
+TxThread), bit for bit: parameters, clocks, factors and peer choices."""
+import numpy as np
+import pytest
+import torch
+
+from dpwa_amd import DpwaConnection, DpwaPyTorchAdapter
+from dpwa_amd.group import LocalGroup
+from oracle import gossip as ogossip
+from oracle import lerp as olerp
+from tests.helpers import load_json, load_npz
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+class Net(torch.nn.Module):
+    def __init__(self, shapes, dtype=torch.float32):
+        super().__init__()
+        for i, s in enumerate(shapes):
+            self.register_parameter("p%d" % i, torch.nn.Parameter(torch.zeros(s, dtype=dtype)))
+
+
+def write_cfg(path, names, fp, interp, thr, value):
+    lines = ["---", "- nodes:"]
+    lines += ["  - {name: %s, host: localhost, port: %d}" % (n, 46000 + i) for i, n in enumerate(names)]
+    lines += ["- fetch_probability: %r" % fp, "- timeout_ms: 2500", "- interpolation: %s" % interp,
+              "- divergence_threshold: %r" % thr, "- constant: { value: %r }" % (value if value is not None else 0.5),
+              "- clock: 0", "- loss: 0"]
+    path.write_text("\n".join(lines) + "\n")
+
+
+def load_flat(net, flat):
+    off = 0
+    with torch.no_grad():
+        for _, p in net.named_parameters():
+            n = p.numel()
+            p.data.copy_(torch.from_numpy(flat[off:off + n]).view(p.shape))
+            off += n
+
+
+def flat_params(net):
+    return np.concatenate([p.detach().cpu().numpy().reshape(-1) for _, p in net.named_parameters()])
+
+
+def run_gossip(case, z, tmp_path, dtype=torch.float32):
+    names = case["names"]
+    G = case["G"]
+    shapes = [tuple(s) for s in load_json("gossip.json")["shapes"]]
+    cfg = tmp_path / ("%s.yaml" % case["key"])
+    write_cfg(cfg, names, case["fetch_probability"], case["interpolation"], case["divergence_threshold"],
+              case["value"])
+    init, deltas = z[case["key"] + "_init"], z[case["key"] + "_deltas"]
+    group = LocalGroup()
+    nets, adapters = [], []
+    for g in range(G):
+        net = Net(shapes).to(DEV)
+        load_flat(net, init[g])
+        nets.append(net)
+        adapters.append(DpwaPyTorchAdapter(net, names[g], str(cfg), seed=case["seeds"][g], group=group))
+    T = deltas.shape[0]
+    out = {"params": np.zeros((T, G, init.shape[1]), np.float32), "clocks": np.zeros((T, G)),
+           "factors": np.zeros((T, G)), "picks": [[None] * G for _ in range(T)], "fetching": np.zeros((T, G), bool)}
+    for r in range(T):
+        for g in range(G):
+            adapters[g].update_send(case["send_loss"][r][g])
+            out["fetching"][r, g] = adapters[g].connection.fetching
+        for g in range(G):
+            with torch.no_grad():
+                off = 0
+                for _, p in nets[g].named_parameters():
+                    k = p.numel()
+                    p.data.add_(torch.from_numpy(deltas[r, g, off:off + k]).to(DEV).view(p.shape))
+                    off += k
+        for g in range(G):
+            c = adapters[g].connection
+            adapters[g].update_wait(case["wait_loss"][r][g])
+            fetched = c._fetch_peer >= 0 and out["fetching"][r, g]
+            out["picks"][r][g] = [c.peers[c._fetch_peer].name] if fetched else []
+            out["factors"][r, g] = float(c._learner.read_coef().factor) if fetched else 0.0
+            out["clocks"][r, g] = c.clock
+            out["params"][r, g] = flat_params(nets[g])
+    for a in adapters:
+        a.connection.close()
+    return out
+
+
+def test_gossip_matches_reference_trajectories(tmp_path):
+    meta = load_json("gossip.json")
+    z = load_npz("gossip.npz")
+    for case in meta["cases"]:
+        k = case["key"]
+        got = run_gossip(case, z, tmp_path)
+        assert np.array_equal(got["fetching"], z[k + "_fetching"]), k
+        assert got["picks"] == case["picks"], k
+        assert np.array_equal(got["factors"], z[k + "_factors"]), k
+        assert np.array_equal(got["clocks"], z[k + "_clocks"]), k
+        assert olerp.bits_equal(got["params"], z[k + "_params"]), k
+
+
+def test_gossip_longer_run_matches_oracle(tmp_path):
+    """A longer synthetic run (loss interpolation, divergence threshold, p<1) against the
+    oracle's lock-step simulation."""
+    rng = np.random.default_rng(9)
+    G, n, T = 5, 5000, 30
+    names = ["n%d" % g for g in range(G)]
+    init = rng.standard_normal((G, n)).astype(np.float32)
+    deltas = (0.01 * rng.standard_normal((T, G, n))).astype(np.float32)
+    send = [[float(2 * np.exp(-r / 8) + 0.05 * rng.random()) for _ in range(G)] for r in range(T)]
+    wait = [[float(2 * np.exp(-(r + .5) / 8) + 0.05 * rng.random()) for _ in range(G)] for r in range(T)]
+    seeds = [77 + g for g in range(G)]
+    exp = ogossip.simulate(names, init, deltas, send, wait, "loss", None, 0.5, 0.8, seeds)
+    cfg = tmp_path / "long.yaml"
+    write_cfg(cfg, names, 0.8, "loss", 0.5, None)
+    group = LocalGroup()
+    flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
+    conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group) for g in range(G)]
+    for r in range(T):
+        for g in range(G):
+            conns[g].update_send(flats[g], send[r][g])
+        for g in range(G):
+            flats[g].add_(torch.from_numpy(deltas[r, g]).to(DEV))
+        for g in range(G):
+            payload, factor = conns[g].update_wait(wait[r][g])
+            if payload is not None:
+                conns[g].average(flats[g])
+        for g in range(G):
+            assert olerp.bits_equal(flats[g].cpu().numpy(), exp["params"][r, g]), (r, g)
+            assert conns[g].clock == exp["clocks"][r, g]
+
+
+def test_loss_tensor_on_device_is_used_without_sync(tmp_path):
+    cfg = tmp_path / "t.yaml"
+    write_cfg(cfg, ["a", "b"], 1.0, "loss", 0.0, None)
+    g = LocalGroup()
+    a = DpwaConnection("a", str(cfg), seed=1, group=g)
+    b = DpwaConnection("b", str(cfg), seed=2, group=g)
+    fa = torch.ones(1000, device=DEV)
+    fb = torch.zeros(1000, device=DEV)
+    a.update_send(fa, torch.tensor(1.0, device=DEV))
+    b.update_send(fb, torch.tensor(3.0, device=DEV, dtype=torch.float32))
+    payload, factor = a.update_wait(torch.tensor(1.0, device=DEV))
+    a.average(fa)
+    assert float(factor) == 1.0 / (1.0 + 3.0)          # loss/(loss+peer_loss)
+    want = torch.full((1000,), np.float32(0.25) * 0.0 + np.float32(0.75) * 1.0, device=DEV)
+    assert torch.equal(fa, want)
+
+
+def test_zero_division_is_raised_at_next_call(tmp_path):
+    cfg = tmp_path / "z.yaml"
+    write_cfg(cfg, ["a", "b"], 1.0, "loss", 0.0, None)
+    g = LocalGroup()
+    a = DpwaConnection("a", str(cfg), seed=1, group=g)
+    b = DpwaConnection("b", str(cfg), seed=2, group=g)
+    fa, fb = torch.ones(64, device=DEV), torch.zeros(64, device=DEV)
+    a.update_send(fa, 0.0)
+    b.update_send(fb, 0.0)
+    a.update_wait(0.0)
+    a.average(fa)
+    with pytest.raises(ZeroDivisionError):
+        a.synchronize()
+    assert torch.equal(fa, torch.ones(64, device=DEV))     # the round was a no-op
+    assert a.clock == 1.0
+
+
+def test_peer_not_up_and_no_state_follow_reference_flow_control(tmp_path):
+    """Peers that are not constructed yet are refused (score -100, no data); constructed but
+    unpublished peers give an empty reply (score +10, pick again)."""
+    cfg = tmp_path / "f.yaml"
+    write_cfg(cfg, ["a", "b", "c"], 1.0, "constant", 0.0, 0.5)
+    g = LocalGroup()
+    a = DpwaConnection("a", str(cfg), seed=3, group=g)
+    fa = torch.ones(256, device=DEV)
+    a.update_send(fa, 1.0)
+    payload, factor = a.update_wait(1.0)
+    assert payload is None and factor == 0
+    assert sorted(a.flow_control_scores().values()) == [900, 1000]
+    b = DpwaConnection("b", str(cfg), seed=4, group=g)
+    c = DpwaConnection("c", str(cfg), seed=5, group=g)
+    fb = torch.zeros(256, device=DEV)
+    b.update_send(fb, 1.0)          # c never publishes
+    for _ in range(5):
+        a.update_send(fa, 1.0)
+        payload, factor = a.update_wait(1.0)
+        assert payload is not None and payload.peer == "b"
+        a.average(fa)
+    a.inject_fault("b", "slow")
+    a.update_send(fa, 1.0)
+    c.update_send(torch.zeros(256, device=DEV), 1.0)
+    payload, _ = a.update_wait(1.0)
+    assert payload is not None and payload.peer == "c"
+    assert a.flow_control_scores()["b"] < 1000
+    a.inject_fault("b", "dead")
+    a.inject_fault("c", "dead")
+    a.update_send(fa, 1.0)
+    payload, _ = a.update_wait(1.0)
+    assert payload is None and set(a.flow_control_scores().values()) == {None}
