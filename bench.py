@@ -152,23 +152,25 @@ def main():
     stream = torch.cuda.current_stream(device)
     loss = 1.0
     lerp_events = []
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps * len(learners) + 1)]
 
     def step(timed):
         done = 0
         for conn, flat in learners:
             conn.update_send(flat, loss)
         for conn, flat in learners:
-            payload, _ = conn.update_wait(loss)
-            if payload is not None:
-                if timed:
-                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    a.record(stream)
-                    conn.average(flat, stream)
-                    b.record(stream)
+            # the adapter's update_wait: fused device factor + lerp (one kernel)
+            if timed:
+                a, b = events[len(lerp_events)]
+                a.record(stream)
+                payload, _ = conn.update_wait_average(flat, loss)
+                b.record(stream)
+                if payload is not None:
                     lerp_events.append((a, b))
-                else:
-                    conn.average(flat, stream)
-                done += 1
+            else:
+                payload, _ = conn.update_wait_average(flat, loss)
+            done += payload is not None
         return done
 
     for _ in range(args.warmup):
@@ -248,7 +250,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "dpwa::k_lerp_%s" % args.dtype,
+                "kernel": "dpwa::k_lerp<Ops%s, COEF_FUSED> (fused factor + lerp)" % args.dtype.upper(),
                 "bytes_per_launch": unit_bytes,
                 "avg_launch_us": round(lerp_us, 2),
                 "launches_timed": len(lerp_events),

@@ -87,6 +87,7 @@ SIGNATURES = {
     "dpwa_learner_lerp": [_vp, _vp, _vp],
     "dpwa_learner_pointers": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                               ctypes.POINTER(_vp)],
+    "dpwa_learner_status_word": [_vp, ctypes.POINTER(_vp)],
     "dpwa_learner_read_clock": [_vp, ctypes.POINTER(_dbl)],
     "dpwa_learner_write_clock": [_vp, _dbl],
     "dpwa_learner_read_coef": [_vp, ctypes.POINTER(Coef)],

@@ -12,8 +12,6 @@ rebinds ``param.data`` to a new tensor), and float32 *and* bfloat16 models are a
 """
 import logging
 
-import torch
-
 from ..dpwa import DpwaConnection
 from ..flat import FlatParameters
 
@@ -33,11 +31,7 @@ class DpwaPyTorchAdapter:
 
     def update_wait(self, loss):
         """pytorch.py:55-68: wait for the fetch and average in place."""
-        payload, factor = self._conn.update_wait(loss)
-        if payload is None:
-            return
-        LOGGER.debug("Averaging with %s", payload.peer)
-        self._conn.average(self._flat.buffer, torch.cuda.current_stream(self._flat.device))
+        self._conn.update_wait_average(self._flat.buffer, loss)
 
     # -- extensions -------------------------------------------------------------------
     @property

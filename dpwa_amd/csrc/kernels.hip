@@ -1,17 +1,25 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of the pairwise-averaging hot path.
 //
 //  * lerp:    the averaging statement of dpwa/adapters/pytorch.py:68,
-//             param = f32(f32(a*peer) + f32(b*param)), fused into ONE streaming pass over
-//             the flat parameter buffer (the reference runs three ATen kernels and allocates
-//             three temporaries per tensor).  Pure HBM streaming: 16-byte loads per lane,
-//             several independent loads in flight per lane, grid-stride; no LDS, no MFMA
-//             (0.25 flop/byte).  Separate roundings are required for bit parity with the
-//             reference (an FMA changes up to ~30% of results near cancellation), so
-//             contraction is switched off for this whole file.
-//  * factor:  dpwa/dpwa.py:139-155 + dpwa/interpolation.py:13-33 in IEEE fp64, one thread,
-//             writing the coefficients the lerp reads (no host round trip).
-//  * publish: update_send's snapshot (dpwa.py:111-116, pytorch.py:49-53) -- clock += 1 on the
-//             device and one copy of the flat buffer into a snapshot slot behind its header.
+//             param = f32(f32(a*peer) + f32(b*param)), as ONE streaming pass over the flat
+//             parameter buffer (the reference runs three ATen kernels and allocates three
+//             temporaries per tensor).  Pure HBM streaming (0.25 flop/byte): no LDS
+//             staging, no MFMA.  Shape chosen by measurement (tools/lerp_tune.hip): one
+//             16-byte item per lane and an exact grid -- thousands of short-lived 4-wave
+//             workgroups keep the most loads in flight per CU; grid-stride loops with
+//             more items per lane or a capped grid were 5-20% slower on gfx950.
+//             Separate roundings are required for bit parity with the reference (an FMA
+//             changes up to ~30% of results near cancellation), so contraction is
+//             switched off for this whole file.
+//  * fused average: the same pass with the factor of dpwa/dpwa.py:139-155 computed in
+//             the kernel: wave 0 of every workgroup evaluates it in fp64 while the
+//             workgroup's loads are in flight and broadcasts (a, b) through LDS; block 0
+//             also writes the new clock (into the other half of a double-buffered clock,
+//             so no workgroup ever reads a clock another one is writing) and dpwa_coef.
+//  * factor:  the same fp64 math as a one-thread kernel for the split API.
+//  * publish: update_send's snapshot (dpwa.py:111-116, pytorch.py:49-53) -- clock += 1 on
+//             the device and one copy of the flat buffer into a snapshot slot behind its
+//             header.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -22,57 +30,26 @@
 
 namespace dpwa {
 
-constexpr int kBlock = 256;      // 4 waves of 64
-constexpr int kUnroll = 4;       // 16-byte items per lane per operand in flight
-constexpr int kMaxGrid = 2048;   // 256 CUs x 8 resident blocks
+constexpr int kBlock = 256;   // 4 waves of 64
 
-int stream_grid(int64_t vec_items, int per_thread)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+static inline int64_t blocks_for(int64_t items)
 {
-    int64_t per_block = (int64_t)kBlock * per_thread;
-    int64_t g = (vec_items + per_block - 1) / per_block;
-    if (g < 1) g = 1;
-    if (g > kMaxGrid) g = kMaxGrid;
-    return (int)g;
+    int64_t g = (items + kBlock - 1) / kBlock;
+    return g < 1 ? 1 : g;
 }
 
-struct AB {
-    float a, b;
-};
-
-// Coefficients: a device block written by the factor kernel (status != 0 -> no-op), or
-// values passed by the host.  Uniform address -> scalar loads.
-__device__ __forceinline__ bool load_coef(const dpwa_coef *coef, float ha, float hb, AB &ab)
-{
-    if (coef) {
-        if (coef->status != DPWA_STATUS_OK) return false;
-        ab.a = coef->a;
-        ab.b = coef->b;
-    } else {
-        ab.a = ha;
-        ab.b = hb;
-    }
-    return true;
-}
-
+// ---------------------------------------------------------------- element ops
 __device__ __forceinline__ float lerp1(float a, float b, float peer, float param)
 {
     float x = a * peer;     // f32(a*t)          pytorch.py:68 `factor * t`
     float y = b * param;    // f32(b*p)          pytorch.py:68 `(1 - factor) * param.data`
     return x + y;           // f32(x + y)        contraction is off for this file
 }
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x4 lerp4(float a, float b, f32x4 q, f32x4 p)
-{
-    f32x4 x = a * q;
-    f32x4 y = b * p;
-    return x + y;
-}
-
-// ---------------------------------------------------------------- bf16 helpers
-typedef float float2v __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -93,152 +70,44 @@ __device__ __forceinline__ uint32_t lerp_bf16x2(float a, float b, uint32_t q, ui
     return pk_bf16(bf_lo(x) + bf_lo(y), bf_hi(x) + bf_hi(y));
 }
 
-__device__ __forceinline__ uint4 lerp_bf16x8(float a, float b, uint4 q, uint4 p)
-{
-    uint4 r;
-    r.x = lerp_bf16x2(a, b, q.x, p.x);
-    r.y = lerp_bf16x2(a, b, q.y, p.y);
-    r.z = lerp_bf16x2(a, b, q.z, p.z);
-    r.w = lerp_bf16x2(a, b, q.w, p.w);
-    return r;
-}
-
-__device__ __forceinline__ uint16_t lerp_bf16x1(float a, float b, uint16_t q, uint16_t p)
-{
-    return (uint16_t)(lerp_bf16x2(a, b, (uint32_t)q, (uint32_t)p) & 0xffffu);
-}
-
-// ---------------------------------------------------------------- lerp kernels
-// 16-byte vector path: both pointers 16-byte aligned.  Each lane keeps kUnroll
-// param and kUnroll peer loads in flight; a wave instruction covers 1 KiB.
-__global__ __launch_bounds__(kBlock) void k_lerp_f32(f32x4 *__restrict__ param,
-                                                     const f32x4 *__restrict__ peer, int64_t n,
-                                                     const dpwa_coef *__restrict__ coef, float ha, float hb)
-{
-    AB ab;
-    if (!load_coef(coef, ha, hb, ab)) return;
-    const int64_t n4 = n >> 2;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    for (; i + (kUnroll - 1) * stride < n4; i += kUnroll * stride) {
-        f32x4 p[kUnroll], q[kUnroll];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            q[u] = peer[i + u * stride];
-            p[u] = param[i + u * stride];
-        }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) param[i + u * stride] = lerp4(ab.a, ab.b, q[u], p[u]);
+struct OpsF32 {
+    using V = f32x4;
+    using S = float;
+    static constexpr int PER = 4;
+    __device__ static __forceinline__ V lerp(float a, float b, V q, V p)
+    {
+        V x = a * q;
+        V y = b * p;
+        return x + y;
     }
-    for (; i < n4; i += stride) param[i] = lerp4(ab.a, ab.b, peer[i], param[i]);
-    // ragged tail (n % 4 elements)
-    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
-        float *pf = reinterpret_cast<float *>(param);
-        const float *qf = reinterpret_cast<const float *>(peer);
-        const int64_t j = (n4 << 2) + threadIdx.x;
-        pf[j] = lerp1(ab.a, ab.b, qf[j], pf[j]);
+    __device__ static __forceinline__ S lerp_s(float a, float b, S q, S p) { return lerp1(a, b, q, p); }
+};
+
+struct OpsBF16 {
+    using V = u32x4;
+    using S = uint16_t;
+    static constexpr int PER = 8;
+    __device__ static __forceinline__ V lerp(float a, float b, V q, V p)
+    {
+        V r;
+        r.x = lerp_bf16x2(a, b, q.x, p.x);
+        r.y = lerp_bf16x2(a, b, q.y, p.y);
+        r.z = lerp_bf16x2(a, b, q.z, p.z);
+        r.w = lerp_bf16x2(a, b, q.w, p.w);
+        return r;
     }
-}
-
-__global__ __launch_bounds__(kBlock) void k_lerp_bf16(uint4 *__restrict__ param, const uint4 *__restrict__ peer,
-                                                      int64_t n, const dpwa_coef *__restrict__ coef, float ha,
-                                                      float hb)
-{
-    AB ab;
-    if (!load_coef(coef, ha, hb, ab)) return;
-    const int64_t n8 = n >> 3;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    for (; i + (kUnroll - 1) * stride < n8; i += kUnroll * stride) {
-        uint4 p[kUnroll], q[kUnroll];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            q[u] = peer[i + u * stride];
-            p[u] = param[i + u * stride];
-        }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) param[i + u * stride] = lerp_bf16x8(ab.a, ab.b, q[u], p[u]);
+    __device__ static __forceinline__ S lerp_s(float a, float b, S q, S p)
+    {
+        return (S)(lerp_bf16x2(a, b, (uint32_t)q, (uint32_t)p) & 0xffffu);
     }
-    for (; i < n8; i += stride) param[i] = lerp_bf16x8(ab.a, ab.b, peer[i], param[i]);
-    if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
-        uint16_t *ph = reinterpret_cast<uint16_t *>(param);
-        const uint16_t *qh = reinterpret_cast<const uint16_t *>(peer);
-        const int64_t j = (n8 << 3) + threadIdx.x;
-        ph[j] = lerp_bf16x1(ab.a, ab.b, qh[j], ph[j]);
-    }
-}
+};
 
-// Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
-__global__ __launch_bounds__(kBlock) void k_lerp_f32_unaligned(float *__restrict__ param,
-                                                               const float *__restrict__ peer, int64_t n,
-                                                               const dpwa_coef *__restrict__ coef, float ha,
-                                                               float hb)
-{
-    AB ab;
-    if (!load_coef(coef, ha, hb, ab)) return;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
-        param[i] = lerp1(ab.a, ab.b, peer[i], param[i]);
-}
-
-__global__ __launch_bounds__(kBlock) void k_lerp_bf16_unaligned(uint16_t *__restrict__ param,
-                                                                const uint16_t *__restrict__ peer, int64_t n,
-                                                                const dpwa_coef *__restrict__ coef, float ha,
-                                                                float hb)
-{
-    AB ab;
-    if (!load_coef(coef, ha, hb, ab)) return;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
-        param[i] = lerp_bf16x1(ab.a, ab.b, peer[i], param[i]);
-}
-
-static inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
-
-hipError_t launch_lerp(int32_t dtype, void *param, const void *peer, int64_t n, const dpwa_coef *coef,
-                       float a, float b, hipStream_t s)
-{
-    if (n <= 0) return hipSuccess;
-    const bool vec = aligned16(param) && aligned16(peer);
-    if (dtype == DPWA_F32) {
-        if (vec) {
-            int g = stream_grid(n >> 2, kUnroll);
-            hipLaunchKernelGGL(k_lerp_f32, dim3(g), dim3(kBlock), 0, s, (f32x4 *)param, (const f32x4 *)peer, n,
-                               coef, a, b);
-        } else {
-            int g = stream_grid(n, 1);
-            hipLaunchKernelGGL(k_lerp_f32_unaligned, dim3(g), dim3(kBlock), 0, s, (float *)param,
-                               (const float *)peer, n, coef, a, b);
-        }
-    } else if (dtype == DPWA_BF16) {
-        if (vec) {
-            int g = stream_grid(n >> 3, kUnroll);
-            hipLaunchKernelGGL(k_lerp_bf16, dim3(g), dim3(kBlock), 0, s, (uint4 *)param, (const uint4 *)peer, n,
-                               coef, a, b);
-        } else {
-            int g = stream_grid(n, 1);
-            hipLaunchKernelGGL(k_lerp_bf16_unaligned, dim3(g), dim3(kBlock), 0, s, (uint16_t *)param,
-                               (const uint16_t *)peer, n, coef, a, b);
-        }
-    } else {
-        return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------- factor
+// ---------------------------------------------------------------- factor math
 // dpwa.py:139-155 in IEEE double with every operation separately rounded, exactly as
 // CPython evaluates it.  Python raises ZeroDivisionError on x/0.0; here that is status 1,
 // the clock is left unchanged and the lerp becomes a no-op.
-__global__ void k_factor(dpwa_interp cfg, double *__restrict__ clock, const dpwa_header *__restrict__ peer,
-                         double loss_h, const double *__restrict__ loss_d, dpwa_coef *__restrict__ coef,
-                         int32_t *__restrict__ status_mirror)
+__device__ __forceinline__ dpwa_coef factor_math(const dpwa_interp &cfg, double c, double pc, double pl, double loss)
 {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    const double loss = loss_d ? *loss_d : loss_h;
-    const double c = *clock;
-    const double pc = peer->clock;
-    const double pl = peer->loss;
     int32_t status = DPWA_STATUS_OK;
     double f = 0.0;
     if (cfg.method == DPWA_INTERP_CONSTANT) {          // interpolation.py:13-15
@@ -260,57 +129,199 @@ __global__ void k_factor(dpwa_interp cfg, double *__restrict__ clock, const dpwa
     out.status = status;
     out.reserved = 0;
     if (status == DPWA_STATUS_OK) {
-        const double nc = f * pc + (1.0 - f) * c;      // dpwa.py:150
         out.factor = f;
-        out.new_clock = nc;
+        out.new_clock = f * pc + (1.0 - f) * c;        // dpwa.py:150
         out.a = (float)f;                              // torch: Python float -> fp32 scalar
         out.b = (float)(1.0 - f);                      // `1 - factor` in double, then fp32
-        *clock = nc;                                   // dpwa.py:155
     } else {
         out.factor = 0.0;
         out.new_clock = c;
         out.a = 0.0f;
         out.b = 1.0f;
     }
-    *coef = out;
-    if (status_mirror && status != DPWA_STATUS_OK) *status_mirror = status;   // sticky pinned host word
+    return out;
 }
 
-hipError_t launch_factor(const dpwa_interp &cfg, double *clock, const dpwa_header *peer, double loss,
-                         const double *loss_dev, dpwa_coef *coef, int32_t *status_mirror, hipStream_t s)
+__device__ __forceinline__ void factor_commit(const FusedArgs &fa, const dpwa_coef &c)
 {
-    hipLaunchKernelGGL(k_factor, dim3(1), dim3(64), 0, s, cfg, clock, peer, loss, loss_dev, coef, status_mirror);
+    *fa.clock_out = c.new_clock;                       // dpwa.py:155 (unchanged on error)
+    *fa.coef_out = c;
+    if (fa.status_mirror && c.status != DPWA_STATUS_OK) *fa.status_mirror = c.status;   // sticky
+}
+
+__global__ void k_factor(FusedArgs fa)
+{
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const double loss = fa.loss_d ? *fa.loss_d : fa.loss_h;
+    const dpwa_coef c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, loss);
+    factor_commit(fa, c);
+}
+
+hipError_t launch_factor(const FusedArgs &fa, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_factor, dim3(1), dim3(64), 0, s, fa);
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- lerp kernels
+enum CoefMode { COEF_HOST = 0, COEF_DEV = 1, COEF_FUSED = 2 };
+
+struct LerpArgs {
+    float a, b;                  // COEF_HOST
+    const dpwa_coef *coef;       // COEF_DEV
+    FusedArgs fused;             // COEF_FUSED
+};
+
+// One 16-byte item per lane; items beyond n/PER (the ragged tail) go to block 0.
+template <class Ops, int MODE>
+__global__ __launch_bounds__(kBlock) void k_lerp(typename Ops::V *__restrict__ param,
+                                                 const typename Ops::V *__restrict__ peer, int64_t n, LerpArgs args)
+{
+    using V = typename Ops::V;
+    const int64_t nv = n / Ops::PER;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool have = i < nv;
+    V q, p;
+    if (have) {              // issue this lane's loads before anything else
+        q = peer[i];
+        p = param[i];
+    }
+    float a, b;
+    if (MODE == COEF_HOST) {
+        a = args.a;
+        b = args.b;
+    } else if (MODE == COEF_DEV) {
+        if (args.coef->status != DPWA_STATUS_OK) return;
+        a = args.coef->a;
+        b = args.coef->b;
+    } else {
+        __shared__ float s_a, s_b;
+        __shared__ int s_ok;
+        if (threadIdx.x < 64) {  // wave 0: fp64 factor while the loads are in flight
+            const FusedArgs &fa = args.fused;
+            const double loss = fa.loss_d ? *fa.loss_d : fa.loss_h;
+            const dpwa_coef c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, loss);
+            if (threadIdx.x == 0) {
+                s_a = c.a;
+                s_b = c.b;
+                s_ok = c.status == DPWA_STATUS_OK;
+                if (blockIdx.x == 0) factor_commit(fa, c);
+            }
+        }
+        __syncthreads();
+        if (!s_ok) return;
+        a = s_a;
+        b = s_b;
+    }
+    if (have) param[i] = Ops::lerp(a, b, q, p);
+    if (blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
+        typename Ops::S *ps = reinterpret_cast<typename Ops::S *>(param);
+        const typename Ops::S *qs = reinterpret_cast<const typename Ops::S *>(peer);
+        const int64_t j = nv * Ops::PER + threadIdx.x;
+        ps[j] = Ops::lerp_s(a, b, qs[j], ps[j]);
+    }
+}
+
+// Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
+template <class Ops, int MODE>
+__global__ __launch_bounds__(kBlock) void k_lerp_unaligned(typename Ops::S *__restrict__ param,
+                                                           const typename Ops::S *__restrict__ peer, int64_t n,
+                                                           LerpArgs args)
+{
+    float a, b;
+    if (MODE == COEF_HOST) {
+        a = args.a;
+        b = args.b;
+    } else if (MODE == COEF_DEV) {
+        if (args.coef->status != DPWA_STATUS_OK) return;
+        a = args.coef->a;
+        b = args.coef->b;
+    } else {
+        const FusedArgs &fa = args.fused;
+        const double loss = fa.loss_d ? *fa.loss_d : fa.loss_h;
+        const dpwa_coef c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, loss);
+        if (blockIdx.x == 0 && threadIdx.x == 0) factor_commit(fa, c);
+        if (c.status != DPWA_STATUS_OK) return;
+        a = c.a;
+        b = c.b;
+    }
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        param[i] = Ops::lerp_s(a, b, peer[i], param[i]);
+}
+
+static inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+template <class Ops, int MODE>
+static hipError_t launch_mode(void *param, const void *peer, int64_t n, const LerpArgs &args, hipStream_t s)
+{
+    if (aligned16(param) && aligned16(peer)) {
+        const int64_t g = blocks_for(n / Ops::PER);
+        hipLaunchKernelGGL((k_lerp<Ops, MODE>), dim3((uint32_t)g), dim3(kBlock), 0, s, (typename Ops::V *)param,
+                           (const typename Ops::V *)peer, n, args);
+    } else {
+        int64_t g = blocks_for(n);
+        if (g > 8192) g = 8192;
+        hipLaunchKernelGGL((k_lerp_unaligned<Ops, MODE>), dim3((uint32_t)g), dim3(kBlock), 0, s,
+                           (typename Ops::S *)param, (const typename Ops::S *)peer, n, args);
+    }
+    return hipGetLastError();
+}
+
+template <class Ops>
+static hipError_t launch_ops(int mode, void *param, const void *peer, int64_t n, const LerpArgs &args, hipStream_t s)
+{
+    if (mode == COEF_HOST) return launch_mode<Ops, COEF_HOST>(param, peer, n, args, s);
+    if (mode == COEF_DEV) return launch_mode<Ops, COEF_DEV>(param, peer, n, args, s);
+    return launch_mode<Ops, COEF_FUSED>(param, peer, n, args, s);
+}
+
+static hipError_t launch_any(int32_t dtype, int mode, void *param, const void *peer, int64_t n, const LerpArgs &args,
+                             hipStream_t s)
+{
+    if (n < 0) return hipErrorInvalidValue;
+    if (n == 0 && mode != COEF_FUSED) return hipSuccess;
+    if (dtype == DPWA_F32) return launch_ops<OpsF32>(mode, param, peer, n, args, s);
+    if (dtype == DPWA_BF16) return launch_ops<OpsBF16>(mode, param, peer, n, args, s);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_lerp(int32_t dtype, void *param, const void *peer, int64_t n, const dpwa_coef *coef, float a,
+                       float b, hipStream_t s)
+{
+    LerpArgs args{};
+    args.a = a;
+    args.b = b;
+    args.coef = coef;
+    return launch_any(dtype, coef ? COEF_DEV : COEF_HOST, param, peer, n, args, s);
+}
+
+hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa, hipStream_t s)
+{
+    LerpArgs args{};
+    args.fused = fa;
+    return launch_any(dtype, COEF_FUSED, param, peer, n, args, s);
+}
+
 // ---------------------------------------------------------------- publish
-template <bool VEC, bool SYS_RELEASE>
+template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_publish(char *__restrict__ slot, const char *__restrict__ flat,
                                                     int64_t nbytes, int64_t n, int32_t dtype,
                                                     double *__restrict__ clock, double loss_h,
                                                     const double *__restrict__ loss_d, uint64_t version)
 {
     char *payload = slot + sizeof(dpwa_header);
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (VEC) {
         const int64_t n16 = nbytes >> 4;
-        const uint4 *src = reinterpret_cast<const uint4 *>(flat);
-        uint4 *dst = reinterpret_cast<uint4 *>(payload);
-        for (; i + (kUnroll - 1) * stride < n16; i += kUnroll * stride) {
-            uint4 v[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) v[u] = src[i + u * stride];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) dst[i + u * stride] = v[u];
-        }
-        for (; i < n16; i += stride) dst[i] = src[i];
+        const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        if (i < n16) reinterpret_cast<u32x4 *>(payload)[i] = reinterpret_cast<const u32x4 *>(flat)[i];
         if (blockIdx.x == 0 && threadIdx.x < (nbytes & 15)) {
             const int64_t j = (n16 << 4) + threadIdx.x;
             payload[j] = flat[j];
         }
     } else {
-        for (; i < nbytes; i += stride) payload[i] = flat[i];
+        const int64_t stride = (int64_t)gridDim.x * kBlock;
+        for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nbytes; i += stride) payload[i] = flat[i];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         dpwa_header *h = reinterpret_cast<dpwa_header *>(slot);
@@ -322,31 +333,31 @@ __global__ __launch_bounds__(kBlock) void k_publish(char *__restrict__ slot, con
         h->n = n;
         h->dtype = dtype;
     }
-    if (SYS_RELEASE) {
-        __syncthreads();
-        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope
-    }
+}
+
+// Writes back every XCD's L2 (system-scope release from 256 workgroups, which the
+// dispatcher deals round-robin over the 8 XCDs) so a snapshot that another GPU will pull
+// is in HBM, not only in this GPU's L2s.  Used only once the slots are IPC-exported.
+__global__ __launch_bounds__(64) void k_release_system()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t n, int32_t dtype, double *clock,
-                          double loss, const double *loss_dev, uint64_t version, bool system_release,
-                          hipStream_t s)
+                          double loss, const double *loss_dev, uint64_t version, bool system_release, hipStream_t s)
 {
-    const bool vec = aligned16(flat);
-    const int g = vec ? stream_grid(nbytes >> 4, kUnroll) : stream_grid(nbytes, 4);
     const char *src = (const char *)flat;
-    if (vec && system_release)
-        hipLaunchKernelGGL((k_publish<true, true>), dim3(g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype, clock,
+    if (aligned16(flat)) {
+        const int64_t g = blocks_for(nbytes >> 4);
+        hipLaunchKernelGGL((k_publish<true>), dim3((uint32_t)g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype, clock,
                            loss, loss_dev, version);
-    else if (vec)
-        hipLaunchKernelGGL((k_publish<true, false>), dim3(g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype,
+    } else {
+        int64_t g = blocks_for(nbytes);
+        if (g > 8192) g = 8192;
+        hipLaunchKernelGGL((k_publish<false>), dim3((uint32_t)g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype,
                            clock, loss, loss_dev, version);
-    else if (system_release)
-        hipLaunchKernelGGL((k_publish<false, true>), dim3(g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype,
-                           clock, loss, loss_dev, version);
-    else
-        hipLaunchKernelGGL((k_publish<false, false>), dim3(g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype,
-                           clock, loss, loss_dev, version);
+    }
+    if (system_release) hipLaunchKernelGGL(k_release_system, dim3(256), dim3(64), 0, s);
     return hipGetLastError();
 }
 

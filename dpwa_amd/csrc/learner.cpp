@@ -74,8 +74,7 @@ struct IpcBlob {
 static_assert(sizeof(IpcBlob) <= DPWA_IPC_HANDLE_BYTES, "IPC blob too large");
 
 struct Ctl {            // device control block
-    double clock;
-    double pad0;
+    double clock[2];    // double-buffered: a factor reads clock[cur] and writes clock[cur^1]
     dpwa_coef coef;
 };
 
@@ -125,6 +124,7 @@ struct dpwa_learner {
     char *staging = nullptr;        // 1 slot
     Ctl *ctl = nullptr;
     uint64_t version = 0;
+    int cur = 0;                        // index of the live clock in ctl->clock
     bool exported = false;
     hipStream_t side = nullptr;
     hipEvent_t ev_published[2] = {nullptr, nullptr};
@@ -193,7 +193,8 @@ int dpwa_factor(const dpwa_interp *cfg, double *clock_dev, const dpwa_header *pe
 {
     if (!cfg || !clock_dev || !peer_header_dev || !coef_dev) return set_error(DPWA_ERR_ARG, "dpwa_factor: NULL argument");
     if (cfg->method < 0 || cfg->method > 2) return set_error(DPWA_ERR_ARG, "dpwa_factor: unknown method %d", cfg->method);
-    HIP_TRY(launch_factor(*cfg, clock_dev, peer_header_dev, loss, loss_dev, coef_dev, nullptr, (hipStream_t)stream));
+    FusedArgs fa{*cfg, clock_dev, clock_dev, peer_header_dev, loss, loss_dev, coef_dev, nullptr};
+    HIP_TRY(launch_factor(fa, (hipStream_t)stream));
     return DPWA_OK;
 }
 
@@ -291,8 +292,8 @@ int dpwa_learner_publish(dpwa_learner *l, const void *flat, double loss, const d
         l->readers[k].clear();
     }
     char *slot = l->slots + (size_t)k * l->slot_stride;
-    HIP_TRY(launch_publish(slot, flat, (int64_t)l->payload_bytes, l->n, l->dtype, &l->ctl->clock, loss, loss_dev,
-                           l->version + 1, l->exported, s));
+    HIP_TRY(launch_publish(slot, flat, (int64_t)l->payload_bytes, l->n, l->dtype, &l->ctl->clock[l->cur], loss,
+                           loss_dev, l->version + 1, l->exported, s));
     HIP_TRY(hipEventRecord(l->ev_published[k], s));
     l->version++;
     return DPWA_OK;
@@ -416,18 +417,32 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
     return DPWA_OK;
 }
 
+static FusedArgs fused_args(dpwa_learner *l, double loss, const double *loss_dev)
+{
+    return FusedArgs{l->cfg, &l->ctl->clock[l->cur], &l->ctl->clock[l->cur ^ 1], (const dpwa_header *)l->src,
+                     loss, loss_dev, &l->ctl->coef, l->host_status_dev};
+}
+
 int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dpwa_stream_t stream)
 {
     if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_factor: NULL learner");
     if (!l->have_fetch) return set_error(DPWA_ERR_STATE, "dpwa_learner_factor: no fetch in flight");
+    if (l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_factor: factor already computed for this fetch");
     DeviceGuard dg(l->device);
     hipStream_t s = (hipStream_t)stream;
     if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
-    HIP_TRY(launch_factor(l->cfg, &l->ctl->clock, (const dpwa_header *)l->src, loss, loss_dev, &l->ctl->coef,
-                          l->host_status_dev, s));
+    HIP_TRY(launch_factor(fused_args(l, loss, loss_dev), s));
     HIP_TRY(hipEventRecord(l->ev_factor, s));
+    l->cur ^= 1;
     l->have_factor = true;
     return DPWA_OK;
+}
+
+static void finish_fetch(dpwa_learner *l)
+{
+    l->have_fetch = false;
+    l->have_factor = false;
+    l->src = nullptr;
 }
 
 int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream)
@@ -438,27 +453,39 @@ int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream)
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(launch_lerp(l->dtype, flat, l->src + kHeader, l->n, &l->ctl->coef, 0.f, 0.f, s));
     HIP_TRY(hipEventRecord(l->ev_consumed, s));
-    l->have_fetch = false;
-    l->have_factor = false;
-    l->src = nullptr;
+    finish_fetch(l);
     return DPWA_OK;
 }
 
 int dpwa_learner_average(dpwa_learner *l, void *flat, double loss, const double *loss_dev, dpwa_stream_t stream)
 {
-    int rc = dpwa_learner_factor(l, loss, loss_dev, stream);
-    if (rc) return rc;
-    return dpwa_learner_lerp(l, flat, stream);
+    if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_average: NULL argument");
+    if (!l->have_fetch || l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_average: no fetch in flight");
+    DeviceGuard dg(l->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
+    HIP_TRY(launch_average(l->dtype, flat, l->src + kHeader, l->n, fused_args(l, loss, loss_dev), s));
+    HIP_TRY(hipEventRecord(l->ev_consumed, s));
+    l->cur ^= 1;
+    finish_fetch(l);
+    return DPWA_OK;
 }
 
 int dpwa_learner_pointers(dpwa_learner *l, double **clock_dev, dpwa_coef **coef_dev, dpwa_header **staging_header_dev,
                           void **staging_payload_dev)
 {
     if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_pointers: NULL learner");
-    if (clock_dev) *clock_dev = &l->ctl->clock;
+    if (clock_dev) *clock_dev = &l->ctl->clock[l->cur];
     if (coef_dev) *coef_dev = &l->ctl->coef;
     if (staging_header_dev) *staging_header_dev = (dpwa_header *)l->staging;
     if (staging_payload_dev) *staging_payload_dev = l->staging + kHeader;
+    return DPWA_OK;
+}
+
+int dpwa_learner_status_word(dpwa_learner *l, int32_t **status_word)
+{
+    if (!l || !status_word) return set_error(DPWA_ERR_ARG, "dpwa_learner_status_word: NULL argument");
+    *status_word = l->host_status;
     return DPWA_OK;
 }
 
@@ -467,7 +494,7 @@ int dpwa_learner_read_clock(dpwa_learner *l, double *clock)
     if (!l || !clock) return set_error(DPWA_ERR_ARG, "dpwa_learner_read_clock: NULL argument");
     DeviceGuard dg(l->device);
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(clock, &l->ctl->clock, sizeof(double), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(clock, &l->ctl->clock[l->cur], sizeof(double), hipMemcpyDeviceToHost));
     return DPWA_OK;
 }
 
@@ -476,7 +503,7 @@ int dpwa_learner_write_clock(dpwa_learner *l, double clock)
     if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_write_clock: NULL learner");
     DeviceGuard dg(l->device);
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(&l->ctl->clock, &clock, sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(&l->ctl->clock[l->cur], &clock, sizeof(double), hipMemcpyHostToDevice));
     return DPWA_OK;
 }
 

@@ -142,6 +142,7 @@ class DpwaConnection:
         if seed is None:
             seed = self.config.get_seed(name)
         self._sched = Scheduler(len(self.peers), seed, self.fetch_probability)
+        self._status_buf = self._sched.status_buffer()
         self._faults = {}
         self._attached = {}
         self._learner = None
@@ -164,11 +165,13 @@ class DpwaConnection:
     def update_send(self, parameters, loss):
         """dpwa.py:104-123: publish (clock += 1, snapshot + {clock, loss}), then the
         Bernoulli fetch gate; under a DistGroup the fetch starts here on the side stream."""
-        self._raise_pending()
-        if self._learner is None:
-            self._bind(parameters)
-        stream = torch.cuda.current_stream(self._learner.device)
-        self._learner.publish(parameters, loss, stream)
+        learner = self._learner
+        if learner is None:
+            learner = self._bind(parameters)
+        elif learner.take_status():
+            self._zero_division()
+        stream = torch.cuda.current_stream(learner.device)
+        learner.publish(parameters, loss, stream)
         self._group.after_publish(self, stream)
         self._fetch_started = False
         self._fetch_peer = -1
@@ -183,16 +186,20 @@ class DpwaConnection:
     def update_wait(self, loss):
         """dpwa.py:125-156: (None, 0) when not fetching or no peer delivered; otherwise the
         fetched snapshot and the device factor (the clock is updated on the device)."""
-        self._raise_pending()
-        if not self.fetching:
-            return None, 0
-        self.fetching = False
-        stream = torch.cuda.current_stream(self._learner.device)
-        if not self._fetch_started:
-            self._start_fetch(stream)
-        if self._fetch_peer < 0:
+        stream = self._finish_fetch()
+        if stream is None:
             return None, 0
         self._learner.factor(loss, stream)
+        return PeerSnapshot(self, self._fetch_peer, self._fetch_version), DeviceFactor(self._learner)
+
+    def update_wait_average(self, parameters, loss):
+        """update_wait + the adapter's averaging (pytorch.py:60-68) as one fused kernel:
+        the factor is evaluated inside the lerp.  Same results as update_wait() followed by
+        average(); returns what update_wait returns."""
+        stream = self._finish_fetch()
+        if stream is None:
+            return None, 0
+        self._learner.average(parameters, loss, stream)
         return PeerSnapshot(self, self._fetch_peer, self._fetch_version), DeviceFactor(self._learner)
 
     # ---------------------------------------------------------------- extensions
@@ -205,7 +212,7 @@ class DpwaConnection:
 
     def average(self, parameters, stream=None):
         """The lerp of pytorch.py:68 with the coefficients of the last update_wait."""
-        self._learner.lerp(parameters, stream)
+        self._learner.lerp(parameters, stream if stream is not None else torch.cuda.current_stream(self._learner.device))
 
     def synchronize(self):
         """Waits for the device and raises a deferred ZeroDivisionError, if any."""
@@ -249,29 +256,46 @@ class DpwaConnection:
         cfg = self.interpolation.device_config(self.divergence_threshold)
         self._learner = Learner(parameters.device, parameters.numel(), parameters.dtype, cfg)
         self._group.on_bind(self)
+        return self._learner
+
+    def _finish_fetch(self):
+        """dpwa.py:130-137: returns the stream to average on, or None for "no data"."""
+        learner = self._learner
+        if learner is not None and learner.take_status():
+            self._zero_division()
+        if not self.fetching:
+            return None
+        self.fetching = False
+        stream = torch.cuda.current_stream(learner.device)
+        if not self._fetch_started:
+            self._start_fetch(stream)
+        if self._fetch_peer < 0:
+            return None
+        return stream
 
     def _start_fetch(self, stream):
         """TxThread.run for one queue item (conn.py:277-315) + the pull itself."""
         self._fetch_started = True
-        status = []
-        for p in self.peers:
-            st = self._faults.get(p.name)
-            status.append(self._group.peer_status(self, p.name) if st is None else st)
-        k, attempts = self._sched.fetch(status, MAX_FETCH_ATTEMPTS)
+        status = self._status_buf
+        group = self._group
+        for k, p in enumerate(self.peers):
+            st = self._faults.get(p.name) if self._faults else None
+            status[k] = group.peer_status(self, p.name) if st is None else st
+        k, attempts = self._sched.fetch_into(status, MAX_FETCH_ATTEMPTS)
         self.last_fetch_attempts = attempts
         self._fetch_peer = k
         if k < 0:
             return
-        version, zero_copy = self._group.prepare_fetch(self, k)
+        version, zero_copy = group.prepare_fetch(self, k)
         self._fetch_version = version
         self._learner.fetch(k, version, zero_copy, stream)
 
+    def _zero_division(self):
+        raise ZeroDivisionError("float division by zero (interpolation factor, dpwa.py:143-147)")
+
     def _raise_pending(self):
-        if self._learner is None:
-            return
-        done, status = self._learner.poll_status()
-        if status == _lib.STATUS_ZERO_DIVISION:
-            raise ZeroDivisionError("float division by zero (interpolation factor, dpwa.py:143-147)")
+        if self._learner is not None and self._learner.take_status():
+            self._zero_division()
 
     def __del__(self):
         try:

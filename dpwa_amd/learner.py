@@ -2,6 +2,8 @@
 
 A learner owns two snapshot slots, a staging buffer and the device clock/coefficient
 block on its GPU; this class only forwards torch tensors and streams to the C ABI.
+It sits on the per-round path, so it keeps host work small: raw ctypes function
+objects, a Python-side publish counter, validation only when the tensor changes.
 """
 import ctypes
 
@@ -11,6 +13,8 @@ from . import _lib
 
 DTYPES = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}
 
+_c_void_p = ctypes.c_void_p
+
 
 def loss_args(loss, device):
     """(host double, device pointer or None, keep-alive) for a loss given as a number or a
@@ -18,7 +22,7 @@ def loss_args(loss, device):
     if isinstance(loss, torch.Tensor):
         if loss.device.type == "cuda":
             t = loss.detach().to(device=device, dtype=torch.float64).reshape(())
-            return 0.0, ctypes.c_void_p(t.data_ptr()), t
+            return 0.0, _c_void_p(t.data_ptr()), t
         return float(loss.item()), None, None
     return float(loss), None, None
 
@@ -30,16 +34,27 @@ class Learner:
         self.device = torch.device(device)
         self.numel = int(numel)
         self.dtype = dtype
+        lib = _lib.load()
+        self._lib = lib
         self._h = ctypes.c_void_p()
-        cfg = interp_cfg
         _lib.call("dpwa_learner_create", ctypes.byref(self._h), self.device.index, self.numel, DTYPES[dtype],
-                  ctypes.byref(cfg))
+                  ctypes.byref(interp_cfg))
         clock, coef, sh, sp = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
         _lib.call("dpwa_learner_pointers", self._h, ctypes.byref(clock), ctypes.byref(coef), ctypes.byref(sh),
                   ctypes.byref(sp))
-        self.clock_ptr, self.coef_ptr = clock.value, coef.value
+        self.coef_ptr = coef.value
         self.staging_header_ptr, self.staging_payload_ptr = sh.value, sp.value
+        word = ctypes.c_void_p()
+        _lib.call("dpwa_learner_status_word", self._h, ctypes.byref(word))
+        self._status = ctypes.c_int32.from_address(word.value)
+        self.version = 0                 # publishes so far (mirrors dpwa_learner_version)
         self._keep = None
+        self._checked = None             # (id, data_ptr) of the last validated flat tensor
+        self._f_publish = lib.dpwa_learner_publish
+        self._f_fetch = lib.dpwa_learner_fetch
+        self._f_average = lib.dpwa_learner_average
+        self._f_factor = lib.dpwa_learner_factor
+        self._f_lerp = lib.dpwa_learner_lerp
 
     @property
     def handle(self):
@@ -56,23 +71,26 @@ class Learner:
         except Exception:
             pass
 
-    def _check(self, t):
-        if not isinstance(t, torch.Tensor) or t.device != self.device or t.dtype != self.dtype:
-            raise ValueError("expected a %s tensor on %s" % (self.dtype, self.device))
-        if not t.is_contiguous() or t.numel() != self.numel:
-            raise ValueError("expected a contiguous tensor of %d elements, got %s" % (self.numel, tuple(t.shape)))
+    def _ptr(self, t):
+        key = (id(t), t.data_ptr())
+        if key != self._checked:
+            if not isinstance(t, torch.Tensor) or t.device != self.device or t.dtype != self.dtype:
+                raise ValueError("expected a %s tensor on %s" % (self.dtype, self.device))
+            if not t.is_contiguous() or t.numel() != self.numel:
+                raise ValueError("expected a contiguous tensor of %d elements, got %s" % (self.numel, tuple(t.shape)))
+            self._checked = key
+        return key[1]
 
-    def publish(self, flat, loss, stream=None):
-        self._check(flat)
-        h, d, keep = loss_args(loss, self.device)
-        self._keep = keep
-        _lib.call("dpwa_learner_publish", self._h, ctypes.c_void_p(flat.data_ptr()), h, d, _lib.stream_handle(stream))
+    def _fail(self, name, rc):
+        raise _lib.DpwaError(name, rc, self._lib.dpwa_last_error().decode(errors="replace"))
 
-    @property
-    def version(self):
-        v = ctypes.c_uint64()
-        _lib.call("dpwa_learner_version", self._h, ctypes.byref(v))
-        return v.value
+    def publish(self, flat, loss, stream):
+        p = self._ptr(flat)
+        h, d, self._keep = loss_args(loss, self.device)
+        rc = self._f_publish(self._h, p, h, d, stream.cuda_stream)
+        if rc:
+            self._fail("dpwa_learner_publish", rc)
+        self.version += 1
 
     def attach_local(self, peer_id, other):
         _lib.call("dpwa_learner_attach_local", self._h, peer_id, other.handle)
@@ -86,25 +104,36 @@ class Learner:
         buf = ctypes.create_string_buffer(bytes(handle), _lib.IPC_HANDLE_BYTES)
         _lib.call("dpwa_learner_attach_ipc", self._h, peer_id, buf, _lib.IPC_HANDLE_BYTES)
 
-    def fetch(self, peer_id, peer_version, zero_copy=True, stream=None):
-        _lib.call("dpwa_learner_fetch", self._h, peer_id, peer_version, 1 if zero_copy else 0,
-                  _lib.stream_handle(stream))
+    def fetch(self, peer_id, peer_version, zero_copy, stream):
+        rc = self._f_fetch(self._h, peer_id, peer_version, 1 if zero_copy else 0, stream.cuda_stream)
+        if rc:
+            self._fail("dpwa_learner_fetch", rc)
 
-    def factor(self, loss, stream=None):
-        h, d, keep = loss_args(loss, self.device)
-        self._keep = keep
-        _lib.call("dpwa_learner_factor", self._h, h, d, _lib.stream_handle(stream))
+    def factor(self, loss, stream):
+        h, d, self._keep = loss_args(loss, self.device)
+        rc = self._f_factor(self._h, h, d, stream.cuda_stream)
+        if rc:
+            self._fail("dpwa_learner_factor", rc)
 
-    def lerp(self, flat, stream=None):
-        self._check(flat)
-        _lib.call("dpwa_learner_lerp", self._h, ctypes.c_void_p(flat.data_ptr()), _lib.stream_handle(stream))
+    def lerp(self, flat, stream):
+        rc = self._f_lerp(self._h, self._ptr(flat), stream.cuda_stream)
+        if rc:
+            self._fail("dpwa_learner_lerp", rc)
 
-    def average(self, flat, loss, stream=None):
-        self._check(flat)
-        h, d, keep = loss_args(loss, self.device)
-        self._keep = keep
-        _lib.call("dpwa_learner_average", self._h, ctypes.c_void_p(flat.data_ptr()), h, d,
-                  _lib.stream_handle(stream))
+    def average(self, flat, loss, stream):
+        """Fused factor + lerp (one kernel)."""
+        p = self._ptr(flat)
+        h, d, self._keep = loss_args(loss, self.device)
+        rc = self._f_average(self._h, p, h, d, stream.cuda_stream)
+        if rc:
+            self._fail("dpwa_learner_average", rc)
+
+    def take_status(self):
+        """Sticky device-reported status (no sync): non-OK at most once per error."""
+        st = self._status.value
+        if st:
+            self._status.value = 0
+        return st
 
     def read_clock(self):
         c = ctypes.c_double()

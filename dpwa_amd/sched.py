@@ -37,6 +37,9 @@ class Scheduler:
             arr = (ctypes.c_uint32 * max(1, len(key)))(*key)
             _lib.call("dpwa_sched_create", ctypes.byref(self._h), n_peers, arr, len(key), float(fetch_probability))
         self.n_peers = n_peers
+        self._f_fetch = _lib.load().dpwa_sched_fetch
+        self._peer_out, self._att_out = ctypes.c_int(), ctypes.c_int()
+        self._peer_ref, self._att_ref = ctypes.byref(self._peer_out), ctypes.byref(self._att_out)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -68,6 +71,18 @@ class Scheduler:
         arr = (ctypes.c_int32 * max(1, len(peer_status)))(*peer_status)
         peer, att = ctypes.c_int(), ctypes.c_int()
         _lib.call("dpwa_sched_fetch", self._h, arr, max_attempts, ctypes.byref(peer), ctypes.byref(att))
+        return peer.value, att.value
+
+    def status_buffer(self):
+        """A reusable per-peer status array for fetch_into()."""
+        return (ctypes.c_int32 * max(1, self.n_peers))()
+
+    def fetch_into(self, status_buf, max_attempts=1000):
+        """fetch() on a buffer from status_buffer() (no per-call allocation)."""
+        peer, att = self._peer_out, self._att_out
+        rc = self._f_fetch(self._h, status_buf, max_attempts, self._peer_ref, self._att_ref)
+        if rc:
+            raise _lib.DpwaError("dpwa_sched_fetch", rc, _lib.load().dpwa_last_error().decode(errors="replace"))
         return peer.value, att.value
 
     def score(self, peer):

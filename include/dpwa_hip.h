@@ -145,8 +145,10 @@ int dpwa_learner_attach_ipc(dpwa_learner *l, int peer_id, const void *handle, in
 int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int zero_copy,
                        dpwa_stream_t stream);
 
-/* update_wait's averaging (dpwa.py:133-155 + pytorch.py:64-68): make `stream` wait for the
- * fetch, compute factor/clock on the device, then lerp the n-element flat buffer in place. */
+/* update_wait's averaging (dpwa.py:133-155 + pytorch.py:64-68) as ONE kernel: make `stream`
+ * wait for the fetch, then every workgroup evaluates the factor (fp64, from the device clock
+ * and the peer's header) while its loads are in flight and lerps its part of the n-element
+ * flat buffer in place; workgroup 0 writes the new clock and the dpwa_coef. */
 int dpwa_learner_average(dpwa_learner *l, void *flat, double loss, const double *loss_dev,
                          dpwa_stream_t stream);
 
@@ -155,7 +157,10 @@ int dpwa_learner_average(dpwa_learner *l, void *flat, double loss, const double 
 int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dpwa_stream_t stream);
 int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream);
 
-/* Device pointers of the learner's blocks (for zero-copy views from the host side). */
+/* Device pointers of the learner's blocks.  The clock is double-buffered: *clock_dev is the
+ * live one and stays valid until the next factor/average.  status_word: the pinned host
+ * word behind dpwa_learner_poll_status (host address), for callers that poll it directly. */
+int dpwa_learner_status_word(dpwa_learner *l, int32_t **status_word);
 int dpwa_learner_pointers(dpwa_learner *l, double **clock_dev, dpwa_coef **coef_dev,
                           dpwa_header **staging_header_dev, void **staging_payload_dev);
 /* Synchronous reads for inspection (these DO synchronise with the learner's device). */

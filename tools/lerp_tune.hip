@@ -1,0 +1,216 @@
+// lerp_tune.hip -- standalone variant sweep for the fused lerp (not part of the product).
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -o tools/lerp_tune tools/lerp_tune.hip
+// Run:   tools/lerp_tune [numel] [rounds]
+// Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24); buffers rotate over
+// > 1 GiB so every launch streams from HBM, not the 256 MiB Infinity Cache.
+#pragma clang fp contract(off)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CHECK(x)                                                                              \
+    do {                                                                                      \
+        hipError_t e = (x);                                                                   \
+        if (e != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e));  \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 lerp4(float a, float b, f32x4 q, f32x4 p)
+{
+    f32x4 x = a * q;
+    f32x4 y = b * p;
+    return x + y;
+}
+
+template <typename T>
+__device__ __forceinline__ T ld(const T *p, bool nt)
+{
+    return nt ? __builtin_nontemporal_load(p) : *p;
+}
+template <typename T>
+__device__ __forceinline__ void st(T *p, T v, bool nt)
+{
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// Grid-stride, U items per lane in flight (interleaved by grid stride).
+template <int BLOCK, int U, bool NT_LD_Q, bool NT_LD_P, bool NT_ST>
+__global__ __launch_bounds__(BLOCK) void k_gs(f32x4 *__restrict__ param, const f32x4 *__restrict__ peer,
+                                              int64_t n4, float a, float b)
+{
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        f32x4 p[U], q[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            q[u] = ld(peer + i + u * stride, NT_LD_Q);
+            p[u] = ld(param + i + u * stride, NT_LD_P);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) st(param + i + u * stride, lerp4(a, b, q[u], p[u]), NT_ST);
+    }
+    for (; i < n4; i += stride) st(param + i, lerp4(a, b, ld(peer + i, NT_LD_Q), ld(param + i, NT_LD_P)), NT_ST);
+}
+
+// Block-contiguous tiles: block t owns items [t*BLOCK*U, (t+1)*BLOCK*U), lanes interleaved within.
+template <int BLOCK, int U, bool NT>
+__global__ __launch_bounds__(BLOCK) void k_tile(f32x4 *__restrict__ param, const f32x4 *__restrict__ peer,
+                                                int64_t n4, float a, float b)
+{
+    const int64_t tiles = (n4 + (int64_t)BLOCK * U - 1) / ((int64_t)BLOCK * U);
+    for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const int64_t base = t * BLOCK * U + threadIdx.x;
+        if (base + (U - 1) * BLOCK < n4) {
+            f32x4 p[U], q[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                q[u] = ld(peer + base + u * BLOCK, NT);
+                p[u] = ld(param + base + u * BLOCK, false);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) st(param + base + u * BLOCK, lerp4(a, b, q[u], p[u]), NT);
+        } else {
+            for (int u = 0; u < U; ++u) {
+                int64_t i = base + u * BLOCK;
+                if (i < n4) param[i] = lerp4(a, b, peer[i], param[i]);
+            }
+        }
+    }
+}
+
+// Copy (1R:1W) and read-only reduction, for calibration.
+__global__ __launch_bounds__(256) void k_copy(f32x4 *__restrict__ dst, const f32x4 *__restrict__ src, int64_t n4)
+{
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        f32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dst[i + u * stride] = v[u];
+    }
+    for (; i < n4; i += stride) dst[i] = src[i];
+}
+
+struct Variant {
+    std::string name;
+    double bytes_factor;   // x numel*4
+    std::function<void(float *, float *, int64_t, hipStream_t)> run;
+};
+
+static int grid_for(int64_t items, int per_block, int cap)
+{
+    int64_t g = (items + per_block - 1) / per_block;
+    if (cap > 0 && g > cap) g = cap;
+    return (int)std::max<int64_t>(g, 1);
+}
+
+template <int BLOCK, int U, bool A, bool B, bool C>
+Variant gs(const char *name, int cap)
+{
+    return {name, 3.0, [cap](float *p, float *q, int64_t n, hipStream_t s) {
+                int64_t n4 = n / 4;
+                int g = grid_for(n4, BLOCK * U, cap);
+                hipLaunchKernelGGL((k_gs<BLOCK, U, A, B, C>), dim3(g), dim3(BLOCK), 0, s, (f32x4 *)p, (const f32x4 *)q,
+                                   n4, 0.5f, 0.5f);
+            }};
+}
+
+template <int BLOCK, int U, bool NT>
+Variant tile(const char *name, int cap)
+{
+    return {name, 3.0, [cap](float *p, float *q, int64_t n, hipStream_t s) {
+                int64_t n4 = n / 4;
+                int g = grid_for(n4, BLOCK * U, cap);
+                hipLaunchKernelGGL((k_tile<BLOCK, U, NT>), dim3(g), dim3(BLOCK), 0, s, (f32x4 *)p, (const f32x4 *)q, n4,
+                                   0.5f, 0.5f);
+            }};
+}
+
+int main(int argc, char **argv)
+{
+    int64_t n = argc > 1 ? atoll(argv[1]) : 11173962;
+    int rounds = argc > 2 ? atoi(argv[2]) : 20;
+    n = n / 4 * 4;
+    const size_t bytes = (size_t)n * 4;
+    int pairs = (int)std::max<size_t>(4, (size_t)(1.5e9 / (2 * bytes)) + 1);
+    std::vector<float *> P(pairs), Q(pairs);
+    for (int i = 0; i < pairs; ++i) {
+        CHECK(hipMalloc(&P[i], bytes));
+        CHECK(hipMalloc(&Q[i], bytes));
+        CHECK(hipMemset(P[i], 0, bytes));
+        CHECK(hipMemset(Q[i], 0, bytes));
+    }
+    hipStream_t s;
+    CHECK(hipStreamCreate(&s));
+    std::vector<Variant> vs = {
+        gs<256, 4, false, false, false>("gs256x4 cap2048 (product)", 2048),
+        gs<256, 4, false, false, false>("gs256x4 exact", 0),
+        gs<256, 2, false, false, false>("gs256x2 exact", 0),
+        gs<256, 8, false, false, false>("gs256x8 exact", 0),
+        gs<256, 1, false, false, false>("gs256x1 exact", 0),
+        gs<512, 4, false, false, false>("gs512x4 exact", 0),
+        gs<1024, 2, false, false, false>("gs1024x2 exact", 0),
+        gs<256, 4, false, false, false>("gs256x4 cap1024", 1024),
+        gs<256, 4, false, false, false>("gs256x4 cap4096", 4096),
+        gs<256, 4, true, false, false>("gs256x4 exact ntQ", 0),
+        gs<256, 4, true, true, false>("gs256x4 exact ntQP", 0),
+        gs<256, 4, false, false, true>("gs256x4 exact ntST", 0),
+        gs<256, 4, true, true, true>("gs256x4 exact ntALL", 0),
+        tile<256, 4, false>("tile256x4 exact", 0),
+        tile<256, 8, false>("tile256x8 exact", 0),
+        tile<256, 4, false>("tile256x4 cap2048", 2048),
+        tile<512, 4, false>("tile512x4 exact", 0),
+        tile<256, 4, true>("tile256x4 exact nt", 0),
+        {"copy 1R1W (x2 bytes)", 2.0,
+         [](float *p, float *q, int64_t n, hipStream_t s) {
+             int64_t n4 = n / 4;
+             hipLaunchKernelGGL(k_copy, dim3(grid_for(n4, 1024, 0)), dim3(256), 0, s, (f32x4 *)p, (const f32x4 *)q, n4);
+         }},
+        {"hipMemcpyAsync D2D (x2 bytes)", 2.0,
+         [](float *p, float *q, int64_t n, hipStream_t s) { (void)hipMemcpyAsync(p, q, n * 4, hipMemcpyDeviceToDevice, s); }},
+    };
+    std::vector<std::vector<double>> us(vs.size());
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    int rot = 0;
+    for (int r = 0; r < rounds + 2; ++r) {
+        for (size_t v = 0; v < vs.size(); ++v) {
+            const int reps = 8;
+            CHECK(hipEventRecord(e0, s));
+            for (int k = 0; k < reps; ++k) {
+                vs[v].run(P[rot % pairs], Q[rot % pairs], n, s);
+                rot++;
+            }
+            CHECK(hipEventRecord(e1, s));
+            CHECK(hipEventSynchronize(e1));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 2) us[v].push_back(1e3 * ms / reps);
+        }
+    }
+    printf("numel %lld (%.1f MB per operand), %d rotating pairs, %d rounds x 8 launches\n", (long long)n, bytes / 1e6,
+           pairs, rounds);
+    for (size_t v = 0; v < vs.size(); ++v) {
+        auto x = us[v];
+        std::sort(x.begin(), x.end());
+        double med = x[x.size() / 2], best = x[0];
+        double gb = vs[v].bytes_factor * bytes;
+        printf("%-34s median %8.2f us  %7.1f GB/s (%.1f%%)   best %7.1f GB/s\n", vs[v].name.c_str(), med, gb / med / 1e3,
+               100.0 * gb / med / 1e3 / 8000.0, gb / best / 1e3);
+    }
+    return 0;
+}
