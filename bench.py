@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
+    ap.add_argument("--no-write-through", action="store_true", help="skip the write-through variant")
+    ap.add_argument("--sample-every", type=int, default=4, help="time the averaging kernel every k-th step")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="PMC traffic summary (rocprofv3 FETCH_SIZE/WRITE_SIZE passes) to report")
     return ap.parse_args()
@@ -88,29 +90,37 @@ def cpu_baseline(numel, seconds):
             "ms_per_round": 1e3 * el / rounds}
 
 
-def cold_kernel(numel, dtype, device, launches=40):
-    """Lerp alone over rotating buffers (> 512 MiB between reuses: no Infinity-Cache hits)."""
+def cold_kernel(numel, dtype, device, launches=64):
+    """The fused average kernel alone over rotating buffers (> 1 GiB between reuses, so no
+    Infinity-Cache hits), launched back to back; one event pair around the whole batch."""
     from dpwa_amd import _lib
+    from dpwa_amd.interpolation import ConstantInterpolation
+    from dpwa_amd.learner import Learner
     esize = 4 if dtype == torch.float32 else 2
     pairs = max(4, int(np.ceil(1.2e9 / (2 * numel * esize))))
     bufs = [(torch.randn(numel, device=device).to(dtype), torch.randn(numel, device=device).to(dtype))
             for _ in range(pairs)]
     fn = "dpwa_lerp_f32_host" if dtype == torch.float32 else "dpwa_lerp_bf16_host"
     s = _lib.stream_handle(None)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
-    for i in range(launches + pairs):
+    f = getattr(_lib.load(), fn)
+
+    def run(i):
         p, q = bufs[i % pairs]
-        j = i - pairs
-        if j >= 0:
-            evs[j][0].record()
-        _lib.call(fn, ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(q.data_ptr()), numel, 0.5, s)
-        if j >= 0:
-            evs[j][1].record()
+        f(p.data_ptr(), q.data_ptr(), numel, 0.5, s)
+
+    for i in range(pairs):
+        run(i)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(50_000_000)          # let the host queue the whole batch first
+    a.record()
+    for i in range(launches):
+        run(i)
+    b.record()
     torch.cuda.synchronize()
-    ms = np.array([a.elapsed_time(b) for a, b in evs])
+    us = a.elapsed_time(b) * 1e3 / launches
     del bufs
     torch.cuda.empty_cache()
-    return 3 * numel * esize / (ms.mean() * 1e-3) / 1e9, float(ms.mean() * 1e3), pairs
+    return 3 * numel * esize / (us * 1e-6) / 1e9, us, pairs
 
 
 def main():
@@ -151,57 +161,60 @@ def main():
 
     stream = torch.cuda.current_stream(device)
     loss = 1.0
-    lerp_events = []
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps * len(learners) + 1)]
 
-    def step(timed):
-        done = 0
-        for conn, flat in learners:
-            conn.update_send(flat, loss)
-        for conn, flat in learners:
-            # the adapter's update_wait: fused device factor + lerp (one kernel)
-            if timed:
-                a, b = events[len(lerp_events)]
-                a.record(stream)
-                payload, _ = conn.update_wait_average(flat, loss)
-                b.record(stream)
-                if payload is not None:
-                    lerp_events.append((a, b))
-            else:
-                payload, _ = conn.update_wait_average(flat, loss)
-            done += payload is not None
-        return done
+    def run(steps, warmup, write_through, sample_every):
+        """`steps` timed lock-step rounds; the averaging kernel of every `sample_every`-th
+        step is bracketed by HIP events on its stream."""
+        lerp_events = []
+        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range((steps // sample_every + 1) * len(learners))]
 
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    averaged = 0
-    for _ in range(args.steps):
-        averaged += step(True)
-    torch.cuda.synchronize()
-    host_enqueue_done = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        def step(k, timed):
+            done = 0
+            for conn, flat in learners:
+                conn.update_send(flat, loss, reuse_snapshot=write_through)
+            sample = timed and k % sample_every == 0
+            for conn, flat in learners:
+                # the adapter's update_wait: fused device factor + lerp (one kernel)
+                if sample:
+                    a, b = events[len(lerp_events)]
+                    a.record(stream)
+                payload, _ = conn.update_wait_average(flat, loss, write_through=write_through)
+                if sample:
+                    b.record(stream)
+                    if payload is not None:
+                        lerp_events.append((a, b))
+                done += payload is not None
+            return done
 
-    lerp_ms = np.array([a.elapsed_time(b) for a, b in lerp_events]) if lerp_events else np.array([np.nan])
-    stats = torch.tensor([elapsed, float(averaged), float(len(learners) * args.steps)], dtype=torch.float64,
-                         device=device)
-    if world > 1:
-        tmax = stats[0:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        sums = stats[1:].clone()
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax.item())
-        averaged, rounds = float(sums[0].item()), float(sums[1].item())
-    else:
-        averaged, rounds = float(averaged), float(len(learners) * args.steps)
+        for k in range(warmup):
+            step(k, False)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        averaged = 0
+        for k in range(steps):
+            averaged += step(k, True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        lerp_ms = np.array([a.elapsed_time(b) for a, b in lerp_events]) if lerp_events else np.array([np.nan])
+        stats = torch.tensor([elapsed, float(averaged), float(len(learners) * steps)], dtype=torch.float64,
+                             device=device)
+        if world > 1:
+            tmax = stats[0:1].clone()
+            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+            sums = stats[1:].clone()
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+            return float(tmax.item()), float(sums[0].item()), float(sums[1].item()), lerp_ms
+        return elapsed, float(averaged), float(len(learners) * steps), lerp_ms
+
+    elapsed, averaged, rounds, lerp_ms = run(args.steps, args.warmup, False, args.sample_every)
+    wt = run(args.steps, args.warmup, True, args.sample_every) if not args.no_write_through else None
 
     unit_bytes = 3 * args.numel * esize
     if rank == 0:
@@ -253,11 +266,23 @@ def main():
                 "kernel": "dpwa::k_lerp<Ops%s, COEF_FUSED> (fused factor + lerp)" % args.dtype.upper(),
                 "bytes_per_launch": unit_bytes,
                 "avg_launch_us": round(lerp_us, 2),
-                "launches_timed": len(lerp_events),
+                "launches_timed": int(np.isfinite(lerp_ms).sum()),
                 "traffic_source": traffic_src,
             },
-            "host_enqueue_ms_per_step": round(1e3 * (host_enqueue_done - t0) / args.steps, 4),
         }
+        if wt is not None:
+            w_el, w_avg, w_rounds, w_ms = wt
+            w_us = float(np.nanmean(w_ms) * 1e3)
+            out["write_through"] = {
+                "value": round(w_avg * unit_bytes / w_el / 1e9, 2),
+                "ms_per_step": round(1e3 * w_el / args.steps, 4),
+                "note": "update_wait_average(write_through=True) + update_send(reuse_snapshot=True): the "
+                        "averaging kernel also writes the next snapshot (4*N*s bytes), the publish moves only "
+                        "the 256-B header; valid when nothing modifies the parameters between update_wait and "
+                        "the next update_send (the README loop)",
+                "avg_launch_us": round(w_us, 2),
+                "kernel_gbs_4ns": round(4 * args.numel * esize / (w_us * 1e-6) / 1e9, 1),
+            }
         if world == 1 and not args.no_cold:
             gbs, us, pairs = cold_kernel(args.numel, dtype, device)
             out["roofline"]["cold_cache"] = {"achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),

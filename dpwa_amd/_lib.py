@@ -27,6 +27,8 @@ IPC_HANDLE_BYTES = 128
 CONNECT_OK, CONNECT_REFUSED, CONNECT_ERROR = 0, 1, 2
 REPLY_PAYLOAD, REPLY_EMPTY, REPLY_TIMEOUT, REPLY_ERROR = 3, 4, 5, 6
 PEER_READY, PEER_NO_STATE, PEER_DOWN, PEER_SLOW, PEER_DEAD = 0, 1, 2, 3, 4
+NODE_PEER_UNSET, NODE_PEER_LOCAL, NODE_PEER_REMOTE = 0, 1, 2
+FLAG_EAGER, FLAG_ZERO_COPY, FLAG_REUSE_SNAPSHOT, FLAG_WRITE_THROUGH = 1, 2, 4, 8
 
 
 class DpwaLibraryError(RuntimeError):
@@ -83,8 +85,11 @@ SIGNATURES = {
     "dpwa_learner_attach_ipc": [_vp, _int, _vp, _i64],
     "dpwa_learner_fetch": [_vp, _int, _u64, _int, _vp],
     "dpwa_learner_average": [_vp, _vp, _dbl, _vp, _vp],
+    "dpwa_learner_average_through": [_vp, _vp, _dbl, _vp, _vp],
+    "dpwa_learner_publish_reuse": [_vp, _vp, _dbl, _vp, _vp],
     "dpwa_learner_factor": [_vp, _dbl, _vp, _vp],
     "dpwa_learner_lerp": [_vp, _vp, _vp],
+    "dpwa_learner_cancel": [_vp],
     "dpwa_learner_pointers": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                               ctypes.POINTER(_vp)],
     "dpwa_learner_status_word": [_vp, ctypes.POINTER(_vp)],
@@ -92,6 +97,20 @@ SIGNATURES = {
     "dpwa_learner_write_clock": [_vp, _dbl],
     "dpwa_learner_read_coef": [_vp, ctypes.POINTER(Coef)],
     "dpwa_learner_poll_status": [_vp, _pint, ctypes.POINTER(_i32)],
+    "dpwa_node_create": [ctypes.POINTER(_vp), _int, ctypes.POINTER(ctypes.c_uint32), _int, _dbl,
+                         ctypes.POINTER(Interp)],
+    "dpwa_node_destroy": [_vp],
+    "dpwa_node_bind": [_vp, _int, _i64, _i32],
+    "dpwa_node_handles": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp)],
+    "dpwa_node_set_peer": [_vp, _int, _int, _vp],
+    "dpwa_node_set_fault": [_vp, _int, _int],
+    "dpwa_node_update_send": [_vp, _vp, _dbl, _vp, _int, _vp, _pint],
+    "dpwa_node_publish": [_vp, _vp, _dbl, _vp, _int, _vp],
+    "dpwa_node_gate": [_vp, _int, _vp, _pint],
+    "dpwa_node_update_wait": [_vp, _dbl, _vp, _int, _vp, _pint],
+    "dpwa_node_lerp": [_vp, _vp, _vp],
+    "dpwa_node_update_wait_average": [_vp, _vp, _dbl, _vp, _int, _vp, _pint],
+    "dpwa_node_info": [_vp, _pint, _pint, ctypes.POINTER(_u64), _pint],
     "dpwa_sched_create": [ctypes.POINTER(_vp), _int, ctypes.POINTER(ctypes.c_uint32), _int, _dbl],
     "dpwa_sched_destroy": [_vp],
     "dpwa_sched_bernoulli": [_vp, _pint],

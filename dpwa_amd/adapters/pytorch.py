@@ -19,19 +19,37 @@ LOGGER = logging.getLogger(__name__)
 
 
 class DpwaPyTorchAdapter:
-    def __init__(self, net, name, config_file, **connection_kwargs):
+    """write_through (extension, default off): the averaging kernel also writes the next
+    snapshot, and the next update_send publishes only the header when no parameter was
+    modified in between.  Modifications through autograd-visible in-place ops (optimizers,
+    ``param.add_``) are detected from the parameters' version counters and force a full
+    publish; writes through ``param.data`` are invisible to that check, so enable this only
+    for loops that do not touch ``.data`` between update_wait and update_send (the README
+    loop and the reference's example trainer do not)."""
+
+    def __init__(self, net, name, config_file, write_through=False, **connection_kwargs):
         self._net = net
         self._flat = FlatParameters(net.named_parameters())
         self._conn = DpwaConnection(name, config_file, **connection_kwargs)
+        self._write_through = write_through
+        self._versions = None
+
+    def _param_versions(self):
+        return [p._version for p in self._flat.params]
 
     def update_send(self, loss):
         """pytorch.py:42-53: publish the parameters and maybe start a fetch."""
-        self._flat.resync()
-        self._conn.update_send(self._flat.buffer, loss)
+        moved = self._flat.resync()
+        reuse = (self._write_through and moved == 0 and self._versions is not None
+                 and self._versions == self._param_versions())
+        self._versions = None
+        self._conn.update_send(self._flat.buffer, loss, reuse_snapshot=reuse)
 
     def update_wait(self, loss):
         """pytorch.py:55-68: wait for the fetch and average in place."""
-        self._conn.update_wait_average(self._flat.buffer, loss)
+        payload, _ = self._conn.update_wait_average(self._flat.buffer, loss, write_through=self._write_through)
+        if self._write_through and payload is not None:
+            self._versions = self._param_versions()
 
     # -- extensions -------------------------------------------------------------------
     @property

@@ -170,10 +170,13 @@ struct LerpArgs {
     float a, b;                  // COEF_HOST
     const dpwa_coef *coef;       // COEF_DEV
     FusedArgs fused;             // COEF_FUSED
+    void *snap;                  // DUAL: second destination (the next snapshot's payload)
 };
 
 // One 16-byte item per lane; items beyond n/PER (the ragged tail) go to block 0.
-template <class Ops, int MODE>
+// DUAL also stores the result into args.snap (write-through snapshot: the next publish of
+// these parameters then needs no copy).
+template <class Ops, int MODE, bool DUAL>
 __global__ __launch_bounds__(kBlock) void k_lerp(typename Ops::V *__restrict__ param,
                                                  const typename Ops::V *__restrict__ peer, int64_t n, LerpArgs args)
 {
@@ -209,21 +212,34 @@ __global__ __launch_bounds__(kBlock) void k_lerp(typename Ops::V *__restrict__ p
             }
         }
         __syncthreads();
-        if (!s_ok) return;
+        if (!s_ok) {          // no-op round; a write-through snapshot still gets the parameters
+            if (DUAL && have) reinterpret_cast<V *>(args.snap)[i] = p;
+            if (DUAL && blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
+                const int64_t j = nv * Ops::PER + threadIdx.x;
+                reinterpret_cast<typename Ops::S *>(args.snap)[j] = reinterpret_cast<typename Ops::S *>(param)[j];
+            }
+            return;
+        }
         a = s_a;
         b = s_b;
     }
-    if (have) param[i] = Ops::lerp(a, b, q, p);
+    if (have) {
+        const V r = Ops::lerp(a, b, q, p);
+        param[i] = r;
+        if (DUAL) reinterpret_cast<V *>(args.snap)[i] = r;
+    }
     if (blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
         typename Ops::S *ps = reinterpret_cast<typename Ops::S *>(param);
         const typename Ops::S *qs = reinterpret_cast<const typename Ops::S *>(peer);
         const int64_t j = nv * Ops::PER + threadIdx.x;
-        ps[j] = Ops::lerp_s(a, b, qs[j], ps[j]);
+        const typename Ops::S r = Ops::lerp_s(a, b, qs[j], ps[j]);
+        ps[j] = r;
+        if (DUAL) reinterpret_cast<typename Ops::S *>(args.snap)[j] = r;
     }
 }
 
 // Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
-template <class Ops, int MODE>
+template <class Ops, int MODE, bool DUAL>
 __global__ __launch_bounds__(kBlock) void k_lerp_unaligned(typename Ops::S *__restrict__ param,
                                                            const typename Ops::S *__restrict__ peer, int64_t n,
                                                            LerpArgs args)
@@ -241,28 +257,38 @@ __global__ __launch_bounds__(kBlock) void k_lerp_unaligned(typename Ops::S *__re
         const double loss = fa.loss_d ? *fa.loss_d : fa.loss_h;
         const dpwa_coef c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, loss);
         if (blockIdx.x == 0 && threadIdx.x == 0) factor_commit(fa, c);
-        if (c.status != DPWA_STATUS_OK) return;
+        if (c.status != DPWA_STATUS_OK) {
+            if (DUAL) {
+                const int64_t stride = (int64_t)gridDim.x * kBlock;
+                for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+                    reinterpret_cast<typename Ops::S *>(args.snap)[i] = param[i];
+            }
+            return;
+        }
         a = c.a;
         b = c.b;
     }
     const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
-        param[i] = Ops::lerp_s(a, b, peer[i], param[i]);
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const typename Ops::S r = Ops::lerp_s(a, b, peer[i], param[i]);
+        param[i] = r;
+        if (DUAL) reinterpret_cast<typename Ops::S *>(args.snap)[i] = r;
+    }
 }
 
 static inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
-template <class Ops, int MODE>
+template <class Ops, int MODE, bool DUAL>
 static hipError_t launch_mode(void *param, const void *peer, int64_t n, const LerpArgs &args, hipStream_t s)
 {
-    if (aligned16(param) && aligned16(peer)) {
+    if (aligned16(param) && aligned16(peer) && aligned16(args.snap)) {
         const int64_t g = blocks_for(n / Ops::PER);
-        hipLaunchKernelGGL((k_lerp<Ops, MODE>), dim3((uint32_t)g), dim3(kBlock), 0, s, (typename Ops::V *)param,
-                           (const typename Ops::V *)peer, n, args);
+        hipLaunchKernelGGL((k_lerp<Ops, MODE, DUAL>), dim3((uint32_t)g), dim3(kBlock), 0, s,
+                           (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
     } else {
         int64_t g = blocks_for(n);
         if (g > 8192) g = 8192;
-        hipLaunchKernelGGL((k_lerp_unaligned<Ops, MODE>), dim3((uint32_t)g), dim3(kBlock), 0, s,
+        hipLaunchKernelGGL((k_lerp_unaligned<Ops, MODE, DUAL>), dim3((uint32_t)g), dim3(kBlock), 0, s,
                            (typename Ops::S *)param, (const typename Ops::S *)peer, n, args);
     }
     return hipGetLastError();
@@ -271,9 +297,10 @@ static hipError_t launch_mode(void *param, const void *peer, int64_t n, const Le
 template <class Ops>
 static hipError_t launch_ops(int mode, void *param, const void *peer, int64_t n, const LerpArgs &args, hipStream_t s)
 {
-    if (mode == COEF_HOST) return launch_mode<Ops, COEF_HOST>(param, peer, n, args, s);
-    if (mode == COEF_DEV) return launch_mode<Ops, COEF_DEV>(param, peer, n, args, s);
-    return launch_mode<Ops, COEF_FUSED>(param, peer, n, args, s);
+    if (mode == COEF_HOST) return launch_mode<Ops, COEF_HOST, false>(param, peer, n, args, s);
+    if (mode == COEF_DEV) return launch_mode<Ops, COEF_DEV, false>(param, peer, n, args, s);
+    if (args.snap) return launch_mode<Ops, COEF_FUSED, true>(param, peer, n, args, s);
+    return launch_mode<Ops, COEF_FUSED, false>(param, peer, n, args, s);
 }
 
 static hipError_t launch_any(int32_t dtype, int mode, void *param, const void *peer, int64_t n, const LerpArgs &args,
@@ -296,10 +323,12 @@ hipError_t launch_lerp(int32_t dtype, void *param, const void *peer, int64_t n, 
     return launch_any(dtype, coef ? COEF_DEV : COEF_HOST, param, peer, n, args, s);
 }
 
-hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa, hipStream_t s)
+hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa, void *snap,
+                          hipStream_t s)
 {
     LerpArgs args{};
     args.fused = fa;
+    args.snap = snap;
     return launch_any(dtype, COEF_FUSED, param, peer, n, args, s);
 }
 
@@ -357,6 +386,30 @@ hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t 
         hipLaunchKernelGGL((k_publish<false>), dim3((uint32_t)g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype,
                            clock, loss, loss_dev, version);
     }
+    if (system_release) hipLaunchKernelGGL(k_release_system, dim3(256), dim3(64), 0, s);
+    return hipGetLastError();
+}
+
+// Header-only publish: the payload of `slot` was already written by a write-through
+// average of exactly these parameters.
+__global__ void k_publish_header(char *__restrict__ slot, int64_t n, int32_t dtype, double *__restrict__ clock,
+                                 double loss_h, const double *__restrict__ loss_d, uint64_t version)
+{
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    dpwa_header *h = reinterpret_cast<dpwa_header *>(slot);
+    const double c = *clock + 1.0;                     // dpwa.py:112
+    *clock = c;
+    h->clock = c;
+    h->loss = loss_d ? *loss_d : loss_h;
+    h->version = version;
+    h->n = n;
+    h->dtype = dtype;
+}
+
+hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *clock, double loss,
+                                 const double *loss_dev, uint64_t version, bool system_release, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_publish_header, dim3(1), dim3(64), 0, s, slot, n, dtype, clock, loss, loss_dev, version);
     if (system_release) hipLaunchKernelGGL(k_release_system, dim3(256), dim3(64), 0, s);
     return hipGetLastError();
 }

@@ -32,9 +32,9 @@ struct FusedArgs {
 hipError_t launch_lerp(int32_t dtype, void *param, const void *peer, int64_t n, const dpwa_coef *coef,
                        float a, float b, hipStream_t s);
 
-// Fused factor + lerp (one launch).
+// Fused factor + lerp (one launch); a non-null `snap` also receives the result.
 hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa,
-                          hipStream_t s);
+                          void *snap, hipStream_t s);
 
 // Factor + clock only (one thread).
 hipError_t launch_factor(const FusedArgs &fa, hipStream_t s);
@@ -45,5 +45,8 @@ hipError_t launch_factor(const FusedArgs &fa, hipStream_t s);
 hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t n, int32_t dtype,
                           double *clock, double loss, const double *loss_dev, uint64_t version,
                           bool system_release, hipStream_t s);
+// Publish of the header only (the payload was written through by the last average).
+hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *clock, double loss,
+                                 const double *loss_dev, uint64_t version, bool system_release, hipStream_t s);
 
 }  // namespace dpwa

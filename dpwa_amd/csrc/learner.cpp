@@ -127,11 +127,25 @@ struct dpwa_learner {
     int cur = 0;                        // index of the live clock in ctl->clock
     bool exported = false;
     hipStream_t side = nullptr;
+    // Cross-stream ordering is recorded lazily: the stream of every publish / consumption is
+    // remembered and an event is recorded (on that stream, at the moment a dependent
+    // operation is enqueued) only when the dependent operation runs on a different stream.
+    // In the common single-stream loop no event is recorded at all.
     hipEvent_t ev_published[2] = {nullptr, nullptr};
+    hipStream_t publish_stream[2] = {nullptr, nullptr};
+    bool published[2] = {false, false};
     hipEvent_t ev_issue = nullptr;      // fetch may start (recorded on the caller's stream)
     hipEvent_t ev_fetched = nullptr;    // fetch landed (recorded on the side stream)
     hipEvent_t ev_consumed = nullptr;   // this learner finished reading its fetch source
+    hipStream_t consume_stream = nullptr;
+    bool consumed_once = false;
     hipEvent_t ev_factor = nullptr;     // last factor computation done
+    // write-through snapshot: the last average also wrote its result into the slot of the
+    // next publish (for the flat buffer `wt_flat`, on stream `wt_stream`)
+    bool wt_valid = false;
+    const void *wt_flat = nullptr;
+    hipStream_t wt_stream = nullptr;
+    hipEvent_t ev_wt = nullptr;
     // fetch state
     const char *src = nullptr;          // header of the snapshot to average with
     bool src_copied = false;
@@ -231,6 +245,7 @@ int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype
         if ((e = hipEventCreateWithFlags(&l->ev_fetched, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_consumed, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_factor, hipEventDisableTiming)) != hipSuccess) break;
+        if ((e = hipEventCreateWithFlags(&l->ev_wt, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipHostMalloc((void **)&l->host_status, sizeof(int32_t), hipHostMallocMapped)) != hipSuccess) break;
         *l->host_status = 0;
         if ((e = hipHostGetDevicePointer((void **)&l->host_status_dev, l->host_status, 0)) != hipSuccess) break;
@@ -271,6 +286,7 @@ int dpwa_learner_destroy(dpwa_learner *l)
     if (l->ev_fetched) (void)hipEventDestroy(l->ev_fetched);
     if (l->ev_consumed) (void)hipEventDestroy(l->ev_consumed);
     if (l->ev_factor) (void)hipEventDestroy(l->ev_factor);
+    if (l->ev_wt) (void)hipEventDestroy(l->ev_wt);
     if (l->host_status) (void)hipHostFree(l->host_status);
     if (l->slots) (void)hipFree(l->slots);
     if (l->staging) (void)hipFree(l->staging);
@@ -279,24 +295,66 @@ int dpwa_learner_destroy(dpwa_learner *l)
     return DPWA_OK;
 }
 
+// Local learners that read slot k (two publishes ago) must have finished before it is
+// rewritten (WAR); the wait is enqueued on `s` only for readers on another stream.
+static int wait_slot_readers(dpwa_learner *l, int k, hipStream_t s)
+{
+    std::lock_guard<std::mutex> g(l->readers_mu);
+    for (dpwa_learner *r : l->readers[k]) {
+        if (r->have_fetch && r->src_owner == l && r->src_slot == k)
+            return set_error(DPWA_ERR_STATE,
+                             "a peer still has an unconsumed fetch of the snapshot slot about to be rewritten "
+                             "(publish at most once per round)");
+        if (r->consumed_once && r->consume_stream != s) {
+            DeviceGuard rg(r->device);
+            HIP_TRY(hipEventRecord(r->ev_consumed, r->consume_stream));
+            HIP_TRY(hipStreamWaitEvent(s, r->ev_consumed, 0));
+        }
+    }
+    l->readers[k].clear();
+    return DPWA_OK;
+}
+
+static int publish_impl(dpwa_learner *l, const void *flat, double loss, const double *loss_dev, hipStream_t s,
+                        bool reuse)
+{
+    const int k = (int)(l->version % 2);   // slot of publish number version+1
+    char *slot = l->slots + (size_t)k * l->slot_stride;
+    const bool header_only = reuse && l->wt_valid && l->wt_flat == flat;
+    if (header_only) {
+        // the payload was written by the last average (readers of slot k were waited for then)
+        if (l->wt_stream != s) {
+            HIP_TRY(hipEventRecord(l->ev_wt, l->wt_stream));
+            HIP_TRY(hipStreamWaitEvent(s, l->ev_wt, 0));
+        }
+        HIP_TRY(launch_publish_header(slot, l->n, l->dtype, &l->ctl->clock[l->cur], loss, loss_dev, l->version + 1,
+                                      l->exported, s));
+    } else {
+        int rc = wait_slot_readers(l, k, s);
+        if (rc) return rc;
+        HIP_TRY(launch_publish(slot, flat, (int64_t)l->payload_bytes, l->n, l->dtype, &l->ctl->clock[l->cur], loss,
+                               loss_dev, l->version + 1, l->exported, s));
+    }
+    l->wt_valid = false;
+    l->publish_stream[k] = s;
+    l->published[k] = true;
+    l->version++;
+    return DPWA_OK;
+}
+
 int dpwa_learner_publish(dpwa_learner *l, const void *flat, double loss, const double *loss_dev, dpwa_stream_t stream)
 {
     if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_publish: NULL argument");
     DeviceGuard dg(l->device);
-    hipStream_t s = (hipStream_t)stream;
-    const int k = (int)(l->version % 2);   // slot of publish number version+1
-    // Local learners that read slot k (two publishes ago) must have finished.
-    {
-        std::lock_guard<std::mutex> g(l->readers_mu);
-        for (dpwa_learner *r : l->readers[k]) HIP_TRY(hipStreamWaitEvent(s, r->ev_consumed, 0));
-        l->readers[k].clear();
-    }
-    char *slot = l->slots + (size_t)k * l->slot_stride;
-    HIP_TRY(launch_publish(slot, flat, (int64_t)l->payload_bytes, l->n, l->dtype, &l->ctl->clock[l->cur], loss,
-                           loss_dev, l->version + 1, l->exported, s));
-    HIP_TRY(hipEventRecord(l->ev_published[k], s));
-    l->version++;
-    return DPWA_OK;
+    return publish_impl(l, flat, loss, loss_dev, (hipStream_t)stream, false);
+}
+
+int dpwa_learner_publish_reuse(dpwa_learner *l, const void *flat, double loss, const double *loss_dev,
+                               dpwa_stream_t stream)
+{
+    if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_publish_reuse: NULL argument");
+    DeviceGuard dg(l->device);
+    return publish_impl(l, flat, loss, loss_dev, (hipStream_t)stream, true);
 }
 
 int dpwa_learner_version(const dpwa_learner *l, uint64_t *version)
@@ -393,7 +451,13 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
     const char *peer_slot = ep.base + (size_t)k * (size_t)ep.slot_stride;
     if (ep.kind == 1) {
         // RAW: the peer's publish of that slot must be complete before anyone reads it.
-        HIP_TRY(hipStreamWaitEvent(s, ep.local->ev_published[k], 0));
+        dpwa_learner *pl = ep.local;
+        if (!pl->published[k]) return set_error(DPWA_ERR_STATE, "dpwa_learner_fetch: peer %d slot %d never published", peer_id, k);
+        if (pl->publish_stream[k] != s) {
+            DeviceGuard pg(pl->device);
+            HIP_TRY(hipEventRecord(pl->ev_published[k], pl->publish_stream[k]));
+            HIP_TRY(hipStreamWaitEvent(s, pl->ev_published[k], 0));
+        }
         std::lock_guard<std::mutex> g(ep.local->readers_mu);
         auto &rv = ep.local->readers[k];
         if (std::find(rv.begin(), rv.end(), l) == rv.end()) rv.push_back(l);
@@ -405,7 +469,10 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
         HIP_TRY(hipEventRecord(l->ev_issue, s));
         HIP_TRY(hipStreamWaitEvent(l->side, l->ev_issue, 0));
         // WAR on our own staging buffer: the previous average must have consumed it.
-        HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
+        if (l->consumed_once && l->consume_stream != s) {
+            HIP_TRY(hipEventRecord(l->ev_consumed, l->consume_stream));
+            HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
+        }
         HIP_TRY(hipMemcpyAsync(l->staging, peer_slot, kHeader + l->payload_bytes, hipMemcpyDefault, l->side));
         HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
         l->src = l->staging;
@@ -433,6 +500,8 @@ int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dp
     if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
     HIP_TRY(launch_factor(fused_args(l, loss, loss_dev), s));
     HIP_TRY(hipEventRecord(l->ev_factor, s));
+    l->consume_stream = s;   // the header has been read on s
+    l->consumed_once = true;
     l->cur ^= 1;
     l->have_factor = true;
     return DPWA_OK;
@@ -452,7 +521,32 @@ int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream)
     DeviceGuard dg(l->device);
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(launch_lerp(l->dtype, flat, l->src + kHeader, l->n, &l->ctl->coef, 0.f, 0.f, s));
-    HIP_TRY(hipEventRecord(l->ev_consumed, s));
+    l->wt_valid = false;
+    l->consume_stream = s;
+    l->consumed_once = true;
+    finish_fetch(l);
+    return DPWA_OK;
+}
+
+static int average_impl(dpwa_learner *l, void *flat, double loss, const double *loss_dev, hipStream_t s,
+                        bool write_through)
+{
+    if (!l->have_fetch || l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_average: no fetch in flight");
+    char *snap = nullptr;
+    if (write_through) {
+        const int k = (int)(l->version % 2);   // slot of the next publish
+        int rc = wait_slot_readers(l, k, s);
+        if (rc) return rc;
+        snap = l->slots + (size_t)k * l->slot_stride + kHeader;
+    }
+    if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
+    HIP_TRY(launch_average(l->dtype, flat, l->src + kHeader, l->n, fused_args(l, loss, loss_dev), snap, s));
+    l->consume_stream = s;
+    l->consumed_once = true;
+    l->cur ^= 1;
+    l->wt_valid = write_through;
+    l->wt_flat = flat;
+    l->wt_stream = s;
     finish_fetch(l);
     return DPWA_OK;
 }
@@ -460,13 +554,21 @@ int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream)
 int dpwa_learner_average(dpwa_learner *l, void *flat, double loss, const double *loss_dev, dpwa_stream_t stream)
 {
     if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_average: NULL argument");
-    if (!l->have_fetch || l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_average: no fetch in flight");
     DeviceGuard dg(l->device);
-    hipStream_t s = (hipStream_t)stream;
-    if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
-    HIP_TRY(launch_average(l->dtype, flat, l->src + kHeader, l->n, fused_args(l, loss, loss_dev), s));
-    HIP_TRY(hipEventRecord(l->ev_consumed, s));
-    l->cur ^= 1;
+    return average_impl(l, flat, loss, loss_dev, (hipStream_t)stream, false);
+}
+
+int dpwa_learner_average_through(dpwa_learner *l, void *flat, double loss, const double *loss_dev,
+                                 dpwa_stream_t stream)
+{
+    if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_average_through: NULL argument");
+    DeviceGuard dg(l->device);
+    return average_impl(l, flat, loss, loss_dev, (hipStream_t)stream, true);
+}
+
+int dpwa_learner_cancel(dpwa_learner *l)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_cancel: NULL learner");
     finish_fetch(l);
     return DPWA_OK;
 }

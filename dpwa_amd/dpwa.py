@@ -13,6 +13,7 @@ protocol and error behaviour as the reference.  What moves:
   raised at the next call (or at :meth:`synchronize`), because raising at the call itself
   would need a host sync every round.
 """
+import ctypes
 import logging
 
 import torch
@@ -21,12 +22,11 @@ import yaml
 from . import _lib
 from .group import default_group
 from .interpolation import INTERPOLATION_METHODS
-from .learner import Learner
-from .sched import Scheduler
+from .learner import DTYPES, Learner, loss_args
+from .sched import Scheduler, seed_key
 
 LOGGER = logging.getLogger(__name__)
 
-MAX_FETCH_ATTEMPTS = 100000   # the reference loops forever when every peer keeps timing out
 
 
 class Struct:
@@ -128,6 +128,7 @@ class DpwaConnection:
                 self.peers += [node]
                 self._peer_node_index.append(i)
         self.me   # AttributeError for a name that is not in the config, as the reference
+        self._peer_index = {p.name: k for k, p in enumerate(self.peers)}
 
         # Interpolation method (dpwa.py:75-80)
         interpolation_method, interpolation_config = self.config.get_interpolation()
@@ -138,18 +139,39 @@ class DpwaConnection:
         self.divergence_threshold = self.config.get_divergence_threshold()
         self.timeout_ms = self.config.get_timeoutms()
 
-        # TxThread's replacement: the scheduler (conn.py:197-334)
+        # The native node: TxThread's scheduler (conn.py:197-334) + the learner, bound at
+        # the first update_send (the reference's connection never sees the model either).
         if seed is None:
             seed = self.config.get_seed(name)
-        self._sched = Scheduler(len(self.peers), seed, self.fetch_probability)
-        self._status_buf = self._sched.status_buffer()
-        self._faults = {}
-        self._attached = {}
+        lib = _lib.load()
+        self._lib = lib
+        self._node = ctypes.c_void_p()
+        cfg = self.interpolation.device_config(self.divergence_threshold)
+        if seed is None:
+            _lib.call("dpwa_node_create", ctypes.byref(self._node), len(self.peers), None, -1,
+                      float(self.fetch_probability), ctypes.byref(cfg))
+        else:
+            key = seed_key(seed)
+            arr = (ctypes.c_uint32 * max(1, len(key)))(*key)
+            _lib.call("dpwa_node_create", ctypes.byref(self._node), len(self.peers), arr, len(key),
+                      float(self.fetch_probability), ctypes.byref(cfg))
+        sched = ctypes.c_void_p()
+        _lib.call("dpwa_node_handles", self._node, None, ctypes.byref(sched))
+        self._sched = Scheduler(len(self.peers), handle=sched.value)
         self._learner = None
-        self._fetch_peer = -1
-        self._fetch_started = False
-        self.last_fetch_attempts = 0
+        self._out = ctypes.c_int()
+        self._out_ref = ctypes.byref(self._out)
+        self._f_update_send = lib.dpwa_node_update_send
+        self._f_publish = lib.dpwa_node_publish
+        self._f_gate = lib.dpwa_node_gate
+        self._f_wait = lib.dpwa_node_update_wait
+        self._f_wait_avg = lib.dpwa_node_update_wait_average
+        self._f_lerp = lib.dpwa_node_lerp
+        self._raw_stream = torch._C._cuda_getCurrentRawStream
         self._group = group if group is not None else default_group(config_file, self.nodes, name)
+        self._eager = bool(self._group.eager_fetch)
+        self._flags = (_lib.FLAG_EAGER if self._group.eager_fetch else 0) | \
+                      (_lib.FLAG_ZERO_COPY if self._group.zero_copy else 0)
         self._group.join(self)
 
     # ---------------------------------------------------------------- reference API
@@ -159,48 +181,73 @@ class DpwaConnection:
 
     def remove_peer(self, name):
         """dpwa.py:98-99 -> TxThread.remove_peer (conn.py:215-222): permanent."""
-        k = self._peer_by_name(name)
-        _lib.call("dpwa_sched_remove", self._sched._h, k)
+        _lib.call("dpwa_sched_remove", self._sched._h, self._peer_by_name(name))
 
-    def update_send(self, parameters, loss):
+    def update_send(self, parameters, loss, reuse_snapshot=False):
         """dpwa.py:104-123: publish (clock += 1, snapshot + {clock, loss}), then the
-        Bernoulli fetch gate; under a DistGroup the fetch starts here on the side stream."""
+        Bernoulli fetch gate; under a DistGroup the fetch starts here on the side stream.
+
+        reuse_snapshot (extension): the caller asserts `parameters` is unchanged since the
+        last ``update_wait_average(..., write_through=True)``; the publish then writes only
+        the header, the payload having been written by that average."""
         learner = self._learner
         if learner is None:
             learner = self._bind(parameters)
         elif learner.take_status():
             self._zero_division()
-        stream = torch.cuda.current_stream(learner.device)
-        learner.publish(parameters, loss, stream)
-        self._group.after_publish(self, stream)
-        self._fetch_started = False
-        self._fetch_peer = -1
-        if self._sched.bernoulli():
-            LOGGER.debug("update_send(): starting fetch parameters request")
-            self.fetching = True
-            if self._group.eager_fetch:
-                self._start_fetch(stream)
+        p = learner._ptr(parameters)
+        h, d, learner._keep = loss_args(loss, learner.device)
+        s = self._raw_stream(learner.device.index)
+        flags = self._flags | (_lib.FLAG_REUSE_SNAPSHOT if reuse_snapshot else 0)
+        if self._eager:      # DistGroup: publish, stream-ordered barrier, gate + eager pull
+            rc = self._f_publish(self._node, p, h, d, flags, s)
+            if rc:
+                self._fail("dpwa_node_publish", rc)
+            self._group.after_publish(self)
+            rc = self._f_gate(self._node, flags, s, self._out_ref)
         else:
-            self.fetching = False
+            rc = self._f_update_send(self._node, p, h, d, flags, s, self._out_ref)
+        if rc:
+            self._fail("dpwa_node_update_send", rc)
+        learner.version += 1
+        self.fetching = bool(self._out.value)
 
     def update_wait(self, loss):
         """dpwa.py:125-156: (None, 0) when not fetching or no peer delivered; otherwise the
         fetched snapshot and the device factor (the clock is updated on the device)."""
-        stream = self._finish_fetch()
-        if stream is None:
+        learner = self._learner
+        if learner is None:
             return None, 0
-        self._learner.factor(loss, stream)
-        return PeerSnapshot(self, self._fetch_peer, self._fetch_version), DeviceFactor(self._learner)
+        if learner.take_status():
+            self._zero_division()
+        h, d, learner._keep = loss_args(loss, learner.device)
+        rc = self._f_wait(self._node, h, d, self._flags, self._raw_stream(learner.device.index), self._out_ref)
+        if rc:
+            self._fail("dpwa_node_update_wait", rc)
+        self.fetching = False
+        return self._result()
 
-    def update_wait_average(self, parameters, loss):
+    def update_wait_average(self, parameters, loss, write_through=False):
         """update_wait + the adapter's averaging (pytorch.py:60-68) as one fused kernel:
         the factor is evaluated inside the lerp.  Same results as update_wait() followed by
-        average(); returns what update_wait returns."""
-        stream = self._finish_fetch()
-        if stream is None:
+        average(); returns what update_wait returns.
+
+        write_through (extension): the kernel also stores the averaged parameters into the
+        next snapshot slot, so a following ``update_send(..., reuse_snapshot=True)`` moves
+        no payload (4*n*s bytes for the round's averaging + publish instead of 5*n*s)."""
+        learner = self._learner
+        if learner is None:
             return None, 0
-        self._learner.average(parameters, loss, stream)
-        return PeerSnapshot(self, self._fetch_peer, self._fetch_version), DeviceFactor(self._learner)
+        if learner.take_status():
+            self._zero_division()
+        p = learner._ptr(parameters)
+        h, d, learner._keep = loss_args(loss, learner.device)
+        flags = self._flags | (_lib.FLAG_WRITE_THROUGH if write_through else 0)
+        rc = self._f_wait_avg(self._node, p, h, d, flags, self._raw_stream(learner.device.index), self._out_ref)
+        if rc:
+            self._fail("dpwa_node_update_wait_average", rc)
+        self.fetching = False
+        return self._result()
 
     # ---------------------------------------------------------------- extensions
     @property
@@ -212,7 +259,11 @@ class DpwaConnection:
 
     def average(self, parameters, stream=None):
         """The lerp of pytorch.py:68 with the coefficients of the last update_wait."""
-        self._learner.lerp(parameters, stream if stream is not None else torch.cuda.current_stream(self._learner.device))
+        learner = self._learner
+        s = stream.cuda_stream if stream is not None else self._raw_stream(learner.device.index)
+        rc = self._f_lerp(self._node, learner._ptr(parameters), s)
+        if rc:
+            self._fail("dpwa_node_lerp", rc)
 
     def synchronize(self):
         """Waits for the device and raises a deferred ZeroDivisionError, if any."""
@@ -225,70 +276,75 @@ class DpwaConnection:
         'dead' (unrecoverable) or 'no_state'; None clears it."""
         codes = {"down": _lib.PEER_DOWN, "slow": _lib.PEER_SLOW, "dead": _lib.PEER_DEAD,
                  "no_state": _lib.PEER_NO_STATE, "ready": _lib.PEER_READY}
-        self._peer_by_name(peer_name)
-        if status is None:
-            self._faults.pop(peer_name, None)
-        else:
-            self._faults[peer_name] = codes[status]
+        _lib.call("dpwa_node_set_fault", self._node, self._peer_by_name(peer_name),
+                  -1 if status is None else codes[status])
 
     def flow_control_scores(self):
         return {p.name: self._sched.score(k) for k, p in enumerate(self.peers)}
+
+    @property
+    def last_fetch_attempts(self):
+        return self._info()[3]
+
+    @property
+    def last_fetch_peer(self):
+        k = self._info()[1]
+        return None if k < 0 else self.peers[k].name
 
     def peer_rank(self, k):
         return self._peer_node_index[k]
 
     def close(self):
-        self._group.leave(self)
-        if self._learner is not None:
-            self._learner.close()
+        group = getattr(self, "_group", None)
+        if group is not None:
+            group.leave(self)
+            self._group = None
+        if getattr(self, "_learner", None) is not None:
+            self._learner._h = None      # borrowed from the node
             self._learner = None
+        node = getattr(self, "_node", None)
+        if node is not None and node.value and _lib._lib is not None:
+            _lib._lib.dpwa_node_destroy(node)
+        self._node = None
 
     # ---------------------------------------------------------------- internals
     def _peer_by_name(self, name):
-        for k, p in enumerate(self.peers):
-            if p.name == name:
-                return k
-        raise KeyError(name)
+        k = self._peer_index.get(name)
+        if k is None:
+            raise KeyError(name)
+        return k
+
+    def _set_peer(self, k, kind, other):
+        _lib.call("dpwa_node_set_peer", self._node, k, kind, other._node if other is not None else None)
+
+    def _info(self):
+        fetching, peer, att = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        version = ctypes.c_uint64()
+        _lib.call("dpwa_node_info", self._node, ctypes.byref(fetching), ctypes.byref(peer), ctypes.byref(version),
+                  ctypes.byref(att))
+        return bool(fetching.value), peer.value, version.value, att.value
+
+    def _result(self):
+        k = self._out.value
+        if k < 0:
+            return None, 0
+        return PeerSnapshot(self, k, self._learner.version), DeviceFactor(self._learner)
+
+    def _fail(self, name, rc):
+        raise _lib.DpwaError(name, rc, self._lib.dpwa_last_error().decode(errors="replace"))
 
     def _bind(self, parameters):
         if not isinstance(parameters, torch.Tensor) or parameters.device.type != "cuda":
             raise TypeError("DpwaConnection.update_send expects the flat parameter buffer as a GPU tensor")
-        cfg = self.interpolation.device_config(self.divergence_threshold)
-        self._learner = Learner(parameters.device, parameters.numel(), parameters.dtype, cfg)
+        if parameters.dtype not in DTYPES:
+            raise TypeError("dpwa averages float32 or bfloat16 parameters, got %s" % parameters.dtype)
+        _lib.call("dpwa_node_bind", self._node, parameters.device.index, parameters.numel(),
+                  DTYPES[parameters.dtype])
+        h = ctypes.c_void_p()
+        _lib.call("dpwa_node_handles", self._node, ctypes.byref(h), None)
+        self._learner = Learner(parameters.device, parameters.numel(), parameters.dtype, handle=h.value)
         self._group.on_bind(self)
         return self._learner
-
-    def _finish_fetch(self):
-        """dpwa.py:130-137: returns the stream to average on, or None for "no data"."""
-        learner = self._learner
-        if learner is not None and learner.take_status():
-            self._zero_division()
-        if not self.fetching:
-            return None
-        self.fetching = False
-        stream = torch.cuda.current_stream(learner.device)
-        if not self._fetch_started:
-            self._start_fetch(stream)
-        if self._fetch_peer < 0:
-            return None
-        return stream
-
-    def _start_fetch(self, stream):
-        """TxThread.run for one queue item (conn.py:277-315) + the pull itself."""
-        self._fetch_started = True
-        status = self._status_buf
-        group = self._group
-        for k, p in enumerate(self.peers):
-            st = self._faults.get(p.name) if self._faults else None
-            status[k] = group.peer_status(self, p.name) if st is None else st
-        k, attempts = self._sched.fetch_into(status, MAX_FETCH_ATTEMPTS)
-        self.last_fetch_attempts = attempts
-        self._fetch_peer = k
-        if k < 0:
-            return
-        version, zero_copy = group.prepare_fetch(self, k)
-        self._fetch_version = version
-        self._learner.fetch(k, version, zero_copy, stream)
 
     def _zero_division(self):
         raise ZeroDivisionError("float division by zero (interpolation factor, dpwa.py:143-147)")

@@ -1,16 +1,16 @@
-"""Gossip groups: how a DpwaConnection finds its peers' snapshots.
+"""Gossip groups: how a DpwaConnection's node reaches its peers' snapshots.
 
 The reference finds peers by (host, port) from the YAML and fetches over TCP
 (dpwa/conn.py:208-213, 246-251, 297-298).  On MI355X a node is a learner on a GPU and a
-fetch is a device-to-device pull, so a group answers three questions for the scheduler:
-who is up, who has published (the reference's ``have_state``, conn.py:106), and where a
-peer's snapshot lives.
+fetch is a device-to-device pull; a group only wires the native nodes' peer tables
+(dpwa_node_set_peer) -- the per-round logic runs in C++ (dpwa_amd/csrc/node.cpp).
 
 ``LocalGroup``  every node of the config lives in this process (single-GPU multi-learner
-                runs, tests).  A node that has not been constructed yet is "down" (the
-                reference's ConnectionRefusedError); one that has not published is
-                "no state" (the empty reply).  Fetches are resolved at update_wait, after
-                every learner of the round has published (lock-step order).
+                runs, tests).  A node that has not been constructed yet is unreachable
+                (the reference's ConnectionRefusedError); one that has not published
+                answers with no state (the empty reply).  Fetches are resolved at
+                update_wait, after every learner of the round has published (lock-step
+                order); a same-device peer's slot is read in place (no copy).
 ``DistGroup``   one node per torch.distributed rank, rank == node index in the YAML, one
                 GPU per rank.  Snapshot slots are exported with hipIpcGetMemHandle and
                 mapped by every peer at the first publish; each round is lock-step: a
@@ -44,47 +44,45 @@ class LocalGroup:
     def __init__(self):
         self.members = {}
 
-    def join(self, conn):
-        old = self.members.get(conn.name)
-        if old is not None and old() is not None and old() is not conn:
-            raise OSError(98, "node %r is already bound in this process" % conn.name)   # EADDRINUSE
-        self.members[conn.name] = weakref.ref(conn)
-
-    def leave(self, conn):
-        ref = self.members.get(conn.name)
-        if ref is not None and ref() is conn:
-            del self.members[conn.name]
-
     def member(self, name):
         ref = self.members.get(name)
         return ref() if ref is not None else None
 
+    def join(self, conn):
+        old = self.member(conn.name)
+        if old is not None and old is not conn:
+            raise OSError(98, "node %r is already bound in this process" % conn.name)   # EADDRINUSE
+        self.members[conn.name] = weakref.ref(conn)
+        for k, p in enumerate(conn.peers):          # wire both directions
+            other = self.member(p.name)
+            if other is None:
+                continue
+            conn._set_peer(k, _lib.NODE_PEER_LOCAL, other)
+            j = other._peer_index.get(conn.name)
+            if j is not None:
+                other._set_peer(j, _lib.NODE_PEER_LOCAL, conn)
+
+    def leave(self, conn):
+        if self.member(conn.name) is not conn:
+            return
+        del self.members[conn.name]
+        for name in list(self.members):
+            other = self.member(name)
+            j = other._peer_index.get(conn.name) if other is not None else None
+            if j is not None:
+                other._set_peer(j, _lib.NODE_PEER_UNSET, None)
+
     def on_bind(self, conn):
         pass
 
-    def after_publish(self, conn, stream):
+    def after_publish(self, conn):
         pass
-
-    def peer_status(self, conn, peer_name):
-        peer = self.member(peer_name)
-        if peer is None:
-            return _lib.PEER_DOWN
-        if peer._learner is None or peer._learner.version == 0:
-            return _lib.PEER_NO_STATE
-        return _lib.PEER_READY
-
-    def prepare_fetch(self, conn, peer_index):
-        peer = self.member(conn.peers[peer_index].name)
-        key = ("local", id(peer._learner))
-        if conn._attached.get(peer_index) != key:
-            conn._learner.attach_local(peer_index, peer._learner)
-            conn._attached[peer_index] = key
-        return peer._learner.version, self.zero_copy
 
 
 class DistGroup:
     """One learner per rank; see the module docstring."""
     eager_fetch = True
+    zero_copy = False
 
     def __init__(self, nodes, name, process_group=None):
         import torch.distributed as dist
@@ -101,7 +99,7 @@ class DistGroup:
         self._flag = None
 
     def join(self, conn):
-        self.index = {p.name: i for i, p in enumerate(conn.peers)}
+        pass
 
     def leave(self, conn):
         pass
@@ -111,10 +109,9 @@ class DistGroup:
         handle = conn._learner.ipc_handle()
         handles = [None] * self.world
         self.dist.all_gather_object(handles, handle, group=self.pg)
-        for k, peer in enumerate(conn.peers):
-            r = conn.peer_rank(k)
-            conn._learner.attach_ipc(k, handles[r])
-            conn._attached[k] = ("ipc", r)
+        for k in range(len(conn.peers)):
+            conn._learner.attach_ipc(k, handles[conn.peer_rank(k)])
+            conn._set_peer(k, _lib.NODE_PEER_REMOTE, None)
 
     def barrier(self, device):
         """Stream-ordered on RCCL (the current stream waits; the host does not)."""
@@ -126,18 +123,10 @@ class DistGroup:
             torch.cuda.current_stream(device).synchronize()
             self.dist.barrier(group=self.pg)
 
-    def after_publish(self, conn, stream):
+    def after_publish(self, conn):
         # Every peer's publish of this round is complete (and their fetches of the slot we
-        # are about to rewrite two rounds from now are ordered before it) once this returns
-        # on `stream`.
+        # rewrite two rounds from now are ordered before it) once this returns on the stream.
         self.barrier(conn._learner.device)
-
-    def peer_status(self, conn, peer_name):
-        return _lib.PEER_READY
-
-    def prepare_fetch(self, conn, peer_index):
-        # lock-step: every rank has published exactly as often as this one
-        return conn._learner.version, False
 
 
 def default_group(config_file, nodes, name):

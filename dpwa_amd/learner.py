@@ -28,7 +28,8 @@ def loss_args(loss, device):
 
 
 class Learner:
-    def __init__(self, device, numel, dtype, interp_cfg):
+    def __init__(self, device, numel, dtype, interp_cfg=None, handle=None):
+        """Creates a learner, or wraps (without owning) `handle` from dpwa_node_handles."""
         if dtype not in DTYPES:
             raise TypeError("dpwa averages float32 or bfloat16 parameters, got %s" % dtype)
         self.device = torch.device(device)
@@ -36,9 +37,13 @@ class Learner:
         self.dtype = dtype
         lib = _lib.load()
         self._lib = lib
-        self._h = ctypes.c_void_p()
-        _lib.call("dpwa_learner_create", ctypes.byref(self._h), self.device.index, self.numel, DTYPES[dtype],
-                  ctypes.byref(interp_cfg))
+        self._owned = handle is None
+        if handle is None:
+            self._h = ctypes.c_void_p()
+            _lib.call("dpwa_learner_create", ctypes.byref(self._h), self.device.index, self.numel, DTYPES[dtype],
+                      ctypes.byref(interp_cfg))
+        else:
+            self._h = ctypes.c_void_p(handle)
         clock, coef, sh, sp = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
         _lib.call("dpwa_learner_pointers", self._h, ctypes.byref(clock), ctypes.byref(coef), ctypes.byref(sh),
                   ctypes.byref(sp))
@@ -61,7 +66,7 @@ class Learner:
         return self._h
 
     def close(self):
-        if self._h is not None and self._h.value and _lib._lib is not None:
+        if self._owned and self._h is not None and self._h.value and _lib._lib is not None:
             _lib._lib.dpwa_learner_destroy(self._h)
         self._h = None
 
@@ -119,6 +124,9 @@ class Learner:
         rc = self._f_lerp(self._h, self._ptr(flat), stream.cuda_stream)
         if rc:
             self._fail("dpwa_learner_lerp", rc)
+
+    def cancel(self):
+        _lib.call("dpwa_learner_cancel", self._h)
 
     def average(self, flat, loss, stream):
         """Fused factor + lerp (one kernel)."""

@@ -28,9 +28,12 @@ def seed_key(seed):
 
 
 class Scheduler:
-    def __init__(self, n_peers, seed=None, fetch_probability=1.0):
-        self._h = ctypes.c_void_p()
-        if seed is None:
+    def __init__(self, n_peers, seed=None, fetch_probability=1.0, handle=None):
+        self._owned = handle is None
+        self._h = ctypes.c_void_p() if handle is None else ctypes.c_void_p(handle)
+        if handle is not None:
+            pass
+        elif seed is None:
             _lib.call("dpwa_sched_create", ctypes.byref(self._h), n_peers, None, -1, float(fetch_probability))
         else:
             key = seed_key(seed)
@@ -43,7 +46,7 @@ class Scheduler:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h and h.value and _lib._lib is not None:
+        if getattr(self, "_owned", False) and h and h.value and _lib._lib is not None:
             _lib._lib.dpwa_sched_destroy(h)
             self._h = None
 

@@ -152,10 +152,23 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
 int dpwa_learner_average(dpwa_learner *l, void *flat, double loss, const double *loss_dev,
                          dpwa_stream_t stream);
 
+/* Write-through form: the averaged parameters are also stored into the slot of the NEXT
+ * publish (4*n*s bytes instead of 3*n*s here, and that publish then moves no payload). */
+int dpwa_learner_average_through(dpwa_learner *l, void *flat, double loss, const double *loss_dev,
+                                 dpwa_stream_t stream);
+/* Publish that reuses a write-through snapshot when the last average wrote `flat` through
+ * (the caller asserts `flat` is unchanged since): header only; otherwise a full publish. */
+int dpwa_learner_publish_reuse(dpwa_learner *l, const void *flat, double loss, const double *loss_dev,
+                               dpwa_stream_t stream);
+
 /* Split form of dpwa_learner_average for the DpwaConnection / adapter seam:
  * factor only (update_wait's return value), then lerp with the learner's coefficients. */
 int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dpwa_stream_t stream);
 int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream);
+
+/* Abandons a fetch whose factor was computed but whose lerp will never be issued (the
+ * caller of update_wait chose not to average); the snapshot it read may then be reused. */
+int dpwa_learner_cancel(dpwa_learner *l);
 
 /* Device pointers of the learner's blocks.  The clock is double-buffered: *clock_dev is the
  * live one and stays valid until the next factor/average.  status_word: the pinned host
@@ -222,6 +235,58 @@ int dpwa_sched_n_live(const dpwa_sched *s, int *n_live);
 /* raw CPython-equivalent draws, for tests: random.random(), random.randint(a, b) */
 int dpwa_sched_random(dpwa_sched *s, double *out);
 int dpwa_sched_randint(dpwa_sched *s, int64_t a, int64_t b, int64_t *out);
+
+/* ------------------------------------------------------------------------------------
+ * Node: DpwaConnection's per-round logic (dpwa/dpwa.py:54-156) in native code -- the
+ * scheduler, the learner (bound at the first publish) and a peer table.  One call per
+ * half-round keeps the host cost of a gossip round to a few microseconds.
+ * ------------------------------------------------------------------------------------ */
+typedef struct dpwa_node dpwa_node;
+
+#define DPWA_NODE_PEER_UNSET 0    /* not reachable: a fetch is refused (conn.py:253-256)      */
+#define DPWA_NODE_PEER_LOCAL 1    /* another node of this process (any device)                */
+#define DPWA_NODE_PEER_REMOTE 2   /* IPC-attached learner of another process, lock-step rounds */
+
+/* flags of the node calls */
+#define DPWA_FLAG_EAGER 1            /* update_send/gate: start a granted fetch now (DistGroup)    */
+#define DPWA_FLAG_ZERO_COPY 2        /* read a same-device local peer's slot in place              */
+#define DPWA_FLAG_REUSE_SNAPSHOT 4   /* publish: flat unchanged since a write-through average      */
+#define DPWA_FLAG_WRITE_THROUGH 8    /* update_wait_average: also write the next snapshot          */
+
+/* DpwaConnection.__init__ (dpwa.py:54-93) minus the model: scheduler seeded as
+ * dpwa_sched_create, the interpolation config for the learner bound later. */
+int dpwa_node_create(dpwa_node **out, int n_peers, const uint32_t *seed_key, int key_len,
+                     double fetch_probability, const dpwa_interp *cfg);
+int dpwa_node_destroy(dpwa_node *n);
+/* Creates the node's learner for an n-element flat buffer of `dtype` on `device`. */
+int dpwa_node_bind(dpwa_node *n, int device, int64_t numel, int32_t dtype);
+/* Borrowed handles of the node's learner (NULL before bind) and scheduler. */
+int dpwa_node_handles(dpwa_node *n, dpwa_learner **learner, dpwa_sched **sched);
+/* How peer `peer` (scheduler index) is reached: DPWA_NODE_PEER_*; `local` for LOCAL. */
+int dpwa_node_set_peer(dpwa_node *n, int peer, int kind, dpwa_node *local);
+/* Fault injection: force a DPWA_PEER_* status for a peer, -1 clears. */
+int dpwa_node_set_fault(dpwa_node *n, int peer, int status);
+
+/* update_send (dpwa.py:104-123): publish, then the Bernoulli gate; with DPWA_FLAG_EAGER a
+ * granted fetch starts now (peer choice + pull on the side stream), else at update_wait.
+ * Split form: publish, then (after a caller-side barrier) gate. */
+int dpwa_node_update_send(dpwa_node *n, const void *flat, double loss, const double *loss_dev, int flags,
+                          dpwa_stream_t stream, int *fetching);
+int dpwa_node_publish(dpwa_node *n, const void *flat, double loss, const double *loss_dev, int flags,
+                      dpwa_stream_t stream);
+int dpwa_node_gate(dpwa_node *n, int flags, dpwa_stream_t stream, int *fetching);
+/* update_wait (dpwa.py:125-156): *peer = the peer averaged with, or -1 for (None, 0).
+ * _average fuses the adapter's lerp (pytorch.py:66-68) into the same kernel; the split
+ * form computes the factor only and dpwa_node_lerp applies it. */
+int dpwa_node_update_wait(dpwa_node *n, double loss, const double *loss_dev, int flags,
+                          dpwa_stream_t stream, int *peer);
+int dpwa_node_lerp(dpwa_node *n, void *flat, dpwa_stream_t stream);
+int dpwa_node_update_wait_average(dpwa_node *n, void *flat, double loss, const double *loss_dev,
+                                  int flags, dpwa_stream_t stream, int *peer);
+/* State of the current/last round: fetching flag, fetched peer (-1: none), its publish
+ * number, and the picks the last fetch took. */
+int dpwa_node_info(const dpwa_node *n, int *fetching, int *fetch_peer, uint64_t *fetch_version,
+                   int *last_attempts);
 
 #ifdef __cplusplus
 }

@@ -52,9 +52,13 @@ def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of
     for r in range(T):
         conn.update_send(flat, send[r][rank])
         flat.add_(torch.from_numpy(deltas[r, rank]).to(dev))
-        payload, factor = conn.update_wait(wait[r][rank])
+        if r % 2:
+            payload, factor = conn.update_wait(wait[r][rank])      # split: factor kernel, then lerp
+            if payload is not None:
+                conn.average(flat)
+        else:
+            payload, factor = conn.update_wait_average(flat, wait[r][rank])   # fused (adapter path)
         if payload is not None:
-            conn.average(flat)
             peers.append(payload.peer)
         else:
             peers.append(None)

@@ -78,8 +78,8 @@ def run_gossip(case, z, tmp_path, dtype=torch.float32):
         for g in range(G):
             c = adapters[g].connection
             adapters[g].update_wait(case["wait_loss"][r][g])
-            fetched = c._fetch_peer >= 0 and out["fetching"][r, g]
-            out["picks"][r][g] = [c.peers[c._fetch_peer].name] if fetched else []
+            fetched = c.last_fetch_peer is not None and out["fetching"][r, g]
+            out["picks"][r][g] = [c.last_fetch_peer] if fetched else []
             out["factors"][r, g] = float(c._learner.read_coef().factor) if fetched else 0.0
             out["clocks"][r, g] = c.clock
             out["params"][r, g] = flat_params(nets[g])
@@ -198,3 +198,151 @@ def test_peer_not_up_and_no_state_follow_reference_flow_control(tmp_path):
     a.update_send(fa, 1.0)
     payload, _ = a.update_wait(1.0)
     assert payload is None and set(a.flow_control_scores().values()) == {None}
+
+
+def test_cross_stream_ordering(tmp_path):
+    """Each learner runs on its own stream and each stream is stalled with a spin kernel
+    before it publishes / averages, so any missing RAW/WAR dependency on the snapshot
+    slots would read stale or half-written data.  Results must still equal the oracle."""
+    rng = np.random.default_rng(4)
+    G, n, T = 3, 2_000_003, 6
+    names = ["s%d" % g for g in range(G)]
+    init = rng.standard_normal((G, n)).astype(np.float32)
+    deltas = (0.01 * rng.standard_normal((T, G, n))).astype(np.float32)
+    send = [[1.0 + 0.1 * g + r for g in range(G)] for r in range(T)]
+    wait = [[1.5 + 0.1 * g + r for g in range(G)] for r in range(T)]
+    seeds = [31 + g for g in range(G)]
+    exp = ogossip.simulate(names, init, deltas, send, wait, "clock", None, 0.0, 1.0, seeds)
+    cfg = tmp_path / "streams.yaml"
+    write_cfg(cfg, names, 1.0, "clock", 0.0, None)
+    group = LocalGroup()
+    streams = [torch.cuda.Stream() for _ in range(G)]
+    flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
+    dts = [[torch.from_numpy(deltas[r, g]).to(DEV) for g in range(G)] for r in range(T)]
+    torch.cuda.synchronize()
+    conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group) for g in range(G)]
+    for r in range(T):
+        for g in range(G):
+            with torch.cuda.stream(streams[g]):
+                torch.cuda._sleep(2_000_000 * (G - g))      # later learners' streams run ahead
+                conns[g].update_send(flats[g], send[r][g])
+        for g in range(G):
+            with torch.cuda.stream(streams[g]):
+                flats[g].add_(dts[r][g])
+        for g in reversed(range(G)):
+            with torch.cuda.stream(streams[g]):
+                torch.cuda._sleep(1_000_000 * g)
+                payload, _ = conns[g].update_wait_average(flats[g], wait[r][g])
+    torch.cuda.synchronize()
+    for g in range(G):
+        assert olerp.bits_equal(flats[g].cpu().numpy(), exp["params"][-1, g]), g
+        assert conns[g].clock == exp["clocks"][-1, g]
+
+
+def test_update_wait_without_average_then_continue(tmp_path):
+    """update_wait() whose snapshot is never averaged must not block later rounds."""
+    cfg = tmp_path / "skip.yaml"
+    write_cfg(cfg, ["a", "b"], 1.0, "constant", 0.0, 0.5)
+    g = LocalGroup()
+    a = DpwaConnection("a", str(cfg), seed=1, group=g)
+    b = DpwaConnection("b", str(cfg), seed=2, group=g)
+    fa, fb = torch.ones(1024, device=DEV), torch.zeros(1024, device=DEV)
+    for r in range(4):
+        a.update_send(fa, 1.0)
+        b.update_send(fb, 1.0)
+        pa, _ = a.update_wait(1.0)          # never averaged
+        pb, f = b.update_wait(1.0)
+        b.average(fb)
+        assert pa is not None and pb is not None
+    torch.cuda.synchronize()
+    assert torch.equal(fa, torch.ones(1024, device=DEV))
+    assert a.clock == 4.0    # the clock still follows dpwa.py:150 (factor 0.5 between equal clocks)
+
+
+def test_write_through_matches_reference_trajectories(tmp_path):
+    """Adapter with write_through=True: the next snapshot is written by the averaging kernel
+    and the publish moves only the header -- trajectories stay bit-identical."""
+    meta = load_json("gossip.json")
+    z = load_npz("gossip.npz")
+    case = meta["cases"][1]
+    k = case["key"]
+    import dpwa_amd.adapters.pytorch as ap
+    orig = ap.DpwaPyTorchAdapter.__init__
+
+    def init_wt(self, net, name, cfg, **kw):
+        orig(self, net, name, cfg, write_through=True, **kw)
+
+    ap.DpwaPyTorchAdapter.__init__ = init_wt
+    try:
+        got = run_gossip(case, z, tmp_path)
+    finally:
+        ap.DpwaPyTorchAdapter.__init__ = orig
+    assert np.array_equal(got["clocks"], z[k + "_clocks"])
+    assert olerp.bits_equal(got["params"], z[k + "_params"])
+
+
+def test_write_through_detects_inplace_updates(tmp_path):
+    """An optimizer-style in-place update between update_wait and update_send bumps the
+    parameter version counters and forces a full publish (peers see the updated values)."""
+    rng = np.random.default_rng(12)
+    G, n, T = 2, 3000, 6
+    names = ["a", "b"]
+    init = rng.standard_normal((G, n)).astype(np.float32)
+    cfg = tmp_path / "wt.yaml"
+    write_cfg(cfg, names, 1.0, "constant", 0.0, 0.5)
+    group = LocalGroup()
+    nets = []
+    adapters = []
+    for g in range(G):
+        net = Net([(n,)]).to(DEV)
+        load_flat(net, init[g])
+        nets.append(net)
+        adapters.append(DpwaPyTorchAdapter(net, names[g], str(cfg), seed=5 + g, group=group, write_through=True))
+    # oracle: the same loop with the post-average update folded into the next round's delta
+    deltas = np.zeros((T, G, n), np.float32)
+    bumps = (0.5 * rng.standard_normal((T, G, n))).astype(np.float32)
+    params = init.copy()
+    from oracle.policy import OracleLearner
+    L = [OracleLearner(names[g], [names[1 - g]], 1.0, "constant", 0.5, 0.0, 5 + g) for g in range(G)]
+    for r in range(T):
+        for g in range(G):
+            adapters[g].update_send(1.0)
+        snaps = [params[g].copy() for g in range(G)]
+        for g in range(G):
+            L[g].update_send(1.0)
+        for g in range(G):
+            adapters[g].update_wait(1.0)
+            st, pl, _ = L[g].fetch(lambda p: "ok", lambda p: ("payload", {"clock": 1, "loss": 1.0}, None))
+            params[g] = olerp.lerp_f32(params[g], snaps[1 - g], 0.5)
+        for g in range(G):     # the "optimizer step" placed after update_wait
+            with torch.no_grad():
+                nets[g].p0.add_(torch.from_numpy(bumps[r, g]).to(DEV))
+            params[g] = np.add(params[g], bumps[r, g], dtype=np.float32)
+    torch.cuda.synchronize()
+    for g in range(G):
+        assert olerp.bits_equal(nets[g].p0.detach().cpu().numpy(), params[g]), g
+    del deltas
+
+
+def test_connection_write_through_and_reuse(tmp_path):
+    rng = np.random.default_rng(3)
+    G, n, T = 3, 100_001, 8
+    names = ["x%d" % g for g in range(G)]
+    init = rng.standard_normal((G, n)).astype(np.float32)
+    deltas = np.zeros((T, G, n), np.float32)
+    send = [[1.0] * G for _ in range(T)]
+    wait = [[1.0] * G for _ in range(T)]
+    seeds = [9, 10, 11]
+    exp = ogossip.simulate(names, init, deltas, send, wait, "clock", None, 0.0, 1.0, seeds)
+    cfg = tmp_path / "wt2.yaml"
+    write_cfg(cfg, names, 1.0, "clock", 0.0, None)
+    group = LocalGroup()
+    flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
+    conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group) for g in range(G)]
+    for r in range(T):
+        for g in range(G):
+            conns[g].update_send(flats[g], send[r][g], reuse_snapshot=r > 0)
+        for g in range(G):
+            conns[g].update_wait_average(flats[g], wait[r][g], write_through=True)
+    for g in range(G):
+        assert olerp.bits_equal(flats[g].cpu().numpy(), exp["params"][-1, g]), g

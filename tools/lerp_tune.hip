@@ -89,6 +89,44 @@ __global__ __launch_bounds__(BLOCK) void k_tile(f32x4 *__restrict__ param, const
     }
 }
 
+// Software-pipelined grid stride: the next item's loads are issued before this item's
+// store, so the in-order vmcnt wait for them does not also wait for the store.
+template <int BLOCK, bool NT_ST>
+__global__ __launch_bounds__(BLOCK) void k_pipe(f32x4 *__restrict__ param, const f32x4 *__restrict__ peer,
+                                                int64_t n4, float a, float b)
+{
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n4) return;
+    f32x4 q = peer[i], p = param[i];
+    for (;;) {
+        const int64_t j = i + stride;
+        f32x4 q2, p2;
+        const bool more = j < n4;
+        if (more) {
+            q2 = peer[j];
+            p2 = param[j];
+        }
+        st(param + i, lerp4(a, b, q, p), NT_ST);
+        if (!more) break;
+        q = q2;
+        p = p2;
+        i = j;
+    }
+}
+
+// One item per lane, exact grid, optional second destination (publish fused into the lerp).
+template <int BLOCK, bool DUAL, bool NT_ST>
+__global__ __launch_bounds__(BLOCK) void k_one(f32x4 *__restrict__ param, const f32x4 *__restrict__ peer,
+                                               f32x4 *__restrict__ snap, int64_t n4, float a, float b)
+{
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n4) return;
+    const f32x4 r = lerp4(a, b, peer[i], param[i]);
+    st(param + i, r, NT_ST);
+    if (DUAL) st(snap + i, r, NT_ST);
+}
+
 // Copy (1R:1W) and read-only reduction, for calibration.
 __global__ __launch_bounds__(256) void k_copy(f32x4 *__restrict__ dst, const f32x4 *__restrict__ src, int64_t n4)
 {
@@ -139,6 +177,30 @@ Variant tile(const char *name, int cap)
             }};
 }
 
+template <int BLOCK, bool NT>
+Variant pipe(const char *name, int cap)
+{
+    return {name, 3.0, [cap](float *p, float *q, int64_t n, hipStream_t s) {
+                int64_t n4 = n / 4;
+                int g = grid_for(n4, BLOCK, cap);
+                hipLaunchKernelGGL((k_pipe<BLOCK, NT>), dim3(g), dim3(BLOCK), 0, s, (f32x4 *)p, (const f32x4 *)q, n4,
+                                   0.5f, 0.5f);
+            }};
+}
+
+static float *g_snap = nullptr;
+
+template <int BLOCK, bool DUAL, bool NT>
+Variant one(const char *name)
+{
+    return {name, DUAL ? 4.0 : 3.0, [](float *p, float *q, int64_t n, hipStream_t s) {
+                int64_t n4 = n / 4;
+                int g = grid_for(n4, BLOCK, 0);
+                hipLaunchKernelGGL((k_one<BLOCK, DUAL, NT>), dim3(g), dim3(BLOCK), 0, s, (f32x4 *)p, (const f32x4 *)q,
+                                   (f32x4 *)g_snap, n4, 0.5f, 0.5f);
+            }};
+}
+
 int main(int argc, char **argv)
 {
     int64_t n = argc > 1 ? atoll(argv[1]) : 11173962;
@@ -155,25 +217,25 @@ int main(int argc, char **argv)
     }
     hipStream_t s;
     CHECK(hipStreamCreate(&s));
+    CHECK(hipMalloc(&g_snap, bytes));
     std::vector<Variant> vs = {
-        gs<256, 4, false, false, false>("gs256x4 cap2048 (product)", 2048),
+        one<256, false, false>("one256 (product)"),
+        one<512, false, false>("one512"),
+        one<1024, false, false>("one1024"),
+        one<256, false, true>("one256 ntST"),
+        one<256, true, false>("one256 DUAL (x4 bytes)"),
+        one<256, true, true>("one256 DUAL ntST (x4 bytes)"),
+        pipe<256, false>("pipe256 cap1024", 1024),
+        pipe<256, false>("pipe256 cap2048", 2048),
+        pipe<256, false>("pipe256 cap4096", 4096),
+        pipe<256, false>("pipe256 cap8192", 8192),
+        pipe<512, false>("pipe512 cap2048", 2048),
+        pipe<256, true>("pipe256 cap2048 ntST", 2048),
+        gs<256, 4, false, false, false>("gs256x4 cap2048", 2048),
         gs<256, 4, false, false, false>("gs256x4 exact", 0),
         gs<256, 2, false, false, false>("gs256x2 exact", 0),
-        gs<256, 8, false, false, false>("gs256x8 exact", 0),
-        gs<256, 1, false, false, false>("gs256x1 exact", 0),
         gs<512, 4, false, false, false>("gs512x4 exact", 0),
-        gs<1024, 2, false, false, false>("gs1024x2 exact", 0),
-        gs<256, 4, false, false, false>("gs256x4 cap1024", 1024),
-        gs<256, 4, false, false, false>("gs256x4 cap4096", 4096),
-        gs<256, 4, true, false, false>("gs256x4 exact ntQ", 0),
-        gs<256, 4, true, true, false>("gs256x4 exact ntQP", 0),
-        gs<256, 4, false, false, true>("gs256x4 exact ntST", 0),
-        gs<256, 4, true, true, true>("gs256x4 exact ntALL", 0),
         tile<256, 4, false>("tile256x4 exact", 0),
-        tile<256, 8, false>("tile256x8 exact", 0),
-        tile<256, 4, false>("tile256x4 cap2048", 2048),
-        tile<512, 4, false>("tile512x4 exact", 0),
-        tile<256, 4, true>("tile256x4 exact nt", 0),
         {"copy 1R1W (x2 bytes)", 2.0,
          [](float *p, float *q, int64_t n, hipStream_t s) {
              int64_t n4 = n / 4;
