@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
     ap.add_argument("--no-write-through", action="store_true", help="skip the write-through variant")
     ap.add_argument("--sample-every", type=int, default=4, help="time the averaging kernel every k-th step")
+    ap.add_argument("--pull", default="auto",
+                    help="N>1 fetch transport: copy (hipMemcpyAsync), kernel[:blocks], or auto (fastest of a trial)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="PMC traffic summary (rocprofv3 FETCH_SIZE/WRITE_SIZE passes) to report")
     return ap.parse_args()
@@ -213,6 +215,26 @@ def main():
             return float(tmax.item()), float(sums[0].item()), float(sums[1].item()), lerp_ms
         return elapsed, float(averaged), float(len(learners) * steps), lerp_ms
 
+    from dpwa_amd import _lib
+
+    def set_pull(mode):
+        kind, _, blocks = mode.partition(":")
+        for conn, _ in learners:
+            if conn._learner is not None:
+                _lib.call("dpwa_learner_set_pull", conn._learner.handle,
+                          _lib.PULL_KERNEL if kind == "kernel" else _lib.PULL_COPY_ENGINE, int(blocks or 512))
+
+    pull_trials = {}
+    pull = args.pull
+    if world > 1:
+        run(2, 2, False, 1000)   # binds the learners (IPC exchange) before the transport is chosen
+        modes = [args.pull] if args.pull != "auto" else ["copy", "kernel:256", "kernel:1024"]
+        for mode in modes:       # short timed trial of each transport; the fastest is used below
+            set_pull(mode)
+            el, av, _, _ = run(max(10, args.steps // 10), 2, False, 1000)
+            pull_trials[mode] = round(av * 3 * args.numel * esize / el / 1e9, 2)
+        pull = max(pull_trials, key=pull_trials.get)
+        set_pull(pull)
     elapsed, averaged, rounds, lerp_ms = run(args.steps, args.warmup, False, args.sample_every)
     wt = run(args.steps, args.warmup, True, args.sample_every) if not args.no_write_through else None
 
@@ -250,7 +272,7 @@ def main():
                 "learners_per_gpu": len(learners),
                 "numel": args.numel,
                 "transport": "in-place HBM read (co-resident peer)" if world == 1 else
-                             "hipIpc-mapped slot pulled over xGMI on a side stream",
+                             "hipIpc-mapped slot pulled over xGMI on a side stream (%s)" % pull,
                 "parallelism": "gossip x%d" % int(rounds / args.steps),
             },
             "gossip_rounds_per_s": round(rounds / elapsed, 1),
@@ -270,6 +292,8 @@ def main():
                 "traffic_source": traffic_src,
             },
         }
+        if pull_trials:
+            out["pull_trials_gbs"] = pull_trials
         if wt is not None:
             w_el, w_avg, w_rounds, w_ms = wt
             w_us = float(np.nanmean(w_ms) * 1e3)

@@ -28,6 +28,7 @@ CONNECT_OK, CONNECT_REFUSED, CONNECT_ERROR = 0, 1, 2
 REPLY_PAYLOAD, REPLY_EMPTY, REPLY_TIMEOUT, REPLY_ERROR = 3, 4, 5, 6
 PEER_READY, PEER_NO_STATE, PEER_DOWN, PEER_SLOW, PEER_DEAD = 0, 1, 2, 3, 4
 NODE_PEER_UNSET, NODE_PEER_LOCAL, NODE_PEER_REMOTE = 0, 1, 2
+PULL_COPY_ENGINE, PULL_KERNEL = 0, 1
 FLAG_EAGER, FLAG_ZERO_COPY, FLAG_REUSE_SNAPSHOT, FLAG_WRITE_THROUGH = 1, 2, 4, 8
 
 
@@ -90,6 +91,7 @@ SIGNATURES = {
     "dpwa_learner_factor": [_vp, _dbl, _vp, _vp],
     "dpwa_learner_lerp": [_vp, _vp, _vp],
     "dpwa_learner_cancel": [_vp],
+    "dpwa_learner_set_pull": [_vp, _int, _int],
     "dpwa_learner_pointers": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                               ctypes.POINTER(_vp)],
     "dpwa_learner_status_word": [_vp, ctypes.POINTER(_vp)],

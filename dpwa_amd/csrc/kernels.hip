@@ -364,6 +364,35 @@ __global__ __launch_bounds__(kBlock) void k_publish(char *__restrict__ slot, con
     }
 }
 
+// Pull: copy a peer's snapshot (header + payload, IPC-mapped in another GPU's HBM) into the
+// local staging buffer.  The loads travel over the xGMI link to the owner; each lane keeps
+// four 16-byte loads in flight and the grid is capped (grid-stride) so the pull occupies a
+// bounded share of the CUs while the training step runs on the compute stream.
+__global__ __launch_bounds__(kBlock) void k_pull(u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, int64_t n16)
+{
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        u32x4 v0 = src[i], v1 = src[i + stride], v2 = src[i + 2 * stride], v3 = src[i + 3 * stride];
+        dst[i] = v0;
+        dst[i + stride] = v1;
+        dst[i + 2 * stride] = v2;
+        dst[i + 3 * stride] = v3;
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+hipError_t launch_pull(void *dst, const void *src, int64_t nbytes, int max_blocks, hipStream_t s)
+{
+    if (((uintptr_t)dst | (uintptr_t)src | (uintptr_t)nbytes) & 15) return hipErrorInvalidValue;
+    const int64_t n16 = nbytes >> 4;
+    int64_t g = (n16 + kBlock * 4 - 1) / (kBlock * 4);
+    if (g < 1) g = 1;
+    if (g > max_blocks) g = max_blocks;
+    hipLaunchKernelGGL(k_pull, dim3((uint32_t)g), dim3(kBlock), 0, s, (u32x4 *)dst, (const u32x4 *)src, n16);
+    return hipGetLastError();
+}
+
 // Writes back every XCD's L2 (system-scope release from 256 workgroups, which the
 // dispatcher deals round-robin over the 8 XCDs) so a snapshot that another GPU will pull
 // is in HBM, not only in this GPU's L2s.  Used only once the slots are IPC-exported.

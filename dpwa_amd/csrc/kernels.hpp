@@ -45,6 +45,9 @@ hipError_t launch_factor(const FusedArgs &fa, hipStream_t s);
 hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t n, int32_t dtype,
                           double *clock, double loss, const double *loss_dev, uint64_t version,
                           bool system_release, hipStream_t s);
+// Pull of `nbytes` (multiple of 16, 16-B aligned) from a peer's slot into local staging with
+// a copy kernel of at most `max_blocks` workgroups.
+hipError_t launch_pull(void *dst, const void *src, int64_t nbytes, int max_blocks, hipStream_t s);
 // Publish of the header only (the payload was written through by the last average).
 hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *clock, double loss,
                                  const double *loss_dev, uint64_t version, bool system_release, hipStream_t s);

@@ -142,6 +142,8 @@ struct dpwa_learner {
     hipEvent_t ev_factor = nullptr;     // last factor computation done
     // write-through snapshot: the last average also wrote its result into the slot of the
     // next publish (for the flat buffer `wt_flat`, on stream `wt_stream`)
+    int pull_mode = DPWA_PULL_COPY_ENGINE;   // how cross-device fetches move bytes
+    int pull_blocks = 512;
     bool wt_valid = false;
     const void *wt_flat = nullptr;
     hipStream_t wt_stream = nullptr;
@@ -473,7 +475,11 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
             HIP_TRY(hipEventRecord(l->ev_consumed, l->consume_stream));
             HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
         }
-        HIP_TRY(hipMemcpyAsync(l->staging, peer_slot, kHeader + l->payload_bytes, hipMemcpyDefault, l->side));
+        const size_t nbytes = kHeader + round_up(l->payload_bytes, 16);
+        if (l->pull_mode == DPWA_PULL_KERNEL)
+            HIP_TRY(launch_pull(l->staging, peer_slot, (int64_t)nbytes, l->pull_blocks, l->side));
+        else
+            HIP_TRY(hipMemcpyAsync(l->staging, peer_slot, nbytes, hipMemcpyDefault, l->side));
         HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
         l->src = l->staging;
         l->src_copied = true;
@@ -564,6 +570,15 @@ int dpwa_learner_average_through(dpwa_learner *l, void *flat, double loss, const
     if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_average_through: NULL argument");
     DeviceGuard dg(l->device);
     return average_impl(l, flat, loss, loss_dev, (hipStream_t)stream, true);
+}
+
+int dpwa_learner_set_pull(dpwa_learner *l, int mode, int max_blocks)
+{
+    if (!l || (mode != DPWA_PULL_COPY_ENGINE && mode != DPWA_PULL_KERNEL) || max_blocks < 1)
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_set_pull: bad arguments");
+    l->pull_mode = mode;
+    l->pull_blocks = max_blocks;
+    return DPWA_OK;
 }
 
 int dpwa_learner_cancel(dpwa_learner *l)

@@ -15,6 +15,7 @@ protocol and error behaviour as the reference.  What moves:
 """
 import ctypes
 import logging
+import os
 
 import torch
 import yaml
@@ -110,7 +111,7 @@ class DeviceFactor:
 
 
 class DpwaConnection:
-    def __init__(self, name, config_file, seed=None, group=None):
+    def __init__(self, name, config_file, seed=None, group=None, pull=None):
         self.name = name
         self.config = DpwaConfiguration(config_file)
         self.nodes = self.config.get_nodes()
@@ -159,6 +160,8 @@ class DpwaConnection:
         _lib.call("dpwa_node_handles", self._node, None, ctypes.byref(sched))
         self._sched = Scheduler(len(self.peers), handle=sched.value)
         self._learner = None
+        # transport of copying fetches: "copy" (hipMemcpyAsync) or "kernel[:blocks]"
+        self._pull = pull if pull is not None else os.environ.get("DPWA_PULL", "copy")
         self._out = ctypes.c_int()
         self._out_ref = ctypes.byref(self._out)
         self._f_update_send = lib.dpwa_node_update_send
@@ -343,6 +346,11 @@ class DpwaConnection:
         h = ctypes.c_void_p()
         _lib.call("dpwa_node_handles", self._node, ctypes.byref(h), None)
         self._learner = Learner(parameters.device, parameters.numel(), parameters.dtype, handle=h.value)
+        mode, _, blocks = self._pull.partition(":")
+        if mode not in ("copy", "kernel"):
+            raise ValueError("pull must be 'copy' or 'kernel[:blocks]', got %r" % self._pull)
+        _lib.call("dpwa_learner_set_pull", h, _lib.PULL_KERNEL if mode == "kernel" else _lib.PULL_COPY_ENGINE,
+                  int(blocks or 512))
         self._group.on_bind(self)
         return self._learner
 

@@ -166,6 +166,13 @@ int dpwa_learner_publish_reuse(dpwa_learner *l, const void *flat, double loss, c
 int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dpwa_stream_t stream);
 int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream);
 
+/* How a copying fetch (any non-zero-copy fetch) moves its bytes: DPWA_PULL_COPY_ENGINE
+ * (hipMemcpyAsync on the side stream, the default) or DPWA_PULL_KERNEL (a copy kernel of at
+ * most max_blocks workgroups reading the IPC-mapped peer slot over xGMI). */
+#define DPWA_PULL_COPY_ENGINE 0
+#define DPWA_PULL_KERNEL 1
+int dpwa_learner_set_pull(dpwa_learner *l, int mode, int max_blocks);
+
 /* Abandons a fetch whose factor was computed but whose lerp will never be issued (the
  * caller of update_wait chose not to average); the snapshot it read may then be reused. */
 int dpwa_learner_cancel(dpwa_learner *l);

@@ -31,7 +31,7 @@ def write_cfg(path, names, fp, interp, thr):
         f.write("\n".join(lines) + "\n")
 
 
-def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of_rank):
+def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of_rank, pull="copy"):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -43,7 +43,7 @@ def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of
     from dpwa_amd.group import DistGroup
     init, deltas, send, wait = inputs(world, n, T)
     names = ["r%d" % i for i in range(world)]
-    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank)
+    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank, pull=pull)
     assert isinstance(conn._group, DistGroup)
     flat = torch.from_numpy(init[rank]).to(dev)
     params = np.zeros((T, n), np.float32)

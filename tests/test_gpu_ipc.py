@@ -26,13 +26,15 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("world,interp,fp,thr", [(2, "clock", 1.0, 0.0), (3, "loss", 0.7, 0.5)])
-def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr):
+@pytest.mark.parametrize("world,interp,fp,thr,pull", [(2, "clock", 1.0, 0.0, "copy"), (3, "loss", 0.7, 0.5, "copy"),
+                                                       (2, "constant", 1.0, 0.0, "kernel:64"),
+                                                       (3, "clock", 0.7, 0.0, "kernel")])
+def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull):
     n, T = 100_003, 12
     names = ["r%d" % i for i in range(world)]
     cfg = str(tmp_path / "dist.yaml")
     dist_worker.write_cfg(cfg, names, fp, interp, thr)
-    mp.spawn(dist_worker.gossip_worker, args=(world, free_port(), cfg, str(tmp_path), n, T, "gloo", 0),
+    mp.spawn(dist_worker.gossip_worker, args=(world, free_port(), cfg, str(tmp_path), n, T, "gloo", 0, pull),
              nprocs=world, join=True)
     init, deltas, send, wait = dist_worker.inputs(world, n, T)
     exp = ogossip.simulate(names, init, deltas, send, wait, interp, 0.5, thr, fp, [500 + r for r in range(world)])
