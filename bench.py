@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
     ap.add_argument("--no-write-through", action="store_true", help="skip the write-through variant")
     ap.add_argument("--sample-every", type=int, default=4, help="time the averaging kernel every k-th step")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N>1 (gloo only to rehearse on one GPU)")
     ap.add_argument("--pull", default="auto",
                     help="N>1 fetch transport: copy (hipMemcpyAsync), kernel[:blocks], or auto (fastest of a trial)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
@@ -132,10 +134,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d (launch N>1 with torch.distributed.run)" % (args.gpus, world))
-    device = torch.device("cuda", local_rank)
+    # one GPU per rank; the modulo only matters for rehearsals with more ranks than GPUs
+    device = torch.device("cuda", local_rank % torch.cuda.device_count())
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:   # rehearsal of the N>1 path on fewer GPUs (RCCL refuses two ranks per GPU)
+            dist.init_process_group("gloo")
 
     from dpwa_amd import DpwaConnection
     from dpwa_amd.group import LocalGroup
@@ -163,6 +169,7 @@ def main():
 
     stream = torch.cuda.current_stream(device)
     loss = 1.0
+    from dpwa_amd import _lib
 
     def run(steps, warmup, write_through, sample_every):
         """`steps` timed lock-step rounds; the averaging kernel of every `sample_every`-th
@@ -180,6 +187,8 @@ def main():
                 # the adapter's update_wait: fused device factor + lerp (one kernel)
                 if sample:
                     a, b = events[len(lerp_events)]
+                    if world > 1:    # the pull is TxThread's part: order its wait before the timing event
+                        _lib.load().dpwa_learner_wait_fetch(conn._learner.handle, stream.cuda_stream)
                     a.record(stream)
                 payload, _ = conn.update_wait_average(flat, loss, write_through=write_through)
                 if sample:
@@ -206,7 +215,7 @@ def main():
         elapsed = time.perf_counter() - t0
         lerp_ms = np.array([a.elapsed_time(b) for a, b in lerp_events]) if lerp_events else np.array([np.nan])
         stats = torch.tensor([elapsed, float(averaged), float(len(learners) * steps)], dtype=torch.float64,
-                             device=device)
+                             device=device if args.dist_backend == "nccl" else "cpu")
         if world > 1:
             tmax = stats[0:1].clone()
             dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -214,8 +223,6 @@ def main():
             dist.all_reduce(sums, op=dist.ReduceOp.SUM)
             return float(tmax.item()), float(sums[0].item()), float(sums[1].item()), lerp_ms
         return elapsed, float(averaged), float(len(learners) * steps), lerp_ms
-
-    from dpwa_amd import _lib
 
     def set_pull(mode):
         kind, _, blocks = mode.partition(":")

@@ -572,6 +572,16 @@ int dpwa_learner_average_through(dpwa_learner *l, void *flat, double loss, const
     return average_impl(l, flat, loss, loss_dev, (hipStream_t)stream, true);
 }
 
+int dpwa_learner_wait_fetch(dpwa_learner *l, dpwa_stream_t stream)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_wait_fetch: NULL learner");
+    if (l->have_fetch && l->src_copied) {
+        DeviceGuard dg(l->device);
+        HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, l->ev_fetched, 0));
+    }
+    return DPWA_OK;
+}
+
 int dpwa_learner_set_pull(dpwa_learner *l, int mode, int max_blocks)
 {
     if (!l || (mode != DPWA_PULL_COPY_ENGINE && mode != DPWA_PULL_KERNEL) || max_blocks < 1)

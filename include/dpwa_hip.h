@@ -166,6 +166,11 @@ int dpwa_learner_publish_reuse(dpwa_learner *l, const void *flat, double loss, c
 int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dpwa_stream_t stream);
 int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream);
 
+/* Makes `stream` wait for the pull of the fetch in flight, if it copies (TxThread.fetch_wait,
+ * conn.py:326-329); average/factor do this themselves -- this only lets a caller order the
+ * wait before its own timing event. */
+int dpwa_learner_wait_fetch(dpwa_learner *l, dpwa_stream_t stream);
+
 /* How a copying fetch (any non-zero-copy fetch) moves its bytes: DPWA_PULL_COPY_ENGINE
  * (hipMemcpyAsync on the side stream, the default) or DPWA_PULL_KERNEL (a copy kernel of at
  * most max_blocks workgroups reading the IPC-mapped peer slot over xGMI). */
