@@ -93,6 +93,8 @@ SIGNATURES = {
     "dpwa_learner_cancel": [_vp],
     "dpwa_learner_set_pull": [_vp, _int, _int],
     "dpwa_learner_wait_fetch": [_vp, _vp],
+    "dpwa_learner_read_snapshot": [_vp, _vp, _vp, _i64, ctypes.POINTER(_u64)],
+    "dpwa_learner_fetch_host": [_vp, _vp, _vp, _i64, _vp],
     "dpwa_learner_pointers": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                               ctypes.POINTER(_vp)],
     "dpwa_learner_status_word": [_vp, ctypes.POINTER(_vp)],

@@ -27,10 +27,20 @@ class DpwaPyTorchAdapter:
     for loops that do not touch ``.data`` between update_wait and update_send (the README
     loop and the reference's example trainer do not)."""
 
-    def __init__(self, net, name, config_file, write_through=False, **connection_kwargs):
+    def __init__(self, net, name, config_file, write_through=False, transport="device", **connection_kwargs):
+        """transport: "device" (peers are learners of this process or of the torch.distributed
+        job, pulled from HBM/over xGMI) or "wire" (peers are reached over TCP at the YAML's
+        host/port with the reference's protocol -- e.g. reference CPU nodes; dpwa_amd/bridge.py)."""
         self._net = net
         self._flat = FlatParameters(net.named_parameters())
-        self._conn = DpwaConnection(name, config_file, **connection_kwargs)
+        if transport == "wire":
+            from ..bridge import SnapshotCodec, WireConnection
+            self._conn = WireConnection(name, config_file, codec=SnapshotCodec.from_flat(self._flat),
+                                        **connection_kwargs)
+        elif transport == "device":
+            self._conn = DpwaConnection(name, config_file, **connection_kwargs)
+        else:
+            raise ValueError("transport must be 'device' or 'wire'")
         self._write_through = write_through
         self._versions = None
 

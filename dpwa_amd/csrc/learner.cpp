@@ -148,6 +148,10 @@ struct dpwa_learner {
     const void *wt_flat = nullptr;
     hipStream_t wt_stream = nullptr;
     hipEvent_t ev_wt = nullptr;
+    // host readers of published slots (wire bridge) run on other threads
+    std::mutex pub_mu;
+    hipStream_t read_stream = nullptr;
+    hipEvent_t ev_read = nullptr;
     // fetch state
     const char *src = nullptr;          // header of the snapshot to average with
     bool src_copied = false;
@@ -248,6 +252,8 @@ int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype
         if ((e = hipEventCreateWithFlags(&l->ev_consumed, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_factor, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_wt, hipEventDisableTiming)) != hipSuccess) break;
+        if ((e = hipEventCreateWithFlags(&l->ev_read, hipEventDisableTiming)) != hipSuccess) break;
+        if ((e = hipStreamCreateWithFlags(&l->read_stream, hipStreamNonBlocking)) != hipSuccess) break;
         if ((e = hipHostMalloc((void **)&l->host_status, sizeof(int32_t), hipHostMallocMapped)) != hipSuccess) break;
         *l->host_status = 0;
         if ((e = hipHostGetDevicePointer((void **)&l->host_status_dev, l->host_status, 0)) != hipSuccess) break;
@@ -289,6 +295,8 @@ int dpwa_learner_destroy(dpwa_learner *l)
     if (l->ev_consumed) (void)hipEventDestroy(l->ev_consumed);
     if (l->ev_factor) (void)hipEventDestroy(l->ev_factor);
     if (l->ev_wt) (void)hipEventDestroy(l->ev_wt);
+    if (l->ev_read) (void)hipEventDestroy(l->ev_read);
+    if (l->read_stream) (void)hipStreamDestroy(l->read_stream);
     if (l->host_status) (void)hipHostFree(l->host_status);
     if (l->slots) (void)hipFree(l->slots);
     if (l->staging) (void)hipFree(l->staging);
@@ -338,6 +346,7 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
                                loss_dev, l->version + 1, l->exported, s));
     }
     l->wt_valid = false;
+    std::lock_guard<std::mutex> g(l->pub_mu);
     l->publish_stream[k] = s;
     l->published[k] = true;
     l->version++;
@@ -570,6 +579,72 @@ int dpwa_learner_average_through(dpwa_learner *l, void *flat, double loss, const
     if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_average_through: NULL argument");
     DeviceGuard dg(l->device);
     return average_impl(l, flat, loss, loss_dev, (hipStream_t)stream, true);
+}
+
+int dpwa_learner_read_snapshot(dpwa_learner *l, void *header_out, void *payload_out, int64_t payload_bytes,
+                               uint64_t *version_out)
+{
+    if (!l || !header_out || !version_out || payload_bytes < 0 || (payload_bytes > 0 && !payload_out))
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_read_snapshot: bad arguments");
+    if ((size_t)payload_bytes > l->payload_bytes) payload_bytes = (int64_t)l->payload_bytes;
+    DeviceGuard dg(l->device);
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        uint64_t v;
+        int k;
+        {
+            std::lock_guard<std::mutex> g(l->pub_mu);
+            v = l->version;
+            if (v == 0) {
+                *version_out = 0;
+                return DPWA_OK;   // nothing published: the reference replies without state
+            }
+            k = (int)((v - 1) % 2);
+            // order after the publish (and everything before it) on the publisher's stream
+            HIP_TRY(hipEventRecord(l->ev_read, l->publish_stream[k]));
+        }
+        HIP_TRY(hipStreamWaitEvent(l->read_stream, l->ev_read, 0));
+        const char *slot = l->slots + (size_t)k * l->slot_stride;
+        HIP_TRY(hipMemcpyAsync(header_out, slot, kHeader, hipMemcpyDeviceToHost, l->read_stream));
+        if (payload_bytes)
+            HIP_TRY(hipMemcpyAsync(payload_out, slot + kHeader, (size_t)payload_bytes, hipMemcpyDeviceToHost,
+                                   l->read_stream));
+        HIP_TRY(hipStreamSynchronize(l->read_stream));
+        // a slot is rewritten two publishes later: if that happened meanwhile, read again
+        std::lock_guard<std::mutex> g(l->pub_mu);
+        if (l->version < v + 2 && ((const dpwa_header *)header_out)->version == v) {
+            *version_out = v;
+            return DPWA_OK;
+        }
+    }
+    return set_error(DPWA_ERR_STATE, "dpwa_learner_read_snapshot: publishes outran the reader");
+}
+
+int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *payload, int64_t payload_bytes,
+                            dpwa_stream_t stream)
+{
+    if (!l || !header || payload_bytes != (int64_t)l->payload_bytes || (payload_bytes > 0 && !payload))
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_fetch_host: need a header and %zu payload bytes",
+                         l ? l->payload_bytes : (size_t)0);
+    DeviceGuard dg(l->device);
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipEventRecord(l->ev_issue, s));
+    HIP_TRY(hipStreamWaitEvent(l->side, l->ev_issue, 0));
+    if (l->consumed_once && l->consume_stream != s) {
+        HIP_TRY(hipEventRecord(l->ev_consumed, l->consume_stream));
+        HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
+    }
+    // pageable host sources: the calls return once the host bytes have been taken
+    HIP_TRY(hipMemcpyAsync(l->staging, header, kHeader, hipMemcpyHostToDevice, l->side));
+    if (payload_bytes)
+        HIP_TRY(hipMemcpyAsync(l->staging + kHeader, payload, (size_t)payload_bytes, hipMemcpyHostToDevice, l->side));
+    HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
+    l->src = l->staging;
+    l->src_copied = true;
+    l->src_owner = nullptr;
+    l->src_slot = -1;
+    l->have_fetch = true;
+    l->have_factor = false;
+    return DPWA_OK;
 }
 
 int dpwa_learner_wait_fetch(dpwa_learner *l, dpwa_stream_t stream)

@@ -166,6 +166,16 @@ int dpwa_learner_publish_reuse(dpwa_learner *l, const void *flat, double loss, c
 int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dpwa_stream_t stream);
 int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream);
 
+/* Wire bridge.  read_snapshot: synchronous copy of the latest published
+ * snapshot to host memory (header 256 B + up to payload_bytes), from any host thread --
+ * RxThread's reply (conn.py:108-110); *version_out = 0 when nothing was published.
+ * fetch_host: stage a snapshot received in host memory (a reference node's reply,
+ * conn.py:298) as the fetch to average with; payload_bytes must equal n*sizeof(dtype). */
+int dpwa_learner_read_snapshot(dpwa_learner *l, void *header_out, void *payload_out, int64_t payload_bytes,
+                               uint64_t *version_out);
+int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *payload, int64_t payload_bytes,
+                            dpwa_stream_t stream);
+
 /* Makes `stream` wait for the pull of the fetch in flight, if it copies (TxThread.fetch_wait,
  * conn.py:326-329); average/factor do this themselves -- this only lets a caller order the
  * wait before its own timing event. */

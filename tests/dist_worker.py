@@ -70,3 +70,42 @@ def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of
     dist.barrier()
     conn.close()
     dist.destroy_process_group()
+
+
+FAULTS = {  # rank -> {round: {peer name: fault}}; applied before that round's update_send
+    0: {2: {"r1": "slow"}, 5: {"r1": None}, 7: {"r2": "dead"}},
+    1: {3: {"r0": "down"}, 6: {"r0": None}},
+}
+
+
+def fault_worker(rank, world, port, cfg_path, out_dir, n, T):
+    """Like gossip_worker, with scripted faults (FAULTS) injected into this rank's node."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from dpwa_amd import DpwaConnection
+    init, deltas, send, wait = inputs(world, n, T)
+    names = ["r%d" % i for i in range(world)]
+    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank)
+    flat = torch.from_numpy(init[rank]).to(dev)
+    params, clocks, peers, scores = np.zeros((T, n), np.float32), np.zeros(T), [], []
+    for r in range(T):
+        for peer, f in FAULTS.get(rank, {}).get(r, {}).items():
+            conn.inject_fault(peer, f)
+        conn.update_send(flat, send[r][rank])
+        flat.add_(torch.from_numpy(deltas[r, rank]).to(dev))
+        payload, _ = conn.update_wait_average(flat, wait[r][rank])
+        peers.append(payload.peer if payload is not None else "")
+        params[r] = flat.cpu().numpy()
+        clocks[r] = conn.clock
+        scores.append([conn.flow_control_scores()[p] for p in names if p != names[rank]])
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=params, clocks=clocks, peers=np.array(peers),
+             scores=np.array([[-1 if s is None else s for s in row] for row in scores]))
+    torch.cuda.synchronize()
+    dist.barrier()
+    conn.close()
+    dist.destroy_process_group()

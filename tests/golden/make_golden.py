@@ -619,6 +619,39 @@ def gen_wire():
     print("wire: %d samples" % len(samples))
 
 
+def gen_wire_adapter():
+    """RxThread replies carrying a real adapter blob: header + pickle(state) +
+    pickle({name: raw fp32 bytes}) (pytorch.py:42-53 -> dpwa.py:115-116 -> conn.py:110)."""
+    shapes = [(4, 3), (5,), (2, 2, 2)]
+    rng = np.random.default_rng(77)
+    n = sum(int(np.prod(s_)) for s_ in shapes)
+    flat = rng.standard_normal(n).astype(np.float32)
+    net = Net(shapes)
+    load_flat(net, flat)
+    cap = CaptureConn()
+    adapter_for(net, cap).update_send(0.0)
+    frames = []
+    for state in ({"clock": 3, "loss": 0.5}, {"clock": 7.25, "loss": 1e-3}):
+        a, b = socket.socketpair()
+        rmsg.send_message(a, rconn.MESSAGE_TYPE_FETCH_PARAMETERS, state, cap.blob)
+        a.shutdown(socket.SHUT_WR)
+        raw = b""
+        while True:
+            chunk = b.recv(1 << 16)
+            if not chunk:
+                break
+            raw += chunk
+        a.close()
+        b.close()
+        frames.append({"state": state, "frame_hex": raw.hex()})
+    names = [nm for nm, _ in net.named_parameters()]
+    with open(os.path.join(OUT, "wire_adapter.json"), "wt") as f:
+        json.dump({"source": "reference adapter blob (pytorch.py:49-53) in an RxThread reply (conn.py:110)",
+                   "shapes": shapes, "names": names, "flat_f32_hex": flat.tobytes().hex(),
+                   "blob_hex": cap.blob.hex(), "frames": frames}, f, indent=0)
+    print("wire_adapter: %d frames" % len(frames))
+
+
 # ----------------------------------------------------------------------------
 # G. configuration parsing
 # ----------------------------------------------------------------------------
@@ -691,6 +724,7 @@ def main():
         gen_peer_select(tmp)
         gen_gossip(tmp)
         gen_wire()
+        gen_wire_adapter()
         gen_config(tmp)
     os._exit(0)   # reference TxThreads are non-daemon and never exit on their own (conn.py:170-172)
 

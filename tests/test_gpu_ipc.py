@@ -44,3 +44,49 @@ def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull):
         assert list(got["peers"]) == want_peers, r
         assert np.array_equal(got["clocks"], exp["clocks"][:, r]), r
         assert olerp.bits_equal(got["params"], exp["params"][:, r]), r
+
+
+def test_ipc_gossip_with_injected_faults(tmp_path):
+    """Remote peers marked slow (timeouts), down (refused) or dead (removed) steer the
+    native scheduler exactly as the reference's TxThread: checked against the oracle fed
+    the same outcomes (conn.py:246-313)."""
+    world, n, T = 3, 50_001, 10
+    names = ["r%d" % i for i in range(world)]
+    cfg = str(tmp_path / "faults.yaml")
+    dist_worker.write_cfg(cfg, names, 1.0, "clock", 0.0)
+    mp.spawn(dist_worker.fault_worker, args=(world, free_port(), cfg, str(tmp_path), n, T), nprocs=world, join=True)
+    init, deltas, send, wait = dist_worker.inputs(world, n, T)
+    from oracle.policy import OracleLearner
+    learners = [OracleLearner(names[g], [x for x in names if x != names[g]], 1.0, "clock", None, 0.0, 500 + g)
+                for g in range(world)]
+    params = init.copy()
+    faults = [{} for _ in range(world)]
+    for r in range(T):
+        states, snaps = [], []
+        for g in range(world):
+            for peer, f in dist_worker.FAULTS.get(g, {}).get(r, {}).items():
+                if f is None:
+                    faults[g].pop(peer, None)
+                else:
+                    faults[g][peer] = f
+            states.append(learners[g].update_send(send[r][g]))
+            snaps.append(params[g].copy())
+        for g in range(world):
+            params[g] = np.add(params[g], deltas[r, g], dtype=np.float32)
+        for g in range(world):
+            fl = faults[g]
+            conn_fn = lambda p, fl=fl: {"down": "refused", "dead": "error"}.get(fl.get(p), "ok")
+            req_fn = lambda p, fl=fl: ({"slow": ("timeout", None, None), "dead": ("error", None, None),
+                                        "down": ("error", None, None)}.get(fl.get(p)) or
+                                       ("payload", states[names.index(p)], snaps[names.index(p)]))
+            st, pl, att = learners[g].fetch(conn_fn, req_fn) if learners[g].fetching else (None, None, [])
+            averaged, f = learners[g].update_wait(wait[r][g], st, pl is not None)
+            if averaged:
+                params[g] = olerp.lerp_f32(params[g], pl, f)
+            got = np.load(tmp_path / ("rank%d.npz" % g))
+            want_peer = att[-1]["peer"] if pl is not None else ""
+            assert got["peers"][r] == want_peer, (g, r)
+            assert got["clocks"][r] == learners[g].clock, (g, r)
+            assert olerp.bits_equal(got["params"][r], params[g]), (g, r)
+            want_scores = [-1 if s is None else s for s in learners[g].scores([x for x in names if x != names[g]])]
+            assert list(got["scores"][r]) == want_scores, (g, r)
