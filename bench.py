@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
     ap.add_argument("--no-write-through", action="store_true", help="skip the write-through variant")
     ap.add_argument("--sample-every", type=int, default=4, help="time the averaging kernel every k-th step")
+    ap.add_argument("--streams", default="one", choices=["one", "per-learner"],
+                    help="stream per co-resident learner (their kernels may overlap) or one shared stream")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (gloo only to rehearse on one GPU)")
     ap.add_argument("--pull", default="auto",
@@ -168,6 +170,9 @@ def main():
         learners.append((conn, flat))
 
     stream = torch.cuda.current_stream(device)
+    # co-resident learners on their own streams (their kernels overlap) or all on one
+    streams = ([torch.cuda.Stream(device) for _ in learners] if args.streams == "per-learner"
+               else [stream for _ in learners])
     loss = 1.0
     from dpwa_amd import _lib
 
@@ -180,21 +185,24 @@ def main():
 
         def step(k, timed):
             done = 0
-            for conn, flat in learners:
-                conn.update_send(flat, loss, reuse_snapshot=write_through)
+            for i, (conn, flat) in enumerate(learners):
+                with torch.cuda.stream(streams[i]):
+                    conn.update_send(flat, loss, reuse_snapshot=write_through)
             sample = timed and k % sample_every == 0
-            for conn, flat in learners:
-                # the adapter's update_wait: fused device factor + lerp (one kernel)
-                if sample:
-                    a, b = events[len(lerp_events)]
-                    if world > 1:    # the pull is TxThread's part: order its wait before the timing event
-                        _lib.load().dpwa_learner_wait_fetch(conn._learner.handle, stream.cuda_stream)
-                    a.record(stream)
-                payload, _ = conn.update_wait_average(flat, loss, write_through=write_through)
-                if sample:
-                    b.record(stream)
-                    if payload is not None:
-                        lerp_events.append((a, b))
+            for i, (conn, flat) in enumerate(learners):
+                st = streams[i]
+                with torch.cuda.stream(st):
+                    # the adapter's update_wait: fused device factor + lerp (one kernel)
+                    if sample:
+                        a, b = events[len(lerp_events)]
+                        if world > 1:    # the pull is TxThread's part: order its wait before the timing event
+                            _lib.load().dpwa_learner_wait_fetch(conn._learner.handle, st.cuda_stream)
+                        a.record(st)
+                    payload, _ = conn.update_wait_average(flat, loss, write_through=write_through)
+                    if sample:
+                        b.record(st)
+                        if payload is not None:
+                            lerp_events.append((a, b))
                 done += payload is not None
             return done
 
@@ -281,6 +289,7 @@ def main():
                 "transport": "in-place HBM read (co-resident peer)" if world == 1 else
                              "hipIpc-mapped slot pulled over xGMI on a side stream (%s)" % pull,
                 "parallelism": "gossip x%d" % int(rounds / args.steps),
+                "streams": args.streams,
             },
             "gossip_rounds_per_s": round(rounds / elapsed, 1),
             "gossip_rounds_per_s_per_learner": round(rounds / elapsed / (rounds / args.steps), 1),
