@@ -57,7 +57,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (gloo only to rehearse on one GPU)")
     ap.add_argument("--pull", default="auto",
-                    help="N>1 fetch transport: copy (hipMemcpyAsync), kernel[:blocks], or auto (fastest of a trial)")
+                    help="N>1 fetch transport: copy (hipMemcpyAsync), kernel[:blocks], relay[:blocks] "
+                         "(two-phase multi-link), or auto (fastest of a short trial)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="PMC traffic summary (rocprofv3 FETCH_SIZE/WRITE_SIZE passes) to report")
     return ap.parse_args()
@@ -166,7 +167,8 @@ def main():
     for name, seed in mine:
         g = torch.Generator(device=device).manual_seed(seed)
         flat = torch.randn(args.numel, device=device, generator=g, dtype=torch.float32).to(dtype)
-        conn = DpwaConnection(name, cfg, seed=1000 + seed, group=group)
+        # under a DistGroup the relay buffers are allocated up front so every transport can be tried
+        conn = DpwaConnection(name, cfg, seed=1000 + seed, group=group, pull="relay" if world > 1 else None)
         learners.append((conn, flat))
 
     stream = torch.cuda.current_stream(device)
@@ -233,17 +235,17 @@ def main():
         return elapsed, float(averaged), float(len(learners) * steps), lerp_ms
 
     def set_pull(mode):
-        kind, _, blocks = mode.partition(":")
         for conn, _ in learners:
-            if conn._learner is not None:
-                _lib.call("dpwa_learner_set_pull", conn._learner.handle,
-                          _lib.PULL_KERNEL if kind == "kernel" else _lib.PULL_COPY_ENGINE, int(blocks or 512))
+            conn.set_pull(mode)
+        if world > 1:
+            dist.barrier()
 
     pull_trials = {}
     pull = args.pull
     if world > 1:
         run(2, 2, False, 1000)   # binds the learners (IPC exchange) before the transport is chosen
-        modes = [args.pull] if args.pull != "auto" else ["copy", "kernel:256", "kernel:1024"]
+        modes = [args.pull] if args.pull != "auto" else ["copy", "kernel:256", "kernel:1024", "relay:32",
+                                                         "relay:128"]
         for mode in modes:       # short timed trial of each transport; the fastest is used below
             set_pull(mode)
             el, av, _, _ = run(max(10, args.steps // 10), 2, False, 1000)

@@ -29,7 +29,7 @@ REPLY_PAYLOAD, REPLY_EMPTY, REPLY_TIMEOUT, REPLY_ERROR = 3, 4, 5, 6
 PEER_READY, PEER_NO_STATE, PEER_DOWN, PEER_SLOW, PEER_DEAD = 0, 1, 2, 3, 4
 NODE_PEER_UNSET, NODE_PEER_LOCAL, NODE_PEER_REMOTE = 0, 1, 2
 PULL_COPY_ENGINE, PULL_KERNEL = 0, 1
-FLAG_EAGER, FLAG_ZERO_COPY, FLAG_REUSE_SNAPSHOT, FLAG_WRITE_THROUGH = 1, 2, 4, 8
+FLAG_EAGER, FLAG_ZERO_COPY, FLAG_REUSE_SNAPSHOT, FLAG_WRITE_THROUGH, FLAG_PICK_ONLY = 1, 2, 4, 8, 16
 
 
 class DpwaLibraryError(RuntimeError):
@@ -94,6 +94,13 @@ SIGNATURES = {
     "dpwa_learner_set_pull": [_vp, _int, _int],
     "dpwa_learner_wait_fetch": [_vp, _vp],
     "dpwa_learner_read_snapshot": [_vp, _vp, _vp, _i64, ctypes.POINTER(_u64)],
+    "dpwa_learner_relay_enable": [_vp, _int, _int],
+    "dpwa_learner_relay_handle": [_vp, _vp, _i64],
+    "dpwa_learner_relay_attach": [_vp, _int, _int, _vp, _i64],
+    "dpwa_learner_relay_wait": [_vp, _vp],
+    "dpwa_learner_relay_phase1": [_vp, _vp, _u64, _int, _vp],
+    "dpwa_learner_relay_phase2": [_vp, _vp, _int, _u64, _int],
+    "dpwa_learner_side_stream": [_vp, ctypes.POINTER(_vp)],
     "dpwa_learner_fetch_host": [_vp, _vp, _vp, _i64, _vp],
     "dpwa_learner_pointers": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                               ctypes.POINTER(_vp)],

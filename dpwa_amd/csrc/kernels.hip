@@ -382,14 +382,94 @@ __global__ __launch_bounds__(kBlock) void k_pull(u32x4 *__restrict__ dst, const 
     for (; i < n16; i += stride) dst[i] = src[i];
 }
 
-hipError_t launch_pull(void *dst, const void *src, int64_t nbytes, int max_blocks, hipStream_t s)
+// Invalidates every XCD's L2 lines of other agents' memory (system-scope acquire from 256
+// workgroups, dealt round-robin over the 8 XCDs) ahead of a kernel that reads peer memory.
+__global__ __launch_bounds__(64) void k_acquire_system()
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+hipError_t launch_pull(void *dst, const void *src, int64_t nbytes, int max_blocks, bool remote, hipStream_t s)
 {
     if (((uintptr_t)dst | (uintptr_t)src | (uintptr_t)nbytes) & 15) return hipErrorInvalidValue;
+    if (remote) hipLaunchKernelGGL(k_acquire_system, dim3(256), dim3(64), 0, s);
     const int64_t n16 = nbytes >> 4;
     int64_t g = (n16 + kBlock * 4 - 1) / (kBlock * 4);
     if (g < 1) g = 1;
     if (g > max_blocks) g = max_blocks;
     hipLaunchKernelGGL(k_pull, dim3((uint32_t)g), dim3(kBlock), 0, s, (u32x4 *)dst, (const u32x4 *)src, n16);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- relay (multi-link pull)
+// Lock-step round of G ranks where rank i averages with rank picks[i] (-1: none).  Each
+// snapshot payload is cut into G stripes.  Phase 1 on rank r pulls stripe r of every
+// snapshot some OTHER rank needs into its relay buffer (R_r[j] = stripe r of rank j);
+// after a barrier, phase 2 on rank r gathers stripe s of its peer j's snapshot from rank s's
+// relay buffer (from j itself for s == j, and directly for s == r).  Every pair's xGMI link
+// then carries one stripe per phase instead of one link carrying the whole snapshot.
+// blockIdx.y selects the source (phase 1) or the stripe (phase 2); blockIdx.x strides it.
+__global__ void k_release_system();
+
+__device__ __forceinline__ void copy16(u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, int64_t n16)
+{
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        u32x4 v0 = src[i], v1 = src[i + stride], v2 = src[i + 2 * stride], v3 = src[i + 3 * stride];
+        dst[i] = v0;
+        dst[i + stride] = v1;
+        dst[i + 2 * stride] = v2;
+        dst[i + 3 * stride] = v3;
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+__device__ __forceinline__ int64_t stripe_len(int s, int64_t stripe, int64_t payload)
+{
+    const int64_t beg = (int64_t)s * stripe;
+    if (beg >= payload) return 0;
+    return (payload - beg < stripe ? payload - beg : stripe);
+}
+
+__global__ __launch_bounds__(kBlock) void k_relay_phase1(RelayArgs a)
+{
+    const int j = blockIdx.y;
+    if (j == a.rank) return;
+    bool active = false;                                   // does any rank other than me need j?
+    for (int i = 0; i < a.world; ++i) active |= (i != a.rank && a.picks[i] == j);
+    if (!active) return;
+    const int64_t len = stripe_len(a.rank, a.stripe, a.payload);
+    const char *src = a.slots[j] + a.slot_off + 256 + (int64_t)a.rank * a.stripe;
+    char *dst = a.relay_mine + (int64_t)j * a.stripe;
+    copy16((u32x4 *)dst, (const u32x4 *)src, len >> 4);
+}
+
+__global__ __launch_bounds__(kBlock) void k_relay_phase2(RelayArgs a)
+{
+    const int j = a.picks[a.rank];
+    if (j < 0) return;
+    const int s = blockIdx.y;
+    if (s == 0 && blockIdx.x == 0 && threadIdx.x < 16)     // the 256-B header, straight from j
+        reinterpret_cast<u32x4 *>(a.staging)[threadIdx.x] =
+            reinterpret_cast<const u32x4 *>(a.slots[j] + a.slot_off)[threadIdx.x];
+    const int64_t len = stripe_len(s, a.stripe, a.payload);
+    const char *src = (s == j || s == a.rank) ? a.slots[j] + a.slot_off + 256 + (int64_t)s * a.stripe
+                                              : a.relays[s] + (int64_t)j * a.stripe;
+    copy16((u32x4 *)(a.staging + 256 + (int64_t)s * a.stripe), (const u32x4 *)src, len >> 4);
+}
+
+hipError_t launch_relay(int phase, const RelayArgs &a, int blocks_per_part, hipStream_t s)
+{
+    if (a.world < 1 || a.world > kMaxRelayRanks || (a.stripe & 15) || (a.payload & 15)) return hipErrorInvalidValue;
+    dim3 grid((uint32_t)blocks_per_part, (uint32_t)a.world);
+    hipLaunchKernelGGL(k_acquire_system, dim3(256), dim3(64), 0, s);   // both phases read peers
+    if (phase == 1) {   // the relay buffer is read by other GPUs: write it back from the L2s
+        hipLaunchKernelGGL(k_relay_phase1, grid, dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(k_release_system, dim3(256), dim3(64), 0, s);
+    } else {
+        hipLaunchKernelGGL(k_relay_phase2, grid, dim3(kBlock), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -46,8 +46,25 @@ hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t 
                           double *clock, double loss, const double *loss_dev, uint64_t version,
                           bool system_release, hipStream_t s);
 // Pull of `nbytes` (multiple of 16, 16-B aligned) from a peer's slot into local staging with
-// a copy kernel of at most `max_blocks` workgroups.
-hipError_t launch_pull(void *dst, const void *src, int64_t nbytes, int max_blocks, hipStream_t s);
+// a copy kernel of at most `max_blocks` workgroups.  `remote`: the source is another GPU's
+// memory -- the kernel is preceded by a system-scope acquire on every XCD, so no L2 line of
+// that memory cached by an earlier round is read.
+hipError_t launch_pull(void *dst, const void *src, int64_t nbytes, int max_blocks, bool remote, hipStream_t s);
+// Relay (multi-link) pull of a lock-step round; see kernels.hip.  All pointers are in this
+// process's address space (IPC-mapped for other ranks).
+constexpr int kMaxRelayRanks = 64;
+struct RelayArgs {
+    const char *slots[kMaxRelayRanks];    // slot 0 of every rank's snapshot allocation
+    const char *relays[kMaxRelayRanks];   // every rank's relay buffer
+    char *relay_mine;
+    char *staging;                        // header + payload destination (phase 2)
+    const int32_t *picks;                 // device: the peer every rank averages with, -1 none
+    int64_t slot_off;                     // byte offset of this round's slot from slot 0
+    int64_t stripe;                       // bytes per stripe (multiple of 16)
+    int64_t payload;                      // payload bytes to move (multiple of 16)
+    int32_t world, rank;
+};
+hipError_t launch_relay(int phase, const RelayArgs &a, int blocks_per_part, hipStream_t s);
 // Publish of the header only (the payload was written through by the last average).
 hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *clock, double loss,
                                  const double *loss_dev, uint64_t version, bool system_release, hipStream_t s);

@@ -148,6 +148,16 @@ struct dpwa_learner {
     const void *wt_flat = nullptr;
     hipStream_t wt_stream = nullptr;
     hipEvent_t ev_wt = nullptr;
+    // relay transport (multi-link lock-step pulls), see kernels.hip
+    bool relay_on = false;
+    int relay_world = 0, relay_rank = 0;
+    int64_t relay_stripe = 0;
+    char *relay_buf = nullptr;               // world x stripe, IPC-exported
+    std::vector<const char *> relay_slots;   // per rank: slot 0 base (own or IPC-mapped)
+    std::vector<const char *> relay_bufs;    // per rank: relay buffer (own or IPC-mapped)
+    std::vector<char *> relay_opened;        // IPC mappings to close
+    hipEvent_t ev_relay = nullptr;           // all relay work of the last round
+    bool relay_pending = false;
     // host readers of published slots (wire bridge) run on other threads
     std::mutex pub_mu;
     hipStream_t read_stream = nullptr;
@@ -296,6 +306,9 @@ int dpwa_learner_destroy(dpwa_learner *l)
     if (l->ev_factor) (void)hipEventDestroy(l->ev_factor);
     if (l->ev_wt) (void)hipEventDestroy(l->ev_wt);
     if (l->ev_read) (void)hipEventDestroy(l->ev_read);
+    if (l->ev_relay) (void)hipEventDestroy(l->ev_relay);
+    for (char *p : l->relay_opened) (void)hipIpcCloseMemHandle(p);
+    if (l->relay_buf) (void)hipFree(l->relay_buf);
     if (l->read_stream) (void)hipStreamDestroy(l->read_stream);
     if (l->host_status) (void)hipHostFree(l->host_status);
     if (l->slots) (void)hipFree(l->slots);
@@ -390,6 +403,7 @@ int dpwa_learner_attach_local(dpwa_learner *l, int peer_id, dpwa_learner *peer)
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
             return set_error(DPWA_ERR_HIP, "hipDeviceEnablePeerAccess: %s", hipGetErrorString(e));
         (void)hipGetLastError();
+        peer->exported = true;   // read by another GPU: its publishes release at system scope
     }
     Endpoint ep;
     ep.kind = 1;
@@ -486,7 +500,8 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
         }
         const size_t nbytes = kHeader + round_up(l->payload_bytes, 16);
         if (l->pull_mode == DPWA_PULL_KERNEL)
-            HIP_TRY(launch_pull(l->staging, peer_slot, (int64_t)nbytes, l->pull_blocks, l->side));
+            HIP_TRY(launch_pull(l->staging, peer_slot, (int64_t)nbytes, l->pull_blocks,
+                                ep.kind == 2 || ep.device != l->device, l->side));
         else
             HIP_TRY(hipMemcpyAsync(l->staging, peer_slot, nbytes, hipMemcpyDefault, l->side));
         HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
@@ -644,6 +659,151 @@ int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *pay
     l->src_slot = -1;
     l->have_fetch = true;
     l->have_factor = false;
+    return DPWA_OK;
+}
+
+int dpwa_learner_relay_enable(dpwa_learner *l, int world, int rank)
+{
+    if (!l || world < 2 || world > kMaxRelayRanks || rank < 0 || rank >= world)
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_enable: bad world/rank");
+    if (l->relay_on) return set_error(DPWA_ERR_STATE, "dpwa_learner_relay_enable: already enabled");
+    DeviceGuard dg(l->device);
+    const int64_t payload16 = (int64_t)round_up(l->payload_bytes, 16);
+    l->relay_stripe = (int64_t)round_up((size_t)((payload16 + world - 1) / world), 256);
+    HIP_TRY(hipMalloc(&l->relay_buf, (size_t)l->relay_stripe * world));
+    HIP_TRY(hipEventCreateWithFlags(&l->ev_relay, hipEventDisableTiming));
+    l->relay_world = world;
+    l->relay_rank = rank;
+    l->relay_slots.assign((size_t)world, nullptr);
+    l->relay_bufs.assign((size_t)world, nullptr);
+    l->relay_slots[rank] = l->slots;
+    l->relay_bufs[rank] = l->relay_buf;
+    l->relay_on = true;
+    return DPWA_OK;
+}
+
+int dpwa_learner_relay_handle(dpwa_learner *l, void *handle_out, int64_t handle_len)
+{
+    if (!l || !l->relay_on || !handle_out || handle_len < (int64_t)sizeof(IpcBlob))
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_handle: relay not enabled or short buffer");
+    DeviceGuard dg(l->device);
+    IpcBlob b;
+    memset(&b, 0, sizeof(b));
+    HIP_TRY(hipIpcGetMemHandle(&b.handle, l->relay_buf));
+    b.magic = kIpcMagic;
+    b.slot_stride = l->relay_stripe;
+    b.n = l->n;
+    b.dtype = l->dtype;
+    b.device = l->device;
+    b.pid = (int32_t)getpid();
+    memset(handle_out, 0, (size_t)handle_len);
+    memcpy(handle_out, &b, sizeof(b));
+    l->exported = true;
+    return DPWA_OK;
+}
+
+int dpwa_learner_relay_attach(dpwa_learner *l, int rank, int peer_id, const void *relay_handle, int64_t handle_len)
+{
+    if (!l || !l->relay_on || rank < 0 || rank >= l->relay_world || rank == l->relay_rank || !relay_handle ||
+        handle_len < (int64_t)sizeof(IpcBlob))
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_attach: bad arguments");
+    auto it = l->peers.find(peer_id);
+    if (it == l->peers.end() || it->second.kind != 2)
+        return set_error(DPWA_ERR_STATE, "dpwa_learner_relay_attach: peer %d's slots are not IPC-attached", peer_id);
+    IpcBlob b;
+    memcpy(&b, relay_handle, sizeof(b));
+    if (b.magic != kIpcMagic || b.slot_stride != l->relay_stripe || b.n != l->n || b.dtype != l->dtype)
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_attach: relay buffer of rank %d does not match", rank);
+    DeviceGuard dg(l->device);
+    void *ptr = nullptr;
+    HIP_TRY(hipIpcOpenMemHandle(&ptr, b.handle, hipIpcMemLazyEnablePeerAccess));
+    l->relay_opened.push_back((char *)ptr);
+    l->relay_slots[rank] = it->second.base;
+    l->relay_bufs[rank] = (const char *)ptr;
+    return DPWA_OK;
+}
+
+static int relay_args(dpwa_learner *l, const int32_t *picks_dev, uint64_t version, RelayArgs &a)
+{
+    for (int r = 0; r < l->relay_world; ++r)
+        if (!l->relay_slots[r] || !l->relay_bufs[r])
+            return set_error(DPWA_ERR_STATE, "relay: rank %d not attached", r);
+    if (version == 0) return set_error(DPWA_ERR_STATE, "relay: nothing published");
+    memset(&a, 0, sizeof(a));
+    for (int r = 0; r < l->relay_world; ++r) {
+        a.slots[r] = l->relay_slots[r];
+        a.relays[r] = l->relay_bufs[r];
+    }
+    a.relay_mine = l->relay_buf;
+    a.staging = l->staging;
+    a.picks = picks_dev;
+    a.slot_off = (int64_t)((version - 1) % 2) * (int64_t)l->slot_stride;
+    a.stripe = l->relay_stripe;
+    a.payload = (int64_t)round_up(l->payload_bytes, 16);
+    a.world = l->relay_world;
+    a.rank = l->relay_rank;
+    return DPWA_OK;
+}
+
+int dpwa_learner_relay_wait(dpwa_learner *l, dpwa_stream_t stream)
+{
+    if (!l || !l->relay_on) return set_error(DPWA_ERR_STATE, "dpwa_learner_relay_wait: relay not enabled");
+    if (l->relay_pending) {
+        DeviceGuard dg(l->device);
+        HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, l->ev_relay, 0));
+    }
+    return DPWA_OK;
+}
+
+int dpwa_learner_relay_phase1(dpwa_learner *l, const int32_t *picks_dev, uint64_t version, int blocks,
+                              dpwa_stream_t stream)
+{
+    if (!l || !l->relay_on || !picks_dev || blocks < 1)
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_phase1: bad arguments");
+    RelayArgs a;
+    int rc = relay_args(l, picks_dev, version, a);
+    if (rc) return rc;
+    DeviceGuard dg(l->device);
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipEventRecord(l->ev_issue, s));
+    HIP_TRY(hipStreamWaitEvent(l->side, l->ev_issue, 0));
+    HIP_TRY(launch_relay(1, a, blocks, l->side));
+    HIP_TRY(hipEventRecord(l->ev_relay, l->side));
+    l->relay_pending = true;
+    return DPWA_OK;
+}
+
+int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_pick, uint64_t version, int blocks)
+{
+    if (!l || !l->relay_on || !picks_dev || blocks < 1)
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_phase2: bad arguments");
+    RelayArgs a;
+    int rc = relay_args(l, picks_dev, version, a);
+    if (rc) return rc;
+    DeviceGuard dg(l->device);
+    if (my_pick >= 0 && l->consumed_once && l->consume_stream) {   // WAR on staging
+        HIP_TRY(hipEventRecord(l->ev_consumed, l->consume_stream));
+        HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
+    }
+    HIP_TRY(launch_relay(2, a, blocks, l->side));
+    HIP_TRY(hipEventRecord(l->ev_relay, l->side));
+    l->relay_pending = true;
+    if (my_pick >= 0) {
+        HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
+        l->src = l->staging;
+        l->src_copied = true;
+        l->src_owner = nullptr;
+        l->src_slot = -1;
+        l->have_fetch = true;
+        l->have_factor = false;
+    }
+    return DPWA_OK;
+}
+
+int dpwa_learner_side_stream(dpwa_learner *l, dpwa_stream_t *stream)
+{
+    if (!l || !stream) return set_error(DPWA_ERR_ARG, "dpwa_learner_side_stream: NULL argument");
+    *stream = l->side;
     return DPWA_OK;
 }
 

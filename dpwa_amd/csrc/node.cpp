@@ -154,6 +154,11 @@ static int start_fetch(dpwa_node *n, int flags, dpwa_stream_t stream)
         version = learner_version(n->learner);   // lock-step: every node publishes once per round
         zero_copy = 0;
     }
+    if (flags & DPWA_FLAG_PICK_ONLY) {   // the transport moves the bytes (relay)
+        n->fetch_peer = peer;
+        n->fetch_version = version;
+        return DPWA_OK;
+    }
     if ((rc = dpwa_learner_fetch(n->learner, peer, version, zero_copy, stream))) return rc;
     n->fetch_peer = peer;
     n->fetch_version = version;

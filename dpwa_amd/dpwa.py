@@ -208,6 +208,9 @@ class DpwaConnection:
                 self._fail("dpwa_node_publish", rc)
             self._group.after_publish(self)
             rc = self._f_gate(self._node, flags, s, self._out_ref)
+            if not rc:
+                self.fetching = bool(self._out.value)
+                self._group.after_gate(self)
         else:
             rc = self._f_update_send(self._node, p, h, d, flags, s, self._out_ref)
         if rc:
@@ -346,13 +349,38 @@ class DpwaConnection:
         h = ctypes.c_void_p()
         _lib.call("dpwa_node_handles", self._node, ctypes.byref(h), None)
         self._learner = Learner(parameters.device, parameters.numel(), parameters.dtype, handle=h.value)
-        mode, _, blocks = self._pull.partition(":")
-        if mode not in ("copy", "kernel"):
-            raise ValueError("pull must be 'copy' or 'kernel[:blocks]', got %r" % self._pull)
-        _lib.call("dpwa_learner_set_pull", h, _lib.PULL_KERNEL if mode == "kernel" else _lib.PULL_COPY_ENGINE,
-                  int(blocks or 512))
+        if self._pull.partition(":")[0] == "relay":
+            if not hasattr(self._group, "relay_blocks"):
+                raise ValueError("the relay pull needs a DistGroup (one learner per rank)")
+            self._group.relay_blocks = 1     # allocate + exchange the relay buffers in on_bind
         self._group.on_bind(self)
+        self.set_pull(self._pull)
         return self._learner
+
+    def set_pull(self, mode):
+        """Transport of copying fetches: 'copy' (hipMemcpyAsync on the side stream),
+        'kernel[:blocks]' (pull kernel) or 'relay[:blocks]' (DistGroup only, multi-link
+        two-phase relay; the connection must have been created with pull='relay' so the
+        relay buffers exist).  Every rank must switch between the same two rounds."""
+        kind, _, blocks = mode.partition(":")
+        if kind not in ("copy", "kernel", "relay"):
+            raise ValueError("pull must be 'copy', 'kernel[:blocks]' or 'relay[:blocks]', got %r" % mode)
+        self._pull = mode
+        learner = self._learner
+        if learner is None:
+            return
+        torch.cuda.synchronize(learner.device)
+        if kind == "relay":
+            if not getattr(self._group, "relay_ready", False):
+                raise ValueError("relay pull: create the connection with pull='relay' under a DistGroup")
+            self._group.relay_blocks = int(blocks or 64)
+            self._flags |= _lib.FLAG_PICK_ONLY
+            return
+        if getattr(self._group, "relay_blocks", 0):
+            self._group.relay_blocks = 0
+        self._flags &= ~_lib.FLAG_PICK_ONLY
+        _lib.call("dpwa_learner_set_pull", learner.handle, _lib.PULL_KERNEL if kind == "kernel" else
+                  _lib.PULL_COPY_ENGINE, int(blocks or 512))
 
     def _zero_division(self):
         raise ZeroDivisionError("float division by zero (interpolation factor, dpwa.py:143-147)")

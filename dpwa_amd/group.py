@@ -17,6 +17,7 @@ fetch is a device-to-device pull; a group only wires the native nodes' peer tabl
                 stream-ordered barrier after the publish, then each fetch is pulled over
                 xGMI on the learner's side stream while the training step runs.
 """
+import ctypes
 import os
 import threading
 import weakref
@@ -78,6 +79,9 @@ class LocalGroup:
     def after_publish(self, conn):
         pass
 
+    def after_gate(self, conn):
+        pass
+
 
 class DistGroup:
     """One learner per rank; see the module docstring."""
@@ -97,6 +101,10 @@ class DistGroup:
                              % (self.rank, nodes[self.rank]["name"], name))
         self.backend = dist.get_backend(process_group)
         self._flag = None
+        self.relay_blocks = 0        # > 0: relay transport (set by the connection's pull mode)
+        self.relay_ready = False     # relay buffers allocated and exchanged
+        self._picks = None
+        self._pick = None
 
     def join(self, conn):
         pass
@@ -105,13 +113,33 @@ class DistGroup:
         pass
 
     def on_bind(self, conn):
-        """Collective: every rank exports its snapshot allocation and maps every peer's."""
-        handle = conn._learner.ipc_handle()
+        """Collective: every rank exports its snapshot allocation and maps every peer's (and,
+        for the relay transport, its relay buffer)."""
+        learner = conn._learner
+        handle = learner.ipc_handle()
+        relay = b""
+        if self.relay_blocks:
+            _lib.call("dpwa_learner_relay_enable", learner._h, self.world, self.rank)
+            buf = ctypes.create_string_buffer(_lib.IPC_HANDLE_BYTES)
+            _lib.call("dpwa_learner_relay_handle", learner._h, buf, _lib.IPC_HANDLE_BYTES)
+            relay = buf.raw
         handles = [None] * self.world
-        self.dist.all_gather_object(handles, handle, group=self.pg)
+        self.dist.all_gather_object(handles, (handle, relay), group=self.pg)
         for k in range(len(conn.peers)):
-            conn._learner.attach_ipc(k, handles[conn.peer_rank(k)])
+            r = conn.peer_rank(k)
+            learner.attach_ipc(k, handles[r][0])
+            if self.relay_blocks:
+                blob = ctypes.create_string_buffer(bytes(handles[r][1]), _lib.IPC_HANDLE_BYTES)
+                _lib.call("dpwa_learner_relay_attach", learner._h, r, k, blob, _lib.IPC_HANDLE_BYTES)
             conn._set_peer(k, _lib.NODE_PEER_REMOTE, None)
+        if self.relay_blocks:
+            dev = learner.device
+            self._pick = torch.full((1,), -1, dtype=torch.int32, device=dev)
+            self._picks = torch.full((self.world,), -1, dtype=torch.int32, device=dev)
+            side = ctypes.c_void_p()
+            _lib.call("dpwa_learner_side_stream", learner._h, ctypes.byref(side))
+            self._side = torch.cuda.ExternalStream(side.value, device=dev)
+            self.relay_ready = True
 
     def barrier(self, device):
         """Stream-ordered on RCCL (the current stream waits; the host does not)."""
@@ -124,9 +152,49 @@ class DistGroup:
             self.dist.barrier(group=self.pg)
 
     def after_publish(self, conn):
+        if self.relay_blocks:
+            # the relay's barrier is the pick exchange in after_gate; before it, the stream
+            # waits for last round's relay work (its reads of our slot and relay buffer)
+            _lib.call("dpwa_learner_relay_wait", conn._learner._h,
+                      torch.cuda.current_stream(conn._learner.device).cuda_stream)
+            return
         # Every peer's publish of this round is complete (and their fetches of the slot we
         # rewrite two rounds from now are ordered before it) once this returns on the stream.
         self.barrier(conn._learner.device)
+
+    def after_gate(self, conn):
+        """Relay transport: share every rank's pick (this is the round's barrier: all
+        publishes are complete after it), relay phase 1, a barrier on the side stream,
+        phase 2.  Every rank runs this every round, fetching or not."""
+        if not self.relay_blocks:
+            return
+        learner = conn._learner
+        dev = learner.device
+        k = conn._info()[1] if conn.fetching else -1
+        pick = conn.peer_rank(k) if k >= 0 else -1
+        version = learner.native_version()
+        if self.backend == "nccl":
+            self._pick.fill_(pick)
+            self.dist.all_gather_into_tensor(self._picks, self._pick, group=self.pg)
+        else:
+            torch.cuda.current_stream(dev).synchronize()
+            got = [torch.zeros(1, dtype=torch.int32) for _ in range(self.world)]
+            self.dist.all_gather(got, torch.tensor([pick], dtype=torch.int32), group=self.pg)
+            self._picks.copy_(torch.cat(got))
+        cur = torch.cuda.current_stream(dev).cuda_stream
+        _lib.call("dpwa_learner_relay_phase1", learner._h, self._picks.data_ptr(), version,
+                  self.relay_blocks, cur)
+        if self.backend == "nccl":
+            with torch.cuda.stream(self._side):
+                self._flag_side = getattr(self, "_flag_side", None)
+                if self._flag_side is None:
+                    self._flag_side = torch.zeros(1, dtype=torch.int32, device=dev)
+                self.dist.all_reduce(self._flag_side, group=self.pg)
+        else:
+            self._side.synchronize()
+            self.dist.barrier(group=self.pg)
+        _lib.call("dpwa_learner_relay_phase2", learner._h, self._picks.data_ptr(), pick, version,
+                  self.relay_blocks)
 
 
 def default_group(config_file, nodes, name):

@@ -97,6 +97,12 @@ class Learner:
             self._fail("dpwa_learner_publish", rc)
         self.version += 1
 
+    def native_version(self):
+        """dpwa_learner_version: publishes issued so far (no device sync)."""
+        v = ctypes.c_uint64()
+        _lib.call("dpwa_learner_version", self._h, ctypes.byref(v))
+        return v.value
+
     def attach_local(self, peer_id, other):
         _lib.call("dpwa_learner_attach_local", self._h, peer_id, other.handle)
 

@@ -176,6 +176,27 @@ int dpwa_learner_read_snapshot(dpwa_learner *l, void *header_out, void *payload_
 int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *payload, int64_t payload_bytes,
                             dpwa_stream_t stream);
 
+/* Relay transport: a lock-step round's pulls spread over every xGMI link.  Each snapshot is
+ * cut into `world` stripes; phase 1 (after the caller's collective that shares every rank's
+ * pick, so that all publishes of the round are complete) pulls stripe `rank` of every
+ * snapshot another rank needs into this rank's relay buffer; phase 2 (after a second
+ * barrier) gathers this rank's peer's stripes from all ranks into staging and makes it the
+ * fetch in flight (my_pick = rank averaged with, -1 none).  Both phases run on the learner's
+ * side stream; picks_dev holds `world` int32 on this learner's device.
+ * relay_wait makes `stream` wait for the previous round's relay work (call before the next
+ * round's collective, so a slot or relay buffer is rewritten only after every reader). */
+int dpwa_learner_relay_enable(dpwa_learner *l, int world, int rank);
+int dpwa_learner_relay_handle(dpwa_learner *l, void *handle_out, int64_t handle_len);
+int dpwa_learner_relay_attach(dpwa_learner *l, int rank, int peer_id, const void *relay_handle,
+                              int64_t handle_len);
+int dpwa_learner_relay_wait(dpwa_learner *l, dpwa_stream_t stream);
+int dpwa_learner_relay_phase1(dpwa_learner *l, const int32_t *picks_dev, uint64_t version, int blocks,
+                              dpwa_stream_t stream);
+int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_pick, uint64_t version,
+                              int blocks);
+/* The learner's side stream (fetches and relay phases run on it). */
+int dpwa_learner_side_stream(dpwa_learner *l, dpwa_stream_t *stream);
+
 /* Makes `stream` wait for the pull of the fetch in flight, if it copies (TxThread.fetch_wait,
  * conn.py:326-329); average/factor do this themselves -- this only lets a caller order the
  * wait before its own timing event. */
@@ -274,6 +295,7 @@ typedef struct dpwa_node dpwa_node;
 #define DPWA_FLAG_ZERO_COPY 2        /* read a same-device local peer's slot in place              */
 #define DPWA_FLAG_REUSE_SNAPSHOT 4   /* publish: flat unchanged since a write-through average      */
 #define DPWA_FLAG_WRITE_THROUGH 8    /* update_wait_average: also write the next snapshot          */
+#define DPWA_FLAG_PICK_ONLY 16       /* gate (EAGER): pick the peer, the caller moves the bytes    */
 
 /* DpwaConnection.__init__ (dpwa.py:54-93) minus the model: scheduler seeded as
  * dpwa_sched_create, the interpolation config for the learner bound later. */

@@ -78,7 +78,7 @@ FAULTS = {  # rank -> {round: {peer name: fault}}; applied before that round's u
 }
 
 
-def fault_worker(rank, world, port, cfg_path, out_dir, n, T):
+def fault_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy"):
     """Like gossip_worker, with scripted faults (FAULTS) injected into this rank's node."""
     import torch
     import torch.distributed as dist
@@ -90,7 +90,7 @@ def fault_worker(rank, world, port, cfg_path, out_dir, n, T):
     from dpwa_amd import DpwaConnection
     init, deltas, send, wait = inputs(world, n, T)
     names = ["r%d" % i for i in range(world)]
-    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank)
+    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank, pull=pull)
     flat = torch.from_numpy(init[rank]).to(dev)
     params, clocks, peers, scores = np.zeros((T, n), np.float32), np.zeros(T), [], []
     for r in range(T):

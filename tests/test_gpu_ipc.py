@@ -28,9 +28,12 @@ def free_port():
 
 @pytest.mark.parametrize("world,interp,fp,thr,pull", [(2, "clock", 1.0, 0.0, "copy"), (3, "loss", 0.7, 0.5, "copy"),
                                                        (2, "constant", 1.0, 0.0, "kernel:64"),
-                                                       (3, "clock", 0.7, 0.0, "kernel")])
-def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull):
-    n, T = 100_003, 12
+                                                       (3, "clock", 0.7, 0.0, "kernel"),
+                                                       (2, "clock", 1.0, 0.0, "relay:8"),
+                                                       (3, "loss", 0.7, 0.5, "relay"),
+                                                       (4, "clock", 0.6, 0.0, "relay:16")])
+def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100_003):
+    T = 12
     names = ["r%d" % i for i in range(world)]
     cfg = str(tmp_path / "dist.yaml")
     dist_worker.write_cfg(cfg, names, fp, interp, thr)
@@ -46,7 +49,13 @@ def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull):
         assert olerp.bits_equal(got["params"], exp["params"][:, r]), r
 
 
-def test_ipc_gossip_with_injected_faults(tmp_path):
+def test_relay_tiny_payload(tmp_path):
+    """5 parameters over 4 ranks: one 32-B stripe, three empty ones."""
+    test_ipc_gossip_matches_oracle(tmp_path, 4, "constant", 1.0, 0.0, "relay:2", n=5)
+
+
+@pytest.mark.parametrize("pull", ["copy", "relay:8"])
+def test_ipc_gossip_with_injected_faults(tmp_path, pull):
     """Remote peers marked slow (timeouts), down (refused) or dead (removed) steer the
     native scheduler exactly as the reference's TxThread: checked against the oracle fed
     the same outcomes (conn.py:246-313)."""
@@ -54,7 +63,8 @@ def test_ipc_gossip_with_injected_faults(tmp_path):
     names = ["r%d" % i for i in range(world)]
     cfg = str(tmp_path / "faults.yaml")
     dist_worker.write_cfg(cfg, names, 1.0, "clock", 0.0)
-    mp.spawn(dist_worker.fault_worker, args=(world, free_port(), cfg, str(tmp_path), n, T), nprocs=world, join=True)
+    mp.spawn(dist_worker.fault_worker, args=(world, free_port(), cfg, str(tmp_path), n, T, pull), nprocs=world,
+             join=True)
     init, deltas, send, wait = dist_worker.inputs(world, n, T)
     from oracle.policy import OracleLearner
     learners = [OracleLearner(names[g], [x for x in names if x != names[g]], 1.0, "clock", None, 0.0, 500 + g)
