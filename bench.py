@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--pull", default="auto",
                     help="N>1 fetch transport: copy (hipMemcpyAsync), kernel[:blocks], relay[:blocks] "
                          "(two-phase multi-link), or auto (fastest of a short trial)")
+    ap.add_argument("--compute-us", type=float, default=1000.0,
+                    help="per-learner synthetic training step (bf16 GEMM loop) for the 'overlap' field; 0 = skip")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="PMC traffic summary (rocprofv3 FETCH_SIZE/WRITE_SIZE passes) to report")
     return ap.parse_args()
@@ -234,6 +236,65 @@ def main():
             return float(tmax.item()), float(sums[0].item()), float(sums[1].item()), lerp_ms
         return elapsed, float(averaged), float(len(learners) * steps), lerp_ms
 
+    def make_compute(target_us):
+        """A fixed-duration stand-in for a training step: k back-to-back
+        4096^3 bf16 GEMMs on the compute stream, k calibrated to ~target_us."""
+        a = torch.randn(4096, 4096, device=device, dtype=torch.bfloat16)
+        b = torch.randn(4096, 4096, device=device, dtype=torch.bfloat16)
+        c = torch.empty(4096, 4096, device=device, dtype=torch.bfloat16)
+        for _ in range(5):
+            torch.matmul(a, b, out=c)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(20):
+            torch.matmul(a, b, out=c)
+        e1.record()
+        torch.cuda.synchronize()
+        per_us = e0.elapsed_time(e1) * 1e3 / 20
+        k = max(1, int(round(target_us / per_us)))
+        if world > 1:            # every rank runs the same step
+            kt = torch.tensor([k], dtype=torch.int64, device=device if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+            k = int(kt.item())
+
+        def compute():
+            for _ in range(k):
+                torch.matmul(a, b, out=c)
+        return compute, k, per_us
+
+    def run_overlap(steps, warmup, compute, gossip):
+        """Training-loop shape (main.py:122-158): update_send, the step, update_wait."""
+        def step():
+            done = 0
+            if gossip:
+                for conn, flat in learners:
+                    conn.update_send(flat, loss)
+            for _ in learners:
+                compute()
+            if gossip:
+                for conn, flat in learners:
+                    payload, _ = conn.update_wait_average(flat, loss)
+                    done += payload is not None
+            return done
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                          device=device if args.dist_backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item())
+
     def set_pull(mode):
         for conn, _ in learners:
             conn.set_pull(mode)
@@ -254,6 +315,22 @@ def main():
         set_pull(pull)
     elapsed, averaged, rounds, lerp_ms = run(args.steps, args.warmup, False, args.sample_every)
     wt = run(args.steps, args.warmup, True, args.sample_every) if not args.no_write_through else None
+    overlap = None
+    if args.compute_us > 0:
+        compute, k_gemm, gemm_us = make_compute(args.compute_us)
+        o_steps = max(20, args.steps // 4)
+        t_compute = run_overlap(o_steps, 3, compute, gossip=False)
+        t_both = run_overlap(o_steps, 3, compute, gossip=True)
+        overlap = {
+            "compute": "%d x bf16 GEMM 4096^3 per learner per step (%.1f us each)" % (k_gemm, gemm_us),
+            "steps": o_steps,
+            "compute_only_ms_per_step": round(1e3 * t_compute / o_steps, 4),
+            "ms_per_step": round(1e3 * t_both / o_steps, 4),
+            "gossip_overhead_frac": round(t_both / t_compute - 1.0, 4),
+            "rounds_per_s_per_learner": round(o_steps / t_both, 1),
+            "note": "update_send -> synthetic training step -> update_wait_average (SURVEY §8d C4 "
+                    "weak scaling): the overhead the gossip round adds to a step of this length",
+        }
 
     unit_bytes = 3 * args.numel * esize
     if rank == 0:
@@ -325,6 +402,8 @@ def main():
                 "avg_launch_us": round(w_us, 2),
                 "kernel_gbs_4ns": round(4 * args.numel * esize / (w_us * 1e-6) / 1e9, 1),
             }
+        if overlap is not None:
+            out["overlap"] = overlap
         if world == 1 and not args.no_cold:
             gbs, us, pairs = cold_kernel(args.numel, dtype, device)
             out["roofline"]["cold_cache"] = {"achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
