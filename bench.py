@@ -51,7 +51,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
     ap.add_argument("--no-write-through", action="store_true", help="skip the write-through variant")
-    ap.add_argument("--sample-every", type=int, default=4, help="time the averaging kernel every k-th step")
+    ap.add_argument("--sample-every", type=int, default=8,
+                    help="time the averaging kernel every k-th step (a timed launch costs a few µs)")
+    ap.add_argument("--timing", choices=["dispatch", "bracket", "both"], default="dispatch",
+                    help="averaging-kernel timing: its own dispatch events (hipExtLaunchKernelGGL), an event "
+                         "pair recorded around the launch, or both")
     ap.add_argument("--streams", default="one", choices=["one", "per-learner"],
                     help="stream per co-resident learner (their kernels may overlap) or one shared stream")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -182,10 +186,13 @@ def main():
 
     def run(steps, warmup, write_through, sample_every):
         """`steps` timed lock-step rounds; the averaging kernel of every `sample_every`-th
-        step is bracketed by HIP events on its stream."""
+        step is timed by its own dispatch events (and, as a cross-check, bracketed by an
+        event pair on its stream)."""
         lerp_events = []
         events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range((steps // sample_every + 1) * len(learners))]
+        lib = _lib.load()
+        timed_learners = []
 
         def step(k, timed):
             done = 0
@@ -199,11 +206,14 @@ def main():
                     # the adapter's update_wait: fused device factor + lerp (one kernel)
                     if sample:
                         a, b = events[len(lerp_events)]
-                        if world > 1:    # the pull is TxThread's part: order its wait before the timing event
+                        if world > 1 and args.timing != "dispatch":   # keep the pull wait out of the bracket
                             _lib.load().dpwa_learner_wait_fetch(conn._learner.handle, st.cuda_stream)
-                        a.record(st)
+                        if args.timing != "dispatch":
+                            a.record(st)
+                        if args.timing != "bracket" and conn in timed_learners:
+                            lib.dpwa_learner_arm_timing(conn._learner.handle)
                     payload, _ = conn.update_wait_average(flat, loss, write_through=write_through)
-                    if sample:
+                    if sample and args.timing != "dispatch":
                         b.record(st)
                         if payload is not None:
                             lerp_events.append((a, b))
@@ -212,6 +222,10 @@ def main():
 
         for k in range(warmup):
             step(k, False)
+        for conn, _ in learners:    # kernel-dispatch timing of the sampled averaging launches
+            if conn._learner is not None:
+                _lib.call("dpwa_learner_time_averages", conn._learner.handle, steps // sample_every + 1)
+                timed_learners.append(conn)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -225,7 +239,17 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        lerp_ms = np.array([a.elapsed_time(b) for a, b in lerp_events]) if lerp_events else np.array([np.nan])
+        bracket_ms = np.array([a.elapsed_time(b) for a, b in lerp_events]) if lerp_events else np.array([np.nan])
+        kern_us = []
+        for conn in timed_learners:
+            buf = (ctypes.c_float * len(events))()
+            cnt = ctypes.c_int()
+            _lib.call("dpwa_learner_read_average_times", conn._learner.handle, buf, len(events), ctypes.byref(cnt))
+            kern_us += list(buf[:cnt.value])
+            _lib.call("dpwa_learner_time_averages", conn._learner.handle, 0)
+        if args.timing == "bracket":
+            kern_us = list(bracket_ms * 1e3)
+        lerp_ms = (np.array(kern_us) / 1e3 if kern_us else np.array([np.nan]), bracket_ms)
         stats = torch.tensor([elapsed, float(averaged), float(len(learners) * steps)], dtype=torch.float64,
                              device=device if args.dist_backend == "nccl" else "cpu")
         if world > 1:
@@ -313,7 +337,7 @@ def main():
             pull_trials[mode] = round(av * 3 * args.numel * esize / el / 1e9, 2)
         pull = max(pull_trials, key=pull_trials.get)
         set_pull(pull)
-    elapsed, averaged, rounds, lerp_ms = run(args.steps, args.warmup, False, args.sample_every)
+    elapsed, averaged, rounds, (lerp_ms, bracket_ms) = run(args.steps, args.warmup, False, args.sample_every)
     wt = run(args.steps, args.warmup, True, args.sample_every) if not args.no_write_through else None
     overlap = None
     if args.compute_us > 0:
@@ -384,13 +408,19 @@ def main():
                 "bytes_per_launch": unit_bytes,
                 "avg_launch_us": round(lerp_us, 2),
                 "launches_timed": int(np.isfinite(lerp_ms).sum()),
+                "timing": ("kernel dispatch begin/end events (hipExtLaunchKernelGGL) on the averaging "
+                           "kernel's own stream" if args.timing != "bracket" else
+                           "HIP event pair recorded around the launch on its stream")
+                          + ", every %d-th step" % args.sample_every,
+                "event_bracket_us": (round(float(np.nanmean(bracket_ms) * 1e3), 2)
+                                     if args.timing != "dispatch" else None),
                 "traffic_source": traffic_src,
             },
         }
         if pull_trials:
             out["pull_trials_gbs"] = pull_trials
         if wt is not None:
-            w_el, w_avg, w_rounds, w_ms = wt
+            w_el, w_avg, w_rounds, (w_ms, _) = wt
             w_us = float(np.nanmean(w_ms) * 1e3)
             out["write_through"] = {
                 "value": round(w_avg * unit_bytes / w_el / 1e9, 2),

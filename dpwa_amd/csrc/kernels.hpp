@@ -32,9 +32,16 @@ struct FusedArgs {
 hipError_t launch_lerp(int32_t dtype, void *param, const void *peer, int64_t n, const dpwa_coef *coef,
                        float a, float b, hipStream_t s);
 
+// Optional timing of one launch: HIP records the kernel's own begin/end in the two events
+// (hipExtLaunchKernelGGL), so the figure excludes the dispatch gaps an event pair around the
+// launch would add.
+struct LaunchTiming {
+    hipEvent_t start, stop;
+};
+
 // Fused factor + lerp (one launch); a non-null `snap` also receives the result.
 hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa,
-                          void *snap, hipStream_t s);
+                          void *snap, hipStream_t s, const LaunchTiming *timing = nullptr);
 
 // Factor + clock only (one thread).
 hipError_t launch_factor(const FusedArgs &fa, hipStream_t s);

@@ -148,6 +148,10 @@ struct dpwa_learner {
     const void *wt_flat = nullptr;
     hipStream_t wt_stream = nullptr;
     hipEvent_t ev_wt = nullptr;
+    // timing of the averaging launches (bench): kernel begin/end events, filled in order
+    std::vector<LaunchTiming> timing;
+    int timing_used = 0;
+    bool timing_armed = false;   // time the next averaging launch (one-shot)
     // relay transport (multi-link lock-step pulls), see kernels.hip
     bool relay_on = false;
     int relay_world = 0, relay_rank = 0;
@@ -307,6 +311,10 @@ int dpwa_learner_destroy(dpwa_learner *l)
     if (l->ev_wt) (void)hipEventDestroy(l->ev_wt);
     if (l->ev_read) (void)hipEventDestroy(l->ev_read);
     if (l->ev_relay) (void)hipEventDestroy(l->ev_relay);
+    for (auto &t : l->timing) {
+        (void)hipEventDestroy(t.start);
+        (void)hipEventDestroy(t.stop);
+    }
     for (char *p : l->relay_opened) (void)hipIpcCloseMemHandle(p);
     if (l->relay_buf) (void)hipFree(l->relay_buf);
     if (l->read_stream) (void)hipStreamDestroy(l->read_stream);
@@ -570,7 +578,11 @@ static int average_impl(dpwa_learner *l, void *flat, double loss, const double *
         snap = l->slots + (size_t)k * l->slot_stride + kHeader;
     }
     if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
-    HIP_TRY(launch_average(l->dtype, flat, l->src + kHeader, l->n, fused_args(l, loss, loss_dev), snap, s));
+    const LaunchTiming *timing = nullptr;
+    if (l->timing_armed && l->timing_used < (int)l->timing.size() && ((uintptr_t)flat & 15) == 0)
+        timing = &l->timing[l->timing_used++];
+    l->timing_armed = false;
+    HIP_TRY(launch_average(l->dtype, flat, l->src + kHeader, l->n, fused_args(l, loss, loss_dev), snap, s, timing));
     l->consume_stream = s;
     l->consumed_once = true;
     l->cur ^= 1;
@@ -797,6 +809,50 @@ int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_
         l->have_fetch = true;
         l->have_factor = false;
     }
+    return DPWA_OK;
+}
+
+int dpwa_learner_time_averages(dpwa_learner *l, int capacity)
+{
+    if (!l || capacity < 0) return set_error(DPWA_ERR_ARG, "dpwa_learner_time_averages: bad arguments");
+    DeviceGuard dg(l->device);
+    HIP_TRY(hipDeviceSynchronize());
+    for (auto &t : l->timing) {
+        (void)hipEventDestroy(t.start);
+        (void)hipEventDestroy(t.stop);
+    }
+    l->timing.clear();
+    l->timing_used = 0;
+    l->timing_armed = false;
+    for (int i = 0; i < capacity; ++i) {
+        LaunchTiming t{};
+        HIP_TRY(hipEventCreate(&t.start));
+        HIP_TRY(hipEventCreate(&t.stop));
+        l->timing.push_back(t);
+    }
+    return DPWA_OK;
+}
+
+int dpwa_learner_arm_timing(dpwa_learner *l)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_arm_timing: NULL learner");
+    l->timing_armed = true;
+    return DPWA_OK;
+}
+
+int dpwa_learner_read_average_times(dpwa_learner *l, float *us_out, int max, int *count)
+{
+    if (!l || !count || (max > 0 && !us_out)) return set_error(DPWA_ERR_ARG, "dpwa_learner_read_average_times: bad arguments");
+    DeviceGuard dg(l->device);
+    const int k = l->timing_used < max ? l->timing_used : max;
+    for (int i = 0; i < k; ++i) {
+        HIP_TRY(hipEventSynchronize(l->timing[i].stop));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, l->timing[i].start, l->timing[i].stop));
+        us_out[i] = ms * 1000.f;
+    }
+    *count = k;
+    l->timing_used = 0;
     return DPWA_OK;
 }
 

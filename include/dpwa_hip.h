@@ -194,6 +194,15 @@ int dpwa_learner_relay_phase1(dpwa_learner *l, const int32_t *picks_dev, uint64_
                               dpwa_stream_t stream);
 int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_pick, uint64_t version,
                               int blocks);
+/* Kernel timing for measurement.  time_averages allocates `capacity` begin/end event pairs
+ * (0 frees them; synchronises the device).  After arm_timing, the next averaging launch
+ * (average / average_through, 16-B aligned parameters) goes through hipExtLaunchKernelGGL
+ * with the next free pair, so it is timed as a profiler times it, without the dispatch gaps
+ * of an event pair recorded around the launch.  read_average_times waits for and returns the
+ * recorded durations (µs, launch order) and frees the pairs for reuse. */
+int dpwa_learner_time_averages(dpwa_learner *l, int capacity);
+int dpwa_learner_arm_timing(dpwa_learner *l);
+int dpwa_learner_read_average_times(dpwa_learner *l, float *us_out, int max, int *count);
 /* The learner's side stream (fetches and relay phases run on it). */
 int dpwa_learner_side_stream(dpwa_learner *l, dpwa_stream_t *stream);
 

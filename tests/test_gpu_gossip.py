@@ -346,3 +346,39 @@ def test_connection_write_through_and_reuse(tmp_path):
             conns[g].update_wait_average(flats[g], wait[r][g], write_through=True)
     for g in range(G):
         assert olerp.bits_equal(flats[g].cpu().numpy(), exp["params"][-1, g]), g
+
+
+def test_kernel_dispatch_timing(tmp_path):
+    """dpwa_learner_time_averages / arm_timing / read_average_times: only armed launches are
+    timed, the durations are positive, and timing does not change the results."""
+    import ctypes
+    from dpwa_amd import _lib
+    cfg = tmp_path / "t.yaml"
+    write_cfg(cfg, ["a", "b"], 1.0, "constant", 0.0, 0.5)
+    group = LocalGroup()
+    n = 1 << 20
+    flats = [torch.randn(n, device=DEV), torch.randn(n, device=DEV)]
+    want = (0.5 * flats[1] + 0.5 * flats[0]).clone()
+    conns = [DpwaConnection(nm, str(cfg), seed=i, group=group) for i, nm in enumerate(["a", "b"])]
+    for c, f in zip(conns, flats):
+        c.update_send(f, 1.0)
+    h = conns[0]._learner.handle
+    _lib.call("dpwa_learner_time_averages", h, 4)
+    _lib.call("dpwa_learner_arm_timing", h)
+    for c, f in zip(conns, flats):
+        c.update_wait_average(f, 1.0)
+    for r in range(3):                     # unarmed rounds are not timed
+        for c, f in zip(conns, flats):
+            c.update_send(f, 1.0)
+        for c, f in zip(conns, flats):
+            c.update_wait_average(f, 1.0)
+    buf = (ctypes.c_float * 4)()
+    cnt = ctypes.c_int()
+    _lib.call("dpwa_learner_read_average_times", h, buf, 4, ctypes.byref(cnt))
+    assert cnt.value == 1
+    assert 0.0 < buf[0] < 10_000.0
+    torch.cuda.synchronize()
+    assert torch.equal(flats[0], want) and torch.equal(flats[1], want)   # f = 0.5 fixed point
+    _lib.call("dpwa_learner_time_averages", h, 0)
+    for c in conns:
+        c.close()
