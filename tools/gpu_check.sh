@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU-box pass: GPU parity tests, the default bench line, the kernel variant sweep
+# (cold and Infinity-Cache warm), and the rocprofv3 kernel summary of the bench command.
+# Usage (from this container): gpurun --timeout 1200 -- bash tools/gpu_check.sh
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+    > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest -m gpu failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
+if [ -x tools/lerp_tune ]; then
+    timeout -k 10 120 ./tools/lerp_tune 11173962 10 > gpurun_out/tune_cold.log 2>&1 || exit 1
+    timeout -k 10 120 ./tools/lerp_tune 11173962 10 1 > gpurun_out/tune_warm.log 2>&1 || exit 1
+fi
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+    python bench.py --no-cpu-baseline > gpurun_out/bench_rocprof.json 2> gpurun_out/bench_rocprof.err || { echo "rocprof run failed"; exit 1; }
+cat gpurun_out/bench_rocprof.json
+echo done

@@ -127,6 +127,76 @@ __global__ __launch_bounds__(BLOCK) void k_one(f32x4 *__restrict__ param, const 
     if (DUAL) st(snap + i, r, NT_ST);
 }
 
+// One item per lane with a cache policy per operand (nt = streamed once, no reuse).
+template <int BLOCK, bool NTQ, bool NTP, bool NTS>
+__global__ __launch_bounds__(BLOCK) void k_one_nt(f32x4 *__restrict__ param, const f32x4 *__restrict__ peer,
+                                                  int64_t n4, float a, float b)
+{
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n4) return;
+    const f32x4 q = ld(peer + i, NTQ);
+    const f32x4 p = ld(param + i, NTP);
+    st(param + i, lerp4(a, b, q, p), NTS);
+}
+
+// One item per lane, blockIdx remapped so that each XCD (blocks are dealt round-robin over
+// the 8 XCDs) sweeps one contiguous eighth of the buffer.  Grid padded to a multiple of 8.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_one_xcd(f32x4 *__restrict__ param, const f32x4 *__restrict__ peer,
+                                                   int64_t n4, float a, float b)
+{
+    const uint32_t per = gridDim.x / 8;
+    const uint32_t t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    const int64_t i = (int64_t)t * BLOCK + threadIdx.x;
+    if (i >= n4) return;
+    param[i] = lerp4(a, b, peer[i], param[i]);
+}
+
+// Buffer loads/stores (range-checked, no branch) with explicit aux cache bits
+// (gfx950: 1 = sc0, 2 = nt, 16 = sc1).  32-bit byte offsets: operands < 2 GiB.
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+template <int BLOCK, int AUXQ, int AUXP, int AUXS>
+__global__ __launch_bounds__(BLOCK) void k_buf(float *__restrict__ param, const float *__restrict__ peer, int64_t n4,
+                                               float a, float b)
+{
+    const int nbytes = (int)(n4 * 16);
+    __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(param, 0, nbytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)peer, 0, nbytes, 0x00020000);
+    const int off = (int)(((int64_t)blockIdx.x * BLOCK + threadIdx.x) * 16);
+    const u32x4v q = __builtin_amdgcn_raw_buffer_load_b128(rq, off, 0, AUXQ);
+    const u32x4v p = __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, AUXP);
+    const f32x4 r = lerp4(a, b, __builtin_bit_cast(f32x4, q), __builtin_bit_cast(f32x4, p));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, r), rp, off, 0, AUXS);
+}
+
+// Two items per lane, block-contiguous (512 items per 256-thread block): all four loads are
+// issued before the first store.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_two(f32x4 *__restrict__ param, const f32x4 *__restrict__ peer, int64_t n4,
+                                               float a, float b)
+{
+    const int64_t i = (int64_t)blockIdx.x * (2 * BLOCK) + threadIdx.x;
+    const int64_t j = i + BLOCK;
+    if (j < n4) {
+        const f32x4 q0 = peer[i], p0 = param[i], q1 = peer[j], p1 = param[j];
+        param[i] = lerp4(a, b, q0, p0);
+        param[j] = lerp4(a, b, q1, p1);
+    } else if (i < n4) {
+        param[i] = lerp4(a, b, peer[i], param[i]);
+    }
+}
+
+// One-item-per-lane buffer copy (the publish shape) with a load cache policy.
+template <int BLOCK, int AUXL>
+__global__ __launch_bounds__(BLOCK) void k_copybuf(float *__restrict__ dst, const float *__restrict__ src, int64_t n4)
+{
+    const int nbytes = (int)(n4 * 16);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(dst, 0, nbytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, nbytes, 0x00020000);
+    const int off = (int)(((int64_t)blockIdx.x * BLOCK + threadIdx.x) * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUXL), rd, off, 0, 0);
+}
+
 // Copy (1R:1W) and read-only reduction, for calibration.
 __global__ __launch_bounds__(256) void k_copy(f32x4 *__restrict__ dst, const f32x4 *__restrict__ src, int64_t n4)
 {
@@ -201,13 +271,66 @@ Variant one(const char *name)
             }};
 }
 
+template <int BLOCK, bool NTQ, bool NTP, bool NTS>
+Variant one_nt(const char *name)
+{
+    return {name, 3.0, [](float *p, float *q, int64_t n, hipStream_t s) {
+                int64_t n4 = n / 4;
+                hipLaunchKernelGGL((k_one_nt<BLOCK, NTQ, NTP, NTS>), dim3(grid_for(n4, BLOCK, 0)), dim3(BLOCK), 0, s,
+                                   (f32x4 *)p, (const f32x4 *)q, n4, 0.5f, 0.5f);
+            }};
+}
+
+template <int BLOCK>
+Variant one_xcd(const char *name)
+{
+    return {name, 3.0, [](float *p, float *q, int64_t n, hipStream_t s) {
+                int64_t n4 = n / 4;
+                int g = (grid_for(n4, BLOCK, 0) + 7) / 8 * 8;
+                hipLaunchKernelGGL((k_one_xcd<BLOCK>), dim3(g), dim3(BLOCK), 0, s, (f32x4 *)p, (const f32x4 *)q, n4,
+                                   0.5f, 0.5f);
+            }};
+}
+
+template <int BLOCK, int AQ, int AP, int AS>
+Variant buf(const char *name)
+{
+    return {name, 3.0, [](float *p, float *q, int64_t n, hipStream_t s) {
+                int64_t n4 = n / 4;
+                hipLaunchKernelGGL((k_buf<BLOCK, AQ, AP, AS>), dim3(grid_for(n4, BLOCK, 0)), dim3(BLOCK), 0, s, p, q,
+                                   n4, 0.5f, 0.5f);
+            }};
+}
+
+template <int BLOCK>
+Variant two(const char *name)
+{
+    return {name, 3.0, [](float *p, float *q, int64_t n, hipStream_t s) {
+                int64_t n4 = n / 4;
+                hipLaunchKernelGGL((k_two<BLOCK>), dim3(grid_for(n4, 2 * BLOCK, 0)), dim3(BLOCK), 0, s, (f32x4 *)p,
+                                   (const f32x4 *)q, n4, 0.5f, 0.5f);
+            }};
+}
+
+template <int BLOCK, int AUXL>
+Variant copybuf(const char *name)
+{
+    return {name, 2.0, [](float *p, float *q, int64_t n, hipStream_t s) {
+                int64_t n4 = n / 4;
+                hipLaunchKernelGGL((k_copybuf<BLOCK, AUXL>), dim3(grid_for(n4, BLOCK, 0)), dim3(BLOCK), 0, s, p, q, n4);
+            }};
+}
+
 int main(int argc, char **argv)
 {
     int64_t n = argc > 1 ? atoll(argv[1]) : 11173962;
     int rounds = argc > 2 ? atoi(argv[2]) : 20;
     n = n / 4 * 4;
     const size_t bytes = (size_t)n * 4;
+    // argv[3]: buffer pairs to rotate over (default: > 1.5 GB between reuses = cold;
+    // 1 = the same pair every launch, Infinity-Cache warm like the in-loop kernel)
     int pairs = (int)std::max<size_t>(4, (size_t)(1.5e9 / (2 * bytes)) + 1);
+    if (argc > 3) pairs = std::max(1, atoi(argv[3]));
     std::vector<float *> P(pairs), Q(pairs);
     for (int i = 0; i < pairs; ++i) {
         CHECK(hipMalloc(&P[i], bytes));
@@ -220,27 +343,31 @@ int main(int argc, char **argv)
     CHECK(hipMalloc(&g_snap, bytes));
     std::vector<Variant> vs = {
         one<256, false, false>("one256 (product)"),
-        one<512, false, false>("one512"),
-        one<1024, false, false>("one1024"),
-        one<256, false, true>("one256 ntST"),
+        one<64, false, false>("one64"),
         one<256, true, false>("one256 DUAL (x4 bytes)"),
-        one<256, true, true>("one256 DUAL ntST (x4 bytes)"),
-        pipe<256, false>("pipe256 cap1024", 1024),
-        pipe<256, false>("pipe256 cap2048", 2048),
-        pipe<256, false>("pipe256 cap4096", 4096),
-        pipe<256, false>("pipe256 cap8192", 8192),
-        pipe<512, false>("pipe512 cap2048", 2048),
-        pipe<256, true>("pipe256 cap2048 ntST", 2048),
-        gs<256, 4, false, false, false>("gs256x4 cap2048", 2048),
-        gs<256, 4, false, false, false>("gs256x4 exact", 0),
-        gs<256, 2, false, false, false>("gs256x2 exact", 0),
-        gs<512, 4, false, false, false>("gs512x4 exact", 0),
-        tile<256, 4, false>("tile256x4 exact", 0),
+        buf<256, 0, 0, 0>("buf256"),
+        buf<256, 1, 1, 0>("buf256 sc0 loads"),
+        buf<256, 16, 16, 0>("buf256 sc1 loads"),
+        buf<256, 17, 17, 0>("buf256 sc0sc1 loads"),
+        buf<256, 2, 2, 0>("buf256 nt loads"),
+        buf<256, 3, 3, 0>("buf256 nt+sc0 loads"),
+        buf<256, 18, 18, 0>("buf256 nt+sc1 loads"),
+        buf<256, 19, 19, 0>("buf256 nt+sc0sc1 loads"),
+        buf<256, 2, 2, 2>("buf256 nt all"),
+        buf<256, 2, 2, 16>("buf256 nt loads sc1 store"),
+        buf<256, 2, 2, 18>("buf256 nt loads nt+sc1 store"),
+        buf<64, 2, 2, 0>("buf64 nt loads"),
+        buf<128, 2, 2, 0>("buf128 nt loads"),
+        buf<512, 2, 2, 0>("buf512 nt loads"),
+        buf<1024, 2, 2, 0>("buf1024 nt loads"),
+        buf<64, 0, 0, 0>("buf64"),
         {"copy 1R1W (x2 bytes)", 2.0,
          [](float *p, float *q, int64_t n, hipStream_t s) {
              int64_t n4 = n / 4;
              hipLaunchKernelGGL(k_copy, dim3(grid_for(n4, 1024, 0)), dim3(256), 0, s, (f32x4 *)p, (const f32x4 *)q, n4);
          }},
+        copybuf<256, 0>("copybuf256 (x2 bytes)"),
+        copybuf<256, 2>("copybuf256 nt load (x2 bytes)"),
         {"hipMemcpyAsync D2D (x2 bytes)", 2.0,
          [](float *p, float *q, int64_t n, hipStream_t s) { (void)hipMemcpyAsync(p, q, n * 4, hipMemcpyDeviceToDevice, s); }},
     };
