@@ -187,14 +187,14 @@ __global__ __launch_bounds__(BLOCK) void k_two(f32x4 *__restrict__ param, const 
 }
 
 // One-item-per-lane buffer copy (the publish shape) with a load cache policy.
-template <int BLOCK, int AUXL>
+template <int BLOCK, int AUXL, int AUXS>
 __global__ __launch_bounds__(BLOCK) void k_copybuf(float *__restrict__ dst, const float *__restrict__ src, int64_t n4)
 {
     const int nbytes = (int)(n4 * 16);
     __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(dst, 0, nbytes, 0x00020000);
     __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, nbytes, 0x00020000);
     const int off = (int)(((int64_t)blockIdx.x * BLOCK + threadIdx.x) * 16);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUXL), rd, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUXL), rd, off, 0, AUXS);
 }
 
 // Copy (1R:1W) and read-only reduction, for calibration.
@@ -312,12 +312,12 @@ Variant two(const char *name)
             }};
 }
 
-template <int BLOCK, int AUXL>
+template <int BLOCK, int AUXL, int AUXS>
 Variant copybuf(const char *name)
 {
     return {name, 2.0, [](float *p, float *q, int64_t n, hipStream_t s) {
                 int64_t n4 = n / 4;
-                hipLaunchKernelGGL((k_copybuf<BLOCK, AUXL>), dim3(grid_for(n4, BLOCK, 0)), dim3(BLOCK), 0, s, p, q, n4);
+                hipLaunchKernelGGL((k_copybuf<BLOCK, AUXL, AUXS>), dim3(grid_for(n4, BLOCK, 0)), dim3(BLOCK), 0, s, p, q, n4);
             }};
 }
 
@@ -335,39 +335,33 @@ int main(int argc, char **argv)
     for (int i = 0; i < pairs; ++i) {
         CHECK(hipMalloc(&P[i], bytes));
         CHECK(hipMalloc(&Q[i], bytes));
-        CHECK(hipMemset(P[i], 0, bytes));
-        CHECK(hipMemset(Q[i], 0, bytes));
+        std::vector<float> h((size_t)n);
+        uint32_t x = 12345u + (uint32_t)i;
+        for (auto &v : h) {   // random data (zero-filled operands can change the clock the chip holds)
+            x = x * 1664525u + 1013904223u;
+            v = (float)((int32_t)(x >> 8) - (1 << 23)) / (float)(1 << 23);
+        }
+        CHECK(hipMemcpy(P[i], h.data(), bytes, hipMemcpyHostToDevice));
+        CHECK(hipMemcpy(Q[i], h.data(), bytes, hipMemcpyHostToDevice));
     }
     hipStream_t s;
     CHECK(hipStreamCreate(&s));
     CHECK(hipMalloc(&g_snap, bytes));
     std::vector<Variant> vs = {
-        one<256, false, false>("one256 (product)"),
-        one<64, false, false>("one64"),
-        one<256, true, false>("one256 DUAL (x4 bytes)"),
-        buf<256, 0, 0, 0>("buf256"),
-        buf<256, 1, 1, 0>("buf256 sc0 loads"),
-        buf<256, 16, 16, 0>("buf256 sc1 loads"),
-        buf<256, 17, 17, 0>("buf256 sc0sc1 loads"),
-        buf<256, 2, 2, 0>("buf256 nt loads"),
-        buf<256, 3, 3, 0>("buf256 nt+sc0 loads"),
-        buf<256, 18, 18, 0>("buf256 nt+sc1 loads"),
-        buf<256, 19, 19, 0>("buf256 nt+sc0sc1 loads"),
-        buf<256, 2, 2, 2>("buf256 nt all"),
-        buf<256, 2, 2, 16>("buf256 nt loads sc1 store"),
-        buf<256, 2, 2, 18>("buf256 nt loads nt+sc1 store"),
-        buf<64, 2, 2, 0>("buf64 nt loads"),
-        buf<128, 2, 2, 0>("buf128 nt loads"),
-        buf<512, 2, 2, 0>("buf512 nt loads"),
-        buf<1024, 2, 2, 0>("buf1024 nt loads"),
-        buf<64, 0, 0, 0>("buf64"),
-        {"copy 1R1W (x2 bytes)", 2.0,
-         [](float *p, float *q, int64_t n, hipStream_t s) {
-             int64_t n4 = n / 4;
-             hipLaunchKernelGGL(k_copy, dim3(grid_for(n4, 1024, 0)), dim3(256), 0, s, (f32x4 *)p, (const f32x4 *)q, n4);
-         }},
-        copybuf<256, 0>("copybuf256 (x2 bytes)"),
-        copybuf<256, 2>("copybuf256 nt load (x2 bytes)"),
+        one<256, false, false>("one256 (r01a product)"),
+        buf<256, 2, 2, 16>("buf256 nt loads sc1 store (product)"),
+        buf<256, 2, 2, 17>("buf256 nt loads sc0sc1 store"),
+        buf<256, 2, 0, 17>("buf256 nt peer sc0sc1 store"),
+        buf<64, 2, 2, 16>("buf64 nt loads sc1 store"),
+        buf<64, 2, 2, 17>("buf64 nt loads sc0sc1 store"),
+        buf<64, 2, 0, 16>("buf64 nt peer sc1 store"),
+        buf<64, 2, 0, 17>("buf64 nt peer sc0sc1 store"),
+        buf<128, 2, 2, 17>("buf128 nt loads sc0sc1 store"),
+        buf<128, 2, 2, 16>("buf128 nt loads sc1 store"),
+        copybuf<256, 2, 16>("copybuf256 nt load sc1 store (x2 bytes)"),
+        copybuf<256, 2, 17>("copybuf256 nt load sc0sc1 store (x2 bytes)"),
+        copybuf<64, 2, 16>("copybuf64 nt load sc1 store (x2 bytes)"),
+        copybuf<64, 2, 17>("copybuf64 nt load sc0sc1 store (x2 bytes)"),
         {"hipMemcpyAsync D2D (x2 bytes)", 2.0,
          [](float *p, float *q, int64_t n, hipStream_t s) { (void)hipMemcpyAsync(p, q, n * 4, hipMemcpyDeviceToDevice, s); }},
     };
