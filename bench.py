@@ -17,8 +17,10 @@ fetch_probability 1.
 ``value`` = algorithmic averaged bytes (3 * numel * sizeof(dtype) per completed
 averaging) summed over all learners / the max-over-ranks wall time of the
 K timed steps.  ``roofline`` prices the lerp kernel alone from HIP events recorded around
-every lerp launch on the stream it runs on.  ``cpu_baseline`` times the C oracle's
-restatement of the same round (publish copy + averaging) on one host core.
+every lerp launch on the stream it runs on.  ``cpu_baseline`` times the reference's own CPU
+round restated (oracle/ref_round.py: two learner processes on localhost TCP, pickle framing,
+numpy fp32 lerp -- the path this one replaces) on the box's host cores before the GPU is
+touched, and beside it the C oracle's round (publish copy + averaging) on one host core.
 """
 import argparse
 import ctypes
@@ -37,6 +39,9 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 RESNET18_NUMEL = 11_173_962    # examples/pytorch-cifar/models/resnet.py ResNet18
+REF_SAMPLE_MAX = 32_000_000    # cap on the reference-round CPU sample (elements)
+# BASELINE.json north_star sizes, each in its config's dtype (configs[1..4])
+SWEEP = ((RESNET18_NUMEL, "f32"), (100_000_000, "f32"), (1_000_000_000, "bf16"), (7_000_000_000, "bf16"))
 
 
 def parse():
@@ -47,9 +52,12 @@ def parse():
     ap.add_argument("--numel", type=int, default=RESNET18_NUMEL)
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32")
     ap.add_argument("--interpolation", choices=["constant", "clock", "loss"], default="constant")
+    ap.add_argument("--fetch-probability", type=float, default=1.0)
+    ap.add_argument("--divergence-threshold", type=float, default=0.0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the cold kernel sweep over the north_star sizes")
     ap.add_argument("--no-write-through", action="store_true", help="skip the write-through variant")
     ap.add_argument("--sample-every", type=int, default=8,
                     help="time the averaging kernel every k-th step (a timed launch costs a few µs)")
@@ -70,19 +78,29 @@ def parse():
     return ap.parse_args()
 
 
-def write_config(path, names, interp):
+def write_config(path, names, interp, fetch_probability=1.0, divergence_threshold=0.0):
+    """The reference's YAML node config (dpwa/conn.py:246-262, dpwa/dpwa.py:60-90)."""
     lines = ["- nodes:"] + ["  - {name: %s, host: 127.0.0.1, port: %d}" % (n, 45000 + i)
                             for i, n in enumerate(names)]
-    lines += ["- fetch_probability: 1", "- timeout_ms: 2500", "- interpolation: %s" % interp,
-              "- divergence_threshold: 0", "- constant: { value: 0.5 }", "- clock: 0", "- loss: 0"]
+    lines += ["- fetch_probability: %r" % fetch_probability, "- timeout_ms: 2500",
+              "- interpolation: %s" % interp, "- divergence_threshold: %r" % divergence_threshold,
+              "- constant: { value: 0.5 }", "- clock: 0", "- loss: 0"]
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
 
 
 def cpu_baseline(numel, seconds):
-    """The C oracle (oracle/dpwa_oracle.c) running the same round on one host core:
-    publish copy (2*N*4 bytes) + averaging (3*N*4 bytes); reported like `value`."""
+    """The reference's CPU round (update_send -> TCP fetch -> update_wait; oracle/ref_round.py,
+    which cites dpwa/adapters/pytorch.py, dpwa/conn.py and dpwa/messaging.py line by line)
+    between two learner processes on this host, timed for ~`seconds`; reported like `value`
+    (3*numel*4 averaged bytes per completed averaging).  Beside it, the C oracle running the
+    same round's arithmetic on one host core (publish copy + averaging)."""
     from oracle import lerp as olerp
+    from oracle import ref_round
+    # one reference round at 100M fp32 already takes ~9 s here: larger vectors are sampled
+    out = ref_round.run(min(numel, REF_SAMPLE_MAX), seconds)
+    if numel > REF_SAMPLE_MAX:
+        out["sample"] += " (bounded sample of a %d-element workload)" % numel
     lib = olerp.clib()
     rng = np.random.default_rng(0)
     param = rng.standard_normal(numel).astype(np.float32)
@@ -95,24 +113,25 @@ def cpu_baseline(numel, seconds):
         lib.dpwa_oracle_lerp_f32(param.ctypes.data, peer.ctypes.data, numel, 0.5)
         rounds += 1
         el = time.perf_counter() - t0
-        if el >= seconds:
+        if el >= seconds / 2:
             break
-    return {"value": rounds * 3 * numel * 4 / el / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": "%d rounds of publish-copy + fp32 lerp over %d elements (C oracle, -O3, 1 thread, %.1f s)"
-                      % (rounds, numel, el),
-            "ms_per_round": 1e3 * el / rounds}
+    out["c_oracle_round"] = {
+        "value": rounds * 3 * numel * 4 / el / 1e9, "unit": "GB/s", "cores": 1,
+        "sample": "%d rounds of publish-copy + fp32 lerp over %d elements (oracle/dpwa_oracle.c, -O3, 1 thread, "
+                  "%.1f s): the arithmetic alone, no transport" % (rounds, numel, el),
+        "ms_per_round": 1e3 * el / rounds}
+    return out
 
 
 def cold_kernel(numel, dtype, device, launches=64):
     """The fused average kernel alone over rotating buffers (> 1 GiB between reuses, so no
     Infinity-Cache hits), launched back to back; one event pair around the whole batch."""
     from dpwa_amd import _lib
-    from dpwa_amd.interpolation import ConstantInterpolation
-    from dpwa_amd.learner import Learner
     esize = 4 if dtype == torch.float32 else 2
-    pairs = max(4, int(np.ceil(1.2e9 / (2 * numel * esize))))
-    bufs = [(torch.randn(numel, device=device).to(dtype), torch.randn(numel, device=device).to(dtype))
-            for _ in range(pairs)]
+    pairs = max(2, int(np.ceil(1.2e9 / (2 * numel * esize))))
+    launches = max(2 * pairs, min(launches, int(np.ceil(64 * 134e6 / (3 * numel * esize)))))
+    bufs = [(torch.empty(numel, device=device, dtype=dtype).normal_(),
+             torch.empty(numel, device=device, dtype=dtype).normal_()) for _ in range(pairs)]
     fn = "dpwa_lerp_f32_host" if dtype == torch.float32 else "dpwa_lerp_bf16_host"
     s = _lib.stream_handle(None)
     f = getattr(_lib.load(), fn)
@@ -136,6 +155,16 @@ def cold_kernel(numel, dtype, device, launches=64):
     return 3 * numel * esize / (us * 1e-6) / 1e9, us, pairs
 
 
+def size_sweep(device):
+    """The averaging kernel, cold, at every north_star size (11.17M/100M fp32, 1B/7B bf16)."""
+    rows = []
+    for numel, dt in SWEEP:
+        gbs, us, pairs = cold_kernel(numel, torch.float32 if dt == "f32" else torch.bfloat16, device)
+        rows.append({"numel": numel, "dtype": dt, "avg_launch_us": round(us, 2), "achieved": round(gbs, 1),
+                     "frac": round(gbs / HBM_PEAK_GBS, 4), "rotating_buffer_pairs": pairs})
+    return rows
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -143,6 +172,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d (launch N>1 with torch.distributed.run)" % (args.gpus, world))
+    # the CPU baseline first, before anything touches the GPU (its learners are child processes)
+    cpu = cpu_baseline(args.numel, args.cpu_seconds) if world == 1 and not args.no_cpu_baseline else None
     # one GPU per rank; the modulo only matters for rehearsals with more ranks than GPUs
     device = torch.device("cuda", local_rank % torch.cuda.device_count())
     torch.cuda.set_device(device)
@@ -161,12 +192,12 @@ def main():
     cfg = os.path.join(tmp, "bench.yaml")
     if world == 1:
         names = ["w1", "w2"]
-        write_config(cfg, names, args.interpolation)
+        write_config(cfg, names, args.interpolation, args.fetch_probability, args.divergence_threshold)
         group = LocalGroup()
         mine = [(names[0], 0), (names[1], 1)]
     else:
         names = ["w%d" % (r + 1) for r in range(world)]
-        write_config(cfg, names, args.interpolation)
+        write_config(cfg, names, args.interpolation, args.fetch_probability, args.divergence_threshold)
         group = None
         mine = [(names[rank], rank)]
     learners = []
@@ -383,9 +414,11 @@ def main():
             "dtype": "f32" if dtype == torch.float32 else "bf16",
             "data": "synthetic N(0,1) flat parameter vectors (no dataset needed)",
             "config": {
-                "workload": ("configs[1]: synthetic %d-element %s vector per learner (ResNet-18 size), "
-                             "%s interpolation, fetch_probability 1, lock-step gossip rounds"
-                             % (args.numel, args.dtype, args.interpolation)),
+                "workload": ("%ssynthetic %d-element %s vector per learner%s, %s interpolation, "
+                             "fetch_probability %g, divergence_threshold %g, lock-step gossip rounds"
+                             % ("configs[1]: " if args.numel == RESNET18_NUMEL else "", args.numel, args.dtype,
+                                " (ResNet-18 size)" if args.numel == RESNET18_NUMEL else "", args.interpolation,
+                                args.fetch_probability, args.divergence_threshold)),
                 "learners": int(rounds / args.steps),
                 "learners_per_gpu": len(learners),
                 "numel": args.numel,
@@ -438,10 +471,9 @@ def main():
             gbs, us, pairs = cold_kernel(args.numel, dtype, device)
             out["roofline"]["cold_cache"] = {"achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                                              "avg_launch_us": round(us, 2), "rotating_buffer_pairs": pairs}
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.numel, args.cpu_seconds)
-        else:
-            out["cpu_baseline"] = None
+        if world == 1 and not args.no_sweep:
+            out["roofline"]["size_sweep"] = size_sweep(device)
+        out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     for conn, _ in learners:
         conn.close()

@@ -169,6 +169,28 @@ __global__ __launch_bounds__(BLOCK) void k_buf(float *__restrict__ param, const 
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, r), rp, off, 0, AUXS);
 }
 
+// U items per lane, each block one contiguous BLOCK*16*U-byte span; all 2U loads issued
+// before the first store (fewer, fatter workgroups than k_buf).
+template <int BLOCK, int U, int AUXL, int AUXS>
+__global__ __launch_bounds__(BLOCK) void k_bufu(float *__restrict__ param, const float *__restrict__ peer, int64_t n4,
+                                                float a, float b)
+{
+    const int nbytes = (int)(n4 * 16);
+    __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(param, 0, nbytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)peer, 0, nbytes, 0x00020000);
+    const int base = (int)((int64_t)blockIdx.x * BLOCK * U * 16) + threadIdx.x * 16;
+    u32x4v q[U], p[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) q[u] = __builtin_amdgcn_raw_buffer_load_b128(rq, base + u * BLOCK * 16, 0, AUXL);
+#pragma unroll
+    for (int u = 0; u < U; ++u) p[u] = __builtin_amdgcn_raw_buffer_load_b128(rp, base + u * BLOCK * 16, 0, AUXL);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const f32x4 r = lerp4(a, b, __builtin_bit_cast(f32x4, q[u]), __builtin_bit_cast(f32x4, p[u]));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, r), rp, base + u * BLOCK * 16, 0, AUXS);
+    }
+}
+
 // Two items per lane, block-contiguous (512 items per 256-thread block): all four loads are
 // issued before the first store.
 template <int BLOCK>
@@ -302,6 +324,16 @@ Variant buf(const char *name)
             }};
 }
 
+template <int BLOCK, int U, int AL, int AS>
+Variant bufu(const char *name)
+{
+    return {name, 3.0, [](float *p, float *q, int64_t n, hipStream_t s) {
+                int64_t n4 = n / 4;
+                hipLaunchKernelGGL((k_bufu<BLOCK, U, AL, AS>), dim3(grid_for(n4, BLOCK * U, 0)), dim3(BLOCK), 0, s, p,
+                                   q, n4, 0.5f, 0.5f);
+            }};
+}
+
 template <int BLOCK>
 Variant two(const char *name)
 {
@@ -350,18 +382,17 @@ int main(int argc, char **argv)
     std::vector<Variant> vs = {
         one<256, false, false>("one256 (r01a product)"),
         buf<256, 2, 2, 16>("buf256 nt loads sc1 store (product)"),
-        buf<256, 2, 2, 17>("buf256 nt loads sc0sc1 store"),
-        buf<256, 2, 0, 17>("buf256 nt peer sc0sc1 store"),
+        buf<256, 2, 2, 2>("buf256 nt loads nt store"),
+        buf<256, 2, 2, 0>("buf256 nt loads plain store"),
         buf<64, 2, 2, 16>("buf64 nt loads sc1 store"),
-        buf<64, 2, 2, 17>("buf64 nt loads sc0sc1 store"),
-        buf<64, 2, 0, 16>("buf64 nt peer sc1 store"),
-        buf<64, 2, 0, 17>("buf64 nt peer sc0sc1 store"),
-        buf<128, 2, 2, 17>("buf128 nt loads sc0sc1 store"),
-        buf<128, 2, 2, 16>("buf128 nt loads sc1 store"),
+        buf<512, 2, 2, 16>("buf512 nt loads sc1 store"),
+        bufu<256, 2, 2, 16>("bufu256x2 nt loads sc1 store"),
+        bufu<256, 4, 2, 16>("bufu256x4 nt loads sc1 store"),
+        bufu<128, 2, 2, 16>("bufu128x2 nt loads sc1 store"),
+        bufu<64, 4, 2, 16>("bufu64x4 nt loads sc1 store"),
+        bufu<512, 2, 2, 16>("bufu512x2 nt loads sc1 store"),
         copybuf<256, 2, 16>("copybuf256 nt load sc1 store (x2 bytes)"),
-        copybuf<256, 2, 17>("copybuf256 nt load sc0sc1 store (x2 bytes)"),
         copybuf<64, 2, 16>("copybuf64 nt load sc1 store (x2 bytes)"),
-        copybuf<64, 2, 17>("copybuf64 nt load sc0sc1 store (x2 bytes)"),
         {"hipMemcpyAsync D2D (x2 bytes)", 2.0,
          [](float *p, float *q, int64_t n, hipStream_t s) { (void)hipMemcpyAsync(p, q, n * 4, hipMemcpyDeviceToDevice, s); }},
     };
