@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--interpolation", choices=["constant", "clock", "loss"], default="constant")
     ap.add_argument("--fetch-probability", type=float, default=1.0)
     ap.add_argument("--divergence-threshold", type=float, default=0.0)
+    ap.add_argument("--loss-schedule", choices=["constant", "decay"], default="constant",
+                    help="reported loss: 1.0, or SURVEY §8d C4's 2exp(-t/200)+0.05U (crosses a threshold)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
@@ -212,7 +214,15 @@ def main():
     # co-resident learners on their own streams (their kernels overlap) or all on one
     streams = ([torch.cuda.Stream(device) for _ in learners] if args.streams == "per-learner"
                else [stream for _ in learners])
-    loss = 1.0
+    # per-learner loss stream: constant 1.0, or SURVEY §8d C4's synthetic decay
+    # l_t = 2 exp(-t/200) + 0.05 U(0,1) (seeded per learner) so a divergence threshold is crossed
+    loss_rngs = [np.random.default_rng(7 + seed) for _, seed in mine]
+    loss_t = [0]
+
+    def loss_of(i):
+        if args.loss_schedule == "constant":
+            return 1.0
+        return 2.0 * float(np.exp(-loss_t[0] / 200.0)) + 0.05 * float(loss_rngs[i].random())
     from dpwa_amd import _lib
 
     def run(steps, warmup, write_through, sample_every):
@@ -227,9 +237,11 @@ def main():
 
         def step(k, timed):
             done = 0
+            losses = [loss_of(i) for i in range(len(learners))]
+            loss_t[0] += 1
             for i, (conn, flat) in enumerate(learners):
                 with torch.cuda.stream(streams[i]):
-                    conn.update_send(flat, loss, reuse_snapshot=write_through)
+                    conn.update_send(flat, losses[i], reuse_snapshot=write_through)
             sample = timed and k % sample_every == 0
             for i, (conn, flat) in enumerate(learners):
                 st = streams[i]
@@ -243,7 +255,7 @@ def main():
                             a.record(st)
                         if args.timing != "bracket" and conn in timed_learners:
                             lib.dpwa_learner_arm_timing(conn._learner.handle)
-                    payload, _ = conn.update_wait_average(flat, loss, write_through=write_through)
+                    payload, _ = conn.update_wait_average(flat, losses[i], write_through=write_through)
                     if sample and args.timing != "dispatch":
                         b.record(st)
                         if payload is not None:
@@ -322,14 +334,16 @@ def main():
         """Training-loop shape (main.py:122-158): update_send, the step, update_wait."""
         def step():
             done = 0
+            losses = [loss_of(i) for i in range(len(learners))]
+            loss_t[0] += 1
             if gossip:
-                for conn, flat in learners:
-                    conn.update_send(flat, loss)
+                for i, (conn, flat) in enumerate(learners):
+                    conn.update_send(flat, losses[i])
             for _ in learners:
                 compute()
             if gossip:
-                for conn, flat in learners:
-                    payload, _ = conn.update_wait_average(flat, loss)
+                for i, (conn, flat) in enumerate(learners):
+                    payload, _ = conn.update_wait_average(flat, losses[i])
                     done += payload is not None
             return done
 
@@ -415,10 +429,10 @@ def main():
             "data": "synthetic N(0,1) flat parameter vectors (no dataset needed)",
             "config": {
                 "workload": ("%ssynthetic %d-element %s vector per learner%s, %s interpolation, "
-                             "fetch_probability %g, divergence_threshold %g, lock-step gossip rounds"
+                             "fetch_probability %g, divergence_threshold %g, %s loss, lock-step gossip rounds"
                              % ("configs[1]: " if args.numel == RESNET18_NUMEL else "", args.numel, args.dtype,
                                 " (ResNet-18 size)" if args.numel == RESNET18_NUMEL else "", args.interpolation,
-                                args.fetch_probability, args.divergence_threshold)),
+                                args.fetch_probability, args.divergence_threshold, args.loss_schedule)),
                 "learners": int(rounds / args.steps),
                 "learners_per_gpu": len(learners),
                 "numel": args.numel,

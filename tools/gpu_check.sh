@@ -13,10 +13,10 @@ cat gpurun_out/bench.json
 # the other north_star configs, full gossip rounds on one GPU (two co-resident learners)
 V="--no-cpu-baseline --no-sweep --no-cold --compute-us 0 --steps 50 --warmup 10"
 timeout -k 10 200 python bench.py $V --numel 100000000 --interpolation clock > gpurun_out/bench_100m_clock.json 2>> gpurun_out/bench.err &&
-timeout -k 10 200 python bench.py $V --numel 1000000000 --dtype bf16 --interpolation loss --divergence-threshold 0.5 \
+timeout -k 10 200 python bench.py $V --numel 1000000000 --dtype bf16 --interpolation loss --divergence-threshold 0.5 --loss-schedule decay \
     > gpurun_out/bench_1b_bf16_loss.json 2>> gpurun_out/bench.err &&
-timeout -k 10 300 python bench.py $V --numel 7000000000 --dtype bf16 --fetch-probability 0.5 \
-    > gpurun_out/bench_7b_bf16_p05.json 2>> gpurun_out/bench.err || { echo "variant bench failed"; tail gpurun_out/bench.err; exit 1; }
+timeout -k 10 300 python bench.py $V --numel 7000000000 --dtype bf16 --fetch-probability 0.7 \
+    > gpurun_out/bench_7b_bf16_p07.json 2>> gpurun_out/bench.err || { echo "variant bench failed"; tail gpurun_out/bench.err; exit 1; }
 if [ -x tools/lerp_tune ]; then
     timeout -k 10 120 ./tools/lerp_tune 11173962 10 > gpurun_out/tune_cold.log 2>&1 || exit 1
     timeout -k 10 120 ./tools/lerp_tune 11173962 10 1 > gpurun_out/tune_warm.log 2>&1 || exit 1

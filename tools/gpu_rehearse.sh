@@ -1,0 +1,18 @@
+#!/bin/bash
+# The driver's N>1 bench path rehearsed on one GPU (gloo: RCCL refuses two ranks per GPU),
+# plus the C4/C5 config variants.  Usage: gpurun --timeout 900 -- bash tools/gpu_rehearse.sh
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for n in 2 4; do
+  timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+      --master-port $((29500 + n)) bench.py --gpus $n --dist-backend gloo --steps 40 --warmup 5 --compute-us 300 \
+      > gpurun_out/rehearse_n$n.json 2> gpurun_out/rehearse_n$n.err || { echo "rehearsal n=$n failed"; tail -20 gpurun_out/rehearse_n$n.err; exit 1; }
+  cat gpurun_out/rehearse_n$n.json
+done
+V="--no-cpu-baseline --no-sweep --no-cold --compute-us 0 --steps 50 --warmup 10"
+timeout -k 10 200 python bench.py $V --numel 1000000000 --dtype bf16 --interpolation loss --divergence-threshold 0.5 \
+    --loss-schedule decay > gpurun_out/bench_1b_bf16_loss_decay.json 2> gpurun_out/variants.err &&
+timeout -k 10 300 python bench.py $V --numel 7000000000 --dtype bf16 --fetch-probability 0.7 \
+    > gpurun_out/bench_7b_bf16_p07.json 2>> gpurun_out/variants.err || { echo "variant failed"; tail gpurun_out/variants.err; exit 1; }
+echo done
