@@ -397,6 +397,7 @@ def main():
             "ms_per_step": round(1e3 * t_both / o_steps, 4),
             "gossip_overhead_frac": round(t_both / t_compute - 1.0, 4),
             "rounds_per_s_per_learner": round(o_steps / t_both, 1),
+            "gossip_rounds_per_s": round(o_steps * len(learners) * world / t_both, 1),   # all learners, all ranks
             "note": "update_send -> synthetic training step -> update_wait_average (SURVEY §8d C4 "
                     "weak scaling): the overhead the gossip round adds to a step of this length",
         }

@@ -119,6 +119,17 @@ SIGNATURES = {
     "dpwa_node_handles": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp)],
     "dpwa_node_set_peer": [_vp, _int, _int, _vp],
     "dpwa_node_set_fault": [_vp, _int, _int],
+    "dpwa_node_set_board": [_vp, _vp, ctypes.POINTER(_i32), _int],
+    "dpwa_board_open": [ctypes.POINTER(_vp), ctypes.c_char_p, _int, _int, _int],
+    "dpwa_board_unlink": [ctypes.c_char_p],
+    "dpwa_board_close": [_vp],
+    "dpwa_board_register": [_vp, _int],
+    "dpwa_board_status": [_vp, _int, ctypes.POINTER(_i32)],
+    "dpwa_board_read": [_vp, _int, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_i32)],
+    "dpwa_board_acquire": [_vp, _int, ctypes.POINTER(_u64)],
+    "dpwa_board_release": [_vp, _int, _vp, _int],
+    "dpwa_board_publish_wait": [_vp, _u64, _int],
+    "dpwa_board_advertise": [_vp, _u64, _vp, _int],
     "dpwa_node_update_send": [_vp, _vp, _dbl, _vp, _int, _vp, _pint],
     "dpwa_node_publish": [_vp, _vp, _dbl, _vp, _int, _vp],
     "dpwa_node_gate": [_vp, _int, _vp, _pint],

@@ -48,13 +48,6 @@ int set_error(int code, const char *fmt, ...)
 
 using namespace dpwa;
 
-#define HIP_TRY(expr)                                                                                  \
-    do {                                                                                               \
-        hipError_t e_ = (expr);                                                                        \
-        if (e_ != hipSuccess)                                                                          \
-            return set_error(DPWA_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(e_)); \
-    } while (0)
-
 namespace {
 
 constexpr size_t kHeader = sizeof(dpwa_header);

@@ -40,6 +40,10 @@ struct dpwa_node {
     uint64_t fetch_version = 0;
     int last_attempts = 0;
     bool awaiting_lerp = false;    // update_wait (split) done, lerp not yet issued
+    // free-running rounds (board.cpp): REMOTE peers are read through the board
+    dpwa_board *board = nullptr;
+    std::vector<int32_t> board_rank;
+    int publish_timeout_ms = -1;
 };
 
 using namespace dpwa;
@@ -111,6 +115,16 @@ int dpwa_node_set_peer(dpwa_node *n, int peer, int kind, dpwa_node *local)
     return DPWA_OK;
 }
 
+int dpwa_node_set_board(dpwa_node *n, dpwa_board *board, const int32_t *peer_ranks, int publish_timeout_ms)
+{
+    if (!n || (board && !peer_ranks)) return set_error(DPWA_ERR_ARG, "dpwa_node_set_board: bad arguments");
+    n->board = board;
+    n->board_rank.assign(peer_ranks && board ? peer_ranks : (const int32_t *)nullptr,
+                         peer_ranks && board ? peer_ranks + n->peers.size() : (const int32_t *)nullptr);
+    n->publish_timeout_ms = publish_timeout_ms;
+    return DPWA_OK;
+}
+
 int dpwa_node_set_fault(dpwa_node *n, int peer, int status)
 {
     if (!n || peer < 0 || (size_t)peer >= n->peers.size() || status < -1 || status > DPWA_PEER_DEAD)
@@ -124,6 +138,10 @@ static int32_t peer_status(const dpwa_node *n, size_t k)
 {
     const PeerRef &p = n->peers[k];
     if (p.fault >= 0) return p.fault;
+    if (p.kind == PEER_REMOTE && n->board) {             // free-running: what the board says
+        int32_t st = DPWA_PEER_DOWN;
+        return dpwa_board_status(n->board, n->board_rank[k], &st) == DPWA_OK ? st : DPWA_PEER_DOWN;
+    }
     if (p.kind == PEER_REMOTE) return DPWA_PEER_READY;   // lock-step: published this round
     if (p.kind != PEER_LOCAL) return DPWA_PEER_DOWN;     // not listening: ConnectionRefused
     if (!p.node->learner || learner_version(p.node->learner) == 0) return DPWA_PEER_NO_STATE;
@@ -150,6 +168,24 @@ static int start_fetch(dpwa_node *n, int flags, dpwa_stream_t stream)
             n->attached_to[peer] = pl;
         }
         version = learner_version(pl);
+    } else if (n->board) {
+        // free-running: the newest complete publish, held against rewrite until our pull lands
+        if (flags & DPWA_FLAG_PICK_ONLY)
+            return set_error(DPWA_ERR_STATE, "the relay transport needs lock-step rounds, not a board");
+        const int r = n->board_rank[peer];
+        if ((rc = dpwa_board_acquire(n->board, r, &version))) return rc;
+        if (version == 0) return DPWA_OK;   // closed between the pick and now: no data
+        if ((rc = dpwa_learner_fetch(n->learner, peer, version, 0, stream))) {
+            dpwa_board_release(n->board, r, nullptr, 1);
+            return rc;
+        }
+        dpwa_stream_t side = nullptr;
+        if ((rc = dpwa_learner_side_stream(n->learner, &side)) ||
+            (rc = dpwa_board_release(n->board, r, side, 0)))
+            return rc;
+        n->fetch_peer = peer;
+        n->fetch_version = version;
+        return DPWA_OK;
     } else {
         version = learner_version(n->learner);   // lock-step: every node publishes once per round
         zero_copy = 0;
@@ -175,6 +211,15 @@ int dpwa_node_publish(dpwa_node *n, const void *flat, double loss, const double 
     }
     n->fetch_started = false;
     n->fetch_peer = -1;
+    if (n->board) {   // free-running: wait out readers of the slot we rewrite, then announce
+        if (flags & DPWA_FLAG_REUSE_SNAPSHOT)
+            return set_error(DPWA_ERR_STATE, "write-through snapshots need lock-step rounds, not a board");
+        const uint64_t next = learner_version(n->learner) + 1;
+        int rc = dpwa_board_publish_wait(n->board, next, n->publish_timeout_ms);
+        if (!rc) rc = dpwa_learner_publish(n->learner, flat, loss, loss_dev, stream);
+        if (!rc) rc = dpwa_board_advertise(n->board, next, stream, 0);
+        return rc;
+    }
     if (flags & DPWA_FLAG_REUSE_SNAPSHOT) return dpwa_learner_publish_reuse(n->learner, flat, loss, loss_dev, stream);
     return dpwa_learner_publish(n->learner, flat, loss, loss_dev, stream);
 }
@@ -238,7 +283,10 @@ int dpwa_node_update_wait_average(dpwa_node *n, void *flat, double loss, const d
     if (!n || !n->learner || !peer) return set_error(DPWA_ERR_STATE, "dpwa_node_update_wait_average: node not bound");
     int rc = finish_fetch(n, flags, stream, peer);
     if (rc || *peer < 0) return rc;
-    if (flags & DPWA_FLAG_WRITE_THROUGH) return dpwa_learner_average_through(n->learner, flat, loss, loss_dev, stream);
+    if (flags & DPWA_FLAG_WRITE_THROUGH) {
+        if (n->board) return set_error(DPWA_ERR_STATE, "write-through snapshots need lock-step rounds, not a board");
+        return dpwa_learner_average_through(n->learner, flat, loss, loss_dev, stream);
+    }
     return dpwa_learner_average(n->learner, flat, loss, loss_dev, stream);
 }
 

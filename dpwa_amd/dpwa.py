@@ -171,6 +171,12 @@ class DpwaConnection:
         self._f_wait_avg = lib.dpwa_node_update_wait_average
         self._f_lerp = lib.dpwa_node_lerp
         self._raw_stream = torch._C._cuda_getCurrentRawStream
+        if group == "async":    # free-running rounds between ranks (gossip board), see group.py
+            from .group import AsyncDistGroup
+            group = AsyncDistGroup(self.nodes, name)
+        elif group == "lockstep":
+            from .group import DistGroup
+            group = DistGroup(self.nodes, name)
         self._group = group if group is not None else default_group(config_file, self.nodes, name)
         self._eager = bool(self._group.eager_fetch)
         self._flags = (_lib.FLAG_EAGER if self._group.eager_fetch else 0) | \

@@ -197,6 +197,58 @@ class DistGroup:
                   self.relay_blocks)
 
 
+class AsyncDistGroup(DistGroup):
+    """Free-running rounds between the ranks of one node: no barrier, no collective per
+    round.  Peers' snapshots are read through a gossip board (dpwa_amd/csrc/board.cpp): a
+    shared-memory block holding every rank's newest complete publish and who is reading
+    which version, so a publish waits only for readers of the snapshot it would rewrite --
+    the reference's RxThread Lock (conn.py:76-79, 109-110) -- and a rank that has closed or
+    died answers as a refused connection (conn.py:253-256).  The copy and kernel pulls are
+    supported; the relay and write-through snapshots need lock-step rounds."""
+
+    def __init__(self, nodes, name, process_group=None, publish_timeout_ms=None):
+        super().__init__(nodes, name, process_group)
+        self.board = None
+        # a publish waits for a slow reader at most this long (the reference blocks forever)
+        self.publish_timeout_ms = int(publish_timeout_ms if publish_timeout_ms is not None else 600_000)
+
+    def on_bind(self, conn):
+        if getattr(conn, "_pull", "copy").partition(":")[0] == "relay" or self.relay_blocks:
+            raise ValueError("the relay pull needs lock-step rounds (DistGroup), not free-running ones")
+        board = ctypes.c_void_p()
+        bname = None
+        if self.rank == 0:
+            bname = "/dpwa_board_%d_%s" % (os.getpid(), os.urandom(4).hex())
+            _lib.call("dpwa_board_open", ctypes.byref(board), bname.encode(), self.world, 0, 1)
+        names = [None] * self.world
+        self.dist.all_gather_object(names, bname, group=self.pg)     # rank 0 created it
+        bname = names[0]
+        if self.rank != 0:
+            _lib.call("dpwa_board_open", ctypes.byref(board), bname.encode(), self.world, self.rank, 0)
+        self.board = board
+        _lib.call("dpwa_board_register", board, conn._learner.device.index)
+        super().on_bind(conn)                 # IPC exchange; a collective, so every rank has opened
+        if self.rank == 0:
+            _lib.call("dpwa_board_unlink", bname.encode())   # nothing left in /dev/shm after a crash
+        ranks = (ctypes.c_int32 * max(1, len(conn.peers)))(*[conn.peer_rank(k) for k in range(len(conn.peers))])
+        _lib.call("dpwa_node_set_board", conn._node, board, ranks, self.publish_timeout_ms)
+
+    def after_publish(self, conn):
+        pass
+
+    def after_gate(self, conn):
+        pass
+
+    def leave(self, conn):
+        board, self.board = self.board, None
+        if board is not None and board.value:
+            if conn._node is not None and conn._node.value:
+                _lib.call("dpwa_node_set_board", conn._node, None, None, -1)
+            if conn._learner is not None:
+                torch.cuda.synchronize(conn._learner.device)   # our pulls are done with every peer
+            _lib.call("dpwa_board_close", board)
+
+
 def default_group(config_file, nodes, name):
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() == len(nodes) > 1:

@@ -319,6 +319,12 @@ int dpwa_node_handles(dpwa_node *n, dpwa_learner **learner, dpwa_sched **sched);
 int dpwa_node_set_peer(dpwa_node *n, int peer, int kind, dpwa_node *local);
 /* Fault injection: force a DPWA_PEER_* status for a peer, -1 clears. */
 int dpwa_node_set_fault(dpwa_node *n, int peer, int status);
+/* Free-running rounds (extension of DPWA_NODE_PEER_REMOTE): the node's REMOTE peers are
+ * read through `board` (see below) instead of lock-step.  peer_ranks[k] = board rank of
+ * scheduler peer k; publish_timeout_ms bounds a publish's wait for readers (-1 forever).
+ * board NULL returns the node to lock-step.  The node does not own the board. */
+typedef struct dpwa_board dpwa_board;
+int dpwa_node_set_board(dpwa_node *n, dpwa_board *board, const int32_t *peer_ranks, int publish_timeout_ms);
 
 /* update_send (dpwa.py:104-123): publish, then the Bernoulli gate; with DPWA_FLAG_EAGER a
  * granted fetch starts now (peer choice + pull on the side stream), else at update_wait.
@@ -340,6 +346,35 @@ int dpwa_node_update_wait_average(dpwa_node *n, void *flat, double loss, const d
  * number, and the picks the last fetch took. */
 int dpwa_node_info(const dpwa_node *n, int *fetching, int *fetch_peer, uint64_t *fetch_version,
                    int *last_attempts);
+
+/* ------------------------------------------------------------------------------------
+ * Gossip board: free-running rounds across the processes of one node (extension).
+ * Replaces the reference's always-on RxThread server (conn.py:51-172) and its publish Lock
+ * (conn.py:76-79, 109-110) with a POSIX shared-memory block: the newest complete publish
+ * of every rank (written by its stream after the publish), per (publisher, reader) the
+ * version being pulled, and liveness (a closed entry or a dead pid is a refused
+ * connection, conn.py:253-256).  No collective runs per round.
+ * ------------------------------------------------------------------------------------ */
+/* name: "/..." (shm_open); create != 0 on exactly one rank, before the others open. */
+int dpwa_board_open(dpwa_board **out, const char *name, int world, int rank, int create);
+int dpwa_board_unlink(const char *name);
+/* marks this rank closed (peers see a refused connection) and unmaps */
+int dpwa_board_close(dpwa_board *b);
+/* hipHostRegister the block for stream writes from `device` (needed before a device
+ * advertise/release) */
+int dpwa_board_register(dpwa_board *b, int device);
+/* DPWA_PEER_DOWN / NO_STATE / READY for rank r */
+int dpwa_board_status(dpwa_board *b, int r, int32_t *status);
+/* raw view of rank r: its newest complete publish, our read mark on it, liveness */
+int dpwa_board_read(dpwa_board *b, int r, uint64_t *version, uint64_t *reading_by_me, int32_t *alive);
+/* reader: a version of r that r will not overwrite until released (0 = never published) */
+int dpwa_board_acquire(dpwa_board *b, int r, uint64_t *version);
+/* reader: clear the read mark on r after the work on `stream` (host != 0: now) */
+int dpwa_board_release(dpwa_board *b, int r, dpwa_stream_t stream, int host);
+/* publisher: wait until publish `next` may rewrite its slot (timeout_ms < 0: forever) */
+int dpwa_board_publish_wait(dpwa_board *b, uint64_t next, int timeout_ms);
+/* publisher: announce publish `version` after the work on `stream` (host != 0: now) */
+int dpwa_board_advertise(dpwa_board *b, uint64_t version, dpwa_stream_t stream, int host);
 
 #ifdef __cplusplus
 }

@@ -109,3 +109,59 @@ def fault_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy"):
     dist.barrier()
     conn.close()
     dist.destroy_process_group()
+
+
+def async_base(rank, r, n):
+    """The parameters rank `rank` publishes at its round r (publish number r + 1)."""
+    return (np.arange(n, dtype=np.float32) * np.float32(1e-3) + np.float32(rank * 1000 + r)).astype(np.float32)
+
+
+def async_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy", die_rank=-1, die_round=-1):
+    """Free-running gossip (AsyncDistGroup): every round sets the parameters to
+    async_base(rank, r), publishes, sleeps a rank- and round-dependent time on the GPU and
+    averages with whatever version of a peer the board hands out.  Records the peer, the
+    version it read, the result and the clock; the test recomputes them from the bases."""
+    import time
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from dpwa_amd import DpwaConnection
+    from dpwa_amd.group import AsyncDistGroup
+    names = ["r%d" % i for i in range(world)]
+    conn = DpwaConnection(names[rank], cfg_path, seed=700 + rank, group="async", pull=pull)
+    assert isinstance(conn._group, AsyncDistGroup)
+    rng = np.random.default_rng(rank)
+    flat = torch.empty(n, device=dev, dtype=torch.float32)
+    bases = [torch.from_numpy(async_base(rank, r, n)).to(dev) for r in range(T)]
+    params, clocks, peers, versions, scores = np.zeros((T, n), np.float32), np.zeros(T), [], [], []
+    for r in range(T):
+        if rank == die_rank and r == die_round:
+            torch.cuda.synchronize()
+            conn._group.leave(conn)    # leaves mid-run (the board entry closes, its readers drain)
+            os._exit(0)                # ... and dies: no close(), no barrier
+        flat.copy_(bases[r])
+        conn.update_send(flat, 1.0)
+        torch.cuda._sleep(int(rng.integers(0, 400_000)))     # uneven "training steps"
+        payload, _ = conn.update_wait_average(flat, 1.0)
+        peers.append(payload.peer if payload is not None else "")
+        versions.append(conn._info()[2] if payload is not None else 0)
+        params[r] = flat.cpu().numpy()
+        clocks[r] = conn.clock
+        scores.append([conn.flow_control_scores()[p] for p in names if p != names[rank]])
+        if rank == 0 and r % 7 == 0:
+            time.sleep(0.002)      # host-side jitter too
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=params, clocks=clocks, peers=np.array(peers),
+             versions=np.array(versions, dtype=np.int64),
+             scores=np.array([[-1 if s is None else s for s in row] for row in scores]))
+    # no collective at the end either: a dead rank would never join it
+    open(os.path.join(out_dir, "done%d" % rank), "w").close()
+    while sum(os.path.exists(os.path.join(out_dir, "done%d" % q)) for q in range(world) if q != die_rank) < \
+            world - (1 if die_rank >= 0 else 0):
+        time.sleep(0.01)
+    conn.close()
+    os._exit(0)                    # skip the process-group teardown (the dead rank never joins it)
