@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--pull", default="auto",
                     help="N>1 fetch transport: copy (hipMemcpyAsync), kernel[:blocks], relay[:blocks] "
                          "(two-phase multi-link), or auto (fastest of a short trial)")
+    ap.add_argument("--gossip", default="auto", choices=["auto", "lockstep", "async"],
+                    help="N>1: lock-step rounds (DistGroup), free-running rounds (AsyncDistGroup, gossip "
+                         "board), or a short trial of both keeping the faster")
     ap.add_argument("--compute-us", type=float, default=1000.0,
                     help="per-learner synthetic training step (bf16 GEMM loop) for the 'overlap' field; 0 = skip")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
@@ -372,18 +375,44 @@ def main():
 
     pull_trials = {}
     pull = args.pull
+    lockstep_learners = list(learners)
+    async_learners = []
     if world > 1:
         run(2, 2, False, 1000)   # binds the learners (IPC exchange) before the transport is chosen
         modes = [args.pull] if args.pull != "auto" else ["copy", "kernel:256", "kernel:1024", "relay:32",
                                                          "relay:128"]
-        for mode in modes:       # short timed trial of each transport; the fastest is used below
-            set_pull(mode)
-            el, av, _, _ = run(max(10, args.steps // 10), 2, False, 1000)
-            pull_trials[mode] = round(av * 3 * args.numel * esize / el / 1e9, 2)
+        trial_steps = max(10, args.steps // 10)
+        if args.gossip != "async":
+            for mode in modes:       # short timed trial of each transport; the fastest is used below
+                set_pull(mode)
+                el, av, _, _ = run(trial_steps, 2, False, 1000)
+                pull_trials[mode] = round(av * 3 * args.numel * esize / el / 1e9, 2)
+        if args.gossip != "lockstep":
+            # free-running rounds over the gossip board, same learners' parameters (a second
+            # set of nodes: a connection's group is fixed at construction)
+            for (name, seed), (_, flat) in zip(mine, lockstep_learners):
+                conn = DpwaConnection(name, cfg, seed=1000 + seed, group="async", pull="copy")
+                async_learners.append((conn, flat))
+            learners[:] = async_learners
+            run(2, 2, False, 1000)
+            for mode in [m for m in modes if not m.startswith("relay")]:
+                set_pull(mode)
+                el, av, _, _ = run(trial_steps, 2, False, 1000)
+                pull_trials["async/" + mode] = round(av * 3 * args.numel * esize / el / 1e9, 2)
         pull = max(pull_trials, key=pull_trials.get)
-        set_pull(pull)
+        if pull.startswith("async/"):
+            learners[:] = async_learners
+            set_pull(pull[len("async/"):])
+        else:
+            learners[:] = lockstep_learners
+            set_pull(pull)
     elapsed, averaged, rounds, (lerp_ms, bracket_ms) = run(args.steps, args.warmup, False, args.sample_every)
-    wt = run(args.steps, args.warmup, True, args.sample_every) if not args.no_write_through else None
+    wt = None
+    if not args.no_write_through and (world == 1 or args.gossip != "async"):
+        chosen = list(learners)
+        learners[:] = lockstep_learners     # write-through snapshots need lock-step rounds
+        wt = run(args.steps, args.warmup, True, args.sample_every)
+        learners[:] = chosen
     overlap = None
     if args.compute_us > 0:
         compute, k_gemm, gemm_us = make_compute(args.compute_us)
@@ -438,7 +467,8 @@ def main():
                 "learners_per_gpu": len(learners),
                 "numel": args.numel,
                 "transport": "in-place HBM read (co-resident peer)" if world == 1 else
-                             "hipIpc-mapped slot pulled over xGMI on a side stream (%s)" % pull,
+                             "hipIpc-mapped slot pulled over xGMI on a side stream (%s, %s rounds)"
+                             % (pull.split("/")[-1], "free-running" if pull.startswith("async/") else "lock-step"),
                 "parallelism": "gossip x%d" % int(rounds / args.steps),
                 "streams": args.streams,
             },
@@ -490,7 +520,7 @@ def main():
             out["roofline"]["size_sweep"] = size_sweep(device)
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
-    for conn, _ in learners:
+    for conn, _ in lockstep_learners + async_learners:
         conn.close()
     if world > 1:
         dist.barrier()
