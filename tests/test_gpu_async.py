@@ -26,7 +26,12 @@ def free_port():
     return p
 
 
-def check_run(tmp_path, world, n, T, ranks):
+def factor_of(interp, clock, pclock):
+    """interpolation.py:13-24 (constant 0.5 / clock-weighted)."""
+    return 0.5 if interp == "constant" else pclock / (clock + pclock)
+
+
+def check_run(tmp_path, world, n, T, ranks, interp="constant"):
     names = ["r%d" % i for i in range(world)]
     runs = {g: np.load(tmp_path / ("rank%d.npz" % g)) for g in ranks}
     c_after = {}
@@ -41,7 +46,7 @@ def check_run(tmp_path, world, n, T, ranks):
                 c_after[(g, r)] = c_pub(g, r)
             else:
                 q, v = names.index(str(run["peers"][r])), int(run["versions"][r])
-                factor = 0.5
+                factor = factor_of(interp, c_pub(g, r), c_pub(q, v - 1))
                 c_after[(g, r)] = factor * c_pub(q, v - 1) + (1 - factor) * c_pub(g, r)
         return c_after[(g, r)]
 
@@ -59,7 +64,8 @@ def check_run(tmp_path, world, n, T, ranks):
                 assert 1 <= v, (g, r)
                 assert v >= last.get(q, 0), (g, r, "versions went backwards")
                 last[q] = v
-                want = olerp.lerp_f32(mine, dist_worker.async_base(q, v - 1, n), 0.5)
+                factor = factor_of(interp, c_pub(g, r), c_pub(q, v - 1)) if len(runs) == world else 0.5
+                want = olerp.lerp_f32(mine, dist_worker.async_base(q, v - 1, n), factor)
                 averaged += 1
             assert olerp.bits_equal(run["params"][r], want), (g, r, peer)
             if all(q in runs for q in range(world)):
@@ -67,15 +73,16 @@ def check_run(tmp_path, world, n, T, ranks):
     return runs, averaged
 
 
-@pytest.mark.parametrize("world,pull", [(2, "copy"), (3, "kernel:64")])
-def test_async_gossip_reads_whole_snapshots(tmp_path, world, pull):
+@pytest.mark.parametrize("world,pull,interp", [(2, "copy", "constant"), (3, "kernel:64", "constant"),
+                                               (3, "copy", "clock")])
+def test_async_gossip_reads_whole_snapshots(tmp_path, world, pull, interp):
     n, T = 1_000_003, 40
     names = ["r%d" % i for i in range(world)]
     cfg = str(tmp_path / "async.yaml")
-    dist_worker.write_cfg(cfg, names, 1.0, "constant", 0.0)
+    dist_worker.write_cfg(cfg, names, 1.0, interp, 0.0)
     mp.spawn(dist_worker.async_worker, args=(world, free_port(), cfg, str(tmp_path), n, T, pull), nprocs=world,
              join=True)
-    _, averaged = check_run(tmp_path, world, n, T, range(world))
+    _, averaged = check_run(tmp_path, world, n, T, range(world), interp)
     assert averaged >= world * (T - 3)     # only rounds before a peer's first publish may be empty
 
 
