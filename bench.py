@@ -405,6 +405,11 @@ def main():
             set_pull(pull[len("async/"):])
         else:
             learners[:] = lockstep_learners
+            for conn, _ in async_learners:   # free their streams and slots (fewer HW queues in use)
+                conn.close()
+            async_learners = []
+            torch.cuda.synchronize()
+            dist.barrier()
             set_pull(pull)
     elapsed, averaged, rounds, (lerp_ms, bracket_ms) = run(args.steps, args.warmup, False, args.sample_every)
     wt = None

@@ -10,6 +10,12 @@ for n in 2 4; do
       > gpurun_out/rehearse_n$n.json 2> gpurun_out/rehearse_n$n.err || { echo "rehearsal n=$n failed"; tail -20 gpurun_out/rehearse_n$n.err; exit 1; }
   cat gpurun_out/rehearse_n$n.json
 done
+# six ranks on one GPU: with the default 4 hardware queues per process the card's queue
+# slots are oversubscribed (24) and host-synchronised rounds stall ~20 ms; 2 per process fit
+GPU_MAX_HW_QUEUES=2 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 6 --master-addr 127.0.0.1 \
+    --master-port 29506 bench.py --gpus 6 --dist-backend gloo --steps 40 --warmup 5 --compute-us 300 \
+    > gpurun_out/rehearse_n6.json 2> gpurun_out/rehearse_n6.err || { echo "rehearsal n=6 failed"; tail -20 gpurun_out/rehearse_n6.err; exit 1; }
+cat gpurun_out/rehearse_n6.json
 V="--no-cpu-baseline --no-sweep --no-cold --compute-us 0 --steps 50 --warmup 10"
 timeout -k 10 200 python bench.py $V --numel 1000000000 --dtype bf16 --interpolation loss --divergence-threshold 0.5 \
     --loss-schedule decay > gpurun_out/bench_1b_bf16_loss_decay.json 2> gpurun_out/variants.err &&
