@@ -37,6 +37,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+XGMI_LINK_GBS = 153.6          # MI355X xGMI per link (spec, both directions)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 RESNET18_NUMEL = 11_173_962    # examples/pytorch-cifar/models/resnet.py ResNet18
 REF_SAMPLE_MAX = 32_000_000    # cap on the reference-round CPU sample (elements)
@@ -412,6 +413,23 @@ def main():
             dist.barrier()
             set_pull(pull)
     elapsed, averaged, rounds, (lerp_ms, bracket_ms) = run(args.steps, args.warmup, False, args.sample_every)
+    pull_us = []
+    if world > 1 and not pull.split("/")[-1].startswith("relay"):
+        # the pull alone (side-stream events around each copying fetch), in a short extra run
+        p_steps = max(20, args.steps // 4)
+        for conn, _ in learners:
+            _lib.call("dpwa_learner_time_fetches", conn._learner.handle, p_steps + 4)
+        run(p_steps, 2, False, 1000)
+        for conn, _ in learners:
+            buf = (ctypes.c_float * (p_steps + 4))()
+            cnt = ctypes.c_int()
+            _lib.call("dpwa_learner_read_fetch_times", conn._learner.handle, buf, p_steps + 4, ctypes.byref(cnt))
+            pull_us += list(buf[2:cnt.value])     # the 2 warmup rounds' pulls are left out
+            _lib.call("dpwa_learner_time_fetches", conn._learner.handle, 0)
+        t = torch.tensor([float(np.mean(pull_us)) if pull_us else float("nan")], dtype=torch.float64,
+                         device=device if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        pull_us = [float(t.item()) / world]
     wt = None
     if not args.no_write_through and (world == 1 or args.gossip != "async"):
         chosen = list(learners)
@@ -502,6 +520,18 @@ def main():
         }
         if pull_trials:
             out["pull_trials_gbs"] = pull_trials
+        if world > 1:
+            pull_bytes = 256 + args.numel * esize
+            p_us = pull_us[0] if pull_us and np.isfinite(pull_us[0]) else None
+            out["xgmi"] = {
+                "bytes_per_pull": pull_bytes,
+                "avg_pull_us": round(p_us, 2) if p_us else None,
+                "achieved_gbs_per_pull": round(pull_bytes / (p_us * 1e-6) / 1e9, 1) if p_us else None,
+                "peak_link_gbs": XGMI_LINK_GBS,
+                "note": "one pull = one peer snapshot over the direct link between the two GPUs, timed by "
+                        "side-stream events around each copying fetch (mean over ranks; null for the relay); "
+                        "peak = MI355X xGMI spec per link, both directions together",
+            }
         if wt is not None:
             w_el, w_avg, w_rounds, (w_ms, _) = wt
             w_us = float(np.nanmean(w_ms) * 1e3)

@@ -101,6 +101,8 @@ SIGNATURES = {
     "dpwa_learner_relay_phase1": [_vp, _vp, _u64, _int, _vp],
     "dpwa_learner_relay_phase2": [_vp, _vp, _int, _u64, _int],
     "dpwa_learner_side_stream": [_vp, ctypes.POINTER(_vp)],
+    "dpwa_learner_time_fetches": [_vp, _int],
+    "dpwa_learner_read_fetch_times": [_vp, ctypes.POINTER(ctypes.c_float), _int, ctypes.POINTER(_int)],
     "dpwa_learner_time_averages": [_vp, _int],
     "dpwa_learner_arm_timing": [_vp],
     "dpwa_learner_read_average_times": [_vp, ctypes.POINTER(ctypes.c_float), _int, ctypes.POINTER(_int)],

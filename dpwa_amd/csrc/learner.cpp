@@ -145,6 +145,9 @@ struct dpwa_learner {
     std::vector<LaunchTiming> timing;
     int timing_used = 0;
     bool timing_armed = false;   // time the next averaging launch (one-shot)
+    // timing of copying fetches (bench at N > 1: the pull over xGMI), filled in order
+    std::vector<LaunchTiming> fetch_timing;
+    int fetch_timing_used = 0;
     // relay transport (multi-link lock-step pulls), see kernels.hip
     bool relay_on = false;
     int relay_world = 0, relay_rank = 0;
@@ -305,6 +308,10 @@ int dpwa_learner_destroy(dpwa_learner *l)
     if (l->ev_read) (void)hipEventDestroy(l->ev_read);
     if (l->ev_relay) (void)hipEventDestroy(l->ev_relay);
     for (auto &t : l->timing) {
+        (void)hipEventDestroy(t.start);
+        (void)hipEventDestroy(t.stop);
+    }
+    for (auto &t : l->fetch_timing) {
         (void)hipEventDestroy(t.start);
         (void)hipEventDestroy(t.stop);
     }
@@ -500,11 +507,15 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
             HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
         }
         const size_t nbytes = kHeader + round_up(l->payload_bytes, 16);
+        const LaunchTiming *ft = l->fetch_timing_used < (int)l->fetch_timing.size()
+                                     ? &l->fetch_timing[l->fetch_timing_used++] : nullptr;
+        if (ft) HIP_TRY(hipEventRecord(ft->start, l->side));
         if (l->pull_mode == DPWA_PULL_KERNEL)
             HIP_TRY(launch_pull(l->staging, peer_slot, (int64_t)nbytes, l->pull_blocks,
                                 ep.kind == 2 || ep.device != l->device, l->side));
         else
             HIP_TRY(hipMemcpyAsync(l->staging, peer_slot, nbytes, hipMemcpyDefault, l->side));
+        if (ft) HIP_TRY(hipEventRecord(ft->stop, l->side));
         HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
         l->src = l->staging;
         l->src_copied = true;
@@ -846,6 +857,41 @@ int dpwa_learner_read_average_times(dpwa_learner *l, float *us_out, int max, int
     }
     *count = k;
     l->timing_used = 0;
+    return DPWA_OK;
+}
+
+int dpwa_learner_time_fetches(dpwa_learner *l, int capacity)
+{
+    if (!l || capacity < 0) return set_error(DPWA_ERR_ARG, "dpwa_learner_time_fetches: bad arguments");
+    DeviceGuard dg(l->device);
+    HIP_TRY(hipDeviceSynchronize());
+    for (auto &t : l->fetch_timing) {
+        (void)hipEventDestroy(t.start);
+        (void)hipEventDestroy(t.stop);
+    }
+    l->fetch_timing.clear();
+    l->fetch_timing_used = 0;
+    for (int i = 0; i < capacity; ++i) {
+        LaunchTiming t{};
+        HIP_TRY(hipEventCreate(&t.start));
+        HIP_TRY(hipEventCreate(&t.stop));
+        l->fetch_timing.push_back(t);
+    }
+    return DPWA_OK;
+}
+
+int dpwa_learner_read_fetch_times(dpwa_learner *l, float *us_out, int max, int *count)
+{
+    if (!l || !count || (max > 0 && !us_out)) return set_error(DPWA_ERR_ARG, "dpwa_learner_read_fetch_times: bad arguments");
+    DeviceGuard dg(l->device);
+    const int k = l->fetch_timing_used < max ? l->fetch_timing_used : max;
+    for (int i = 0; i < k; ++i) {
+        HIP_TRY(hipEventSynchronize(l->fetch_timing[i].stop));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, l->fetch_timing[i].start, l->fetch_timing[i].stop));
+        us_out[i] = ms * 1000.f;
+    }
+    *count = k;
     return DPWA_OK;
 }
 

@@ -203,6 +203,10 @@ int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_
 int dpwa_learner_time_averages(dpwa_learner *l, int capacity);
 int dpwa_learner_arm_timing(dpwa_learner *l);
 int dpwa_learner_read_average_times(dpwa_learner *l, float *us_out, int max, int *count);
+/* Bench: time the next `capacity` copying fetches (pull start to landed, on the side
+ * stream; the relay is not timed) and read them back in order, in microseconds. */
+int dpwa_learner_time_fetches(dpwa_learner *l, int capacity);
+int dpwa_learner_read_fetch_times(dpwa_learner *l, float *us_out, int max, int *count);
 /* The learner's side stream (fetches and relay phases run on it). */
 int dpwa_learner_side_stream(dpwa_learner *l, dpwa_stream_t *stream);
 
