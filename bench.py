@@ -381,7 +381,7 @@ def main():
     if world > 1:
         run(2, 2, False, 1000)   # binds the learners (IPC exchange) before the transport is chosen
         modes = [args.pull] if args.pull != "auto" else ["copy", "kernel:256", "kernel:1024", "relay:32",
-                                                         "relay:128"]
+                                                         "relay:128", "relay:512"]
         trial_steps = max(10, args.steps // 10)
         if args.gossip != "async":
             for mode in modes:       # short timed trial of each transport; the fastest is used below
