@@ -184,13 +184,18 @@ struct LerpArgs {
 // against plain loads/stores 11.2M fp32 went from 25.4 to 21.6 us cold and from 18.0 to
 // 16.4 us Infinity-Cache warm, 100M fp32 from 198 to 189 us.
 constexpr int kSpan = kBlock * 16;
+// From 8M 16-byte items per operand (128 MB) the averaging runs one-wave workgroups:
+// tools/lerp_tune.hip measured 64-lane workgroups 1-1.3% faster than 256 at 100M fp32 cold
+// (profiles/r01d_lerp_tune_cold_100m.log) and 2% slower at 11.2M (..._cold_11m.log).
+constexpr int64_t kLargeVectors = 8ll << 20;
 constexpr int kAuxStream = 2;    // nt
 constexpr int kAuxStore = 16;    // sc1
 
+template <int SPAN = kSpan>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const void *base, int64_t off, int64_t total)
 {
     const int64_t rem = total - off;
-    const int num = rem <= 0 ? 0 : (rem < kSpan ? (int)rem : kSpan);
+    const int num = rem <= 0 ? 0 : (rem < SPAN ? (int)rem : SPAN);
     return __builtin_amdgcn_make_buffer_rsrc((void *)((const char *)base + off), 0, num, 0x00020000);
 }
 
@@ -208,17 +213,19 @@ __device__ __forceinline__ void span_store(__amdgpu_buffer_rsrc_t r, int lane_of
 
 // One 16-byte item per lane; items beyond n/PER (the ragged tail) go to block 0.
 // DUAL also stores the result into args.snap (write-through snapshot: the next publish of
-// these parameters then needs no copy).
-template <class Ops, int MODE, bool DUAL>
-__global__ __launch_bounds__(kBlock) void k_lerp(typename Ops::V *__restrict__ param,
-                                                 const typename Ops::V *__restrict__ peer, int64_t n, LerpArgs args)
+// these parameters then needs no copy).  BLOCK: 256 lanes (4 waves) by default, one wave
+// per workgroup for large vectors (see kLargeVectors).
+template <class Ops, int MODE, bool DUAL, int BLOCK = kBlock>
+__global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ param,
+                                                const typename Ops::V *__restrict__ peer, int64_t n, LerpArgs args)
 {
     using V = typename Ops::V;
+    constexpr int SPAN = BLOCK * 16;
     const int64_t nv = n / Ops::PER;
-    const int64_t span_off = (int64_t)blockIdx.x * kSpan;
+    const int64_t span_off = (int64_t)blockIdx.x * SPAN;
     const int lane_off = threadIdx.x * 16;
-    const __amdgpu_buffer_rsrc_t rq = span_rsrc(peer, span_off, nv * 16);
-    const __amdgpu_buffer_rsrc_t rp = span_rsrc(param, span_off, nv * 16);
+    const __amdgpu_buffer_rsrc_t rq = span_rsrc<SPAN>(peer, span_off, nv * 16);
+    const __amdgpu_buffer_rsrc_t rp = span_rsrc<SPAN>(param, span_off, nv * 16);
     // issue this lane's loads before anything else
     const V q = span_load<V>(rq, lane_off);
     const V p = span_load<V>(rp, lane_off);
@@ -246,7 +253,7 @@ __global__ __launch_bounds__(kBlock) void k_lerp(typename Ops::V *__restrict__ p
         }
         __syncthreads();
         if (!s_ok) {          // no-op round; a write-through snapshot still gets the parameters
-            if (DUAL) span_store(span_rsrc(args.snap, span_off, nv * 16), lane_off, p);
+            if (DUAL) span_store(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, p);
             if (DUAL && blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
                 const int64_t j = nv * Ops::PER + threadIdx.x;
                 reinterpret_cast<typename Ops::S *>(args.snap)[j] = reinterpret_cast<typename Ops::S *>(param)[j];
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(kBlock) void k_lerp(typename Ops::V *__restrict__ p
     {
         const V r = Ops::lerp(a, b, q, p);
         span_store(rp, lane_off, r);
-        if (DUAL) span_store(span_rsrc(args.snap, span_off, nv * 16), lane_off, r);
+        if (DUAL) span_store(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, r);
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
         typename Ops::S *ps = reinterpret_cast<typename Ops::S *>(param);
@@ -316,7 +323,18 @@ static hipError_t launch_mode(void *param, const void *peer, int64_t n, const Le
                               const LaunchTiming *timing)
 {
     if (aligned16(param) && aligned16(peer) && aligned16(args.snap)) {
-        const int64_t g = blocks_for(n / Ops::PER);
+        const int64_t nv = n / Ops::PER;
+        if (nv >= kLargeVectors) {   // one-wave workgroups
+            const int64_t g = nv / 64 + 1;
+            if (timing)
+                hipExtLaunchKernelGGL((k_lerp<Ops, MODE, DUAL, 64>), dim3((uint32_t)g), dim3(64), 0, s, timing->start,
+                                      timing->stop, 0, (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
+            else
+                hipLaunchKernelGGL((k_lerp<Ops, MODE, DUAL, 64>), dim3((uint32_t)g), dim3(64), 0, s,
+                                   (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
+            return hipGetLastError();
+        }
+        const int64_t g = blocks_for(nv);
         if (timing)   // the dispatch itself is timed (the kernel's begin/end, as a profiler sees it)
             hipExtLaunchKernelGGL((k_lerp<Ops, MODE, DUAL>), dim3((uint32_t)g), dim3(kBlock), 0, s, timing->start,
                                   timing->stop, 0, (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
