@@ -5,15 +5,16 @@
 //             parameter buffer (the reference runs three ATen kernels and allocates three
 //             temporaries per tensor).  Pure HBM streaming (0.25 flop/byte): no LDS
 //             staging, no MFMA.  Shape chosen by measurement (tools/lerp_tune.hip): one
-//             16-byte item per lane and an exact grid -- thousands of short-lived 4-wave
-//             workgroups keep the most loads in flight per CU; grid-stride loops with
-//             more items per lane or a capped grid were 5-20% slower on gfx950.
+//             16-byte item per lane and an exact grid -- many short-lived one-wave
+//             workgroups keep the most loads in flight per CU (tools/block_sweep.sh);
+//             grid-stride loops with more items per lane or a capped grid were 5-20%
+//             slower on gfx950.
 //             Separate roundings are required for bit parity with the reference (an FMA
 //             changes up to ~30% of results near cancellation), so contraction is
 //             switched off for this whole file.
 //  * fused average: the same pass with the factor of dpwa/dpwa.py:139-155 computed in
 //             the kernel: wave 0 of every workgroup evaluates it in fp64 while the
-//             workgroup's loads are in flight and broadcasts (a, b) through LDS; block 0
+//             workgroup's loads are in flight and shares (a, b) through LDS; block 0
 //             also writes the new clock (into the other half of a double-buffered clock,
 //             so no workgroup ever reads a clock another one is writing) and dpwa_coef.
 //  * factor:  the same fp64 math as a one-thread kernel for the split API.
@@ -176,7 +177,7 @@ struct LerpArgs {
 };
 
 // ---------------------------------------------------------------- streaming buffer access
-// Every workgroup covers one 4 KiB span (256 lanes x 16 B) of each operand through its own
+// Every workgroup covers one span (BLOCK lanes x 16 B) of each operand through its own
 // buffer descriptor: 32-bit lane offsets whatever the buffer size (7B bf16 = 14 GB), and the
 // hardware range check drops the lanes past the end (loads return 0, stores are discarded),
 // so no lane branches.  Cache policy, chosen by measurement (tools/lerp_tune.hip,
@@ -184,10 +185,11 @@ struct LerpArgs {
 // against plain loads/stores 11.2M fp32 went from 25.4 to 21.6 us cold and from 18.0 to
 // 16.4 us Infinity-Cache warm, 100M fp32 from 198 to 189 us.
 constexpr int kSpan = kBlock * 16;
-// From 8M 16-byte items per operand (128 MB) the averaging runs one-wave workgroups:
-// tools/lerp_tune.hip measured 64-lane workgroups 1-1.3% faster than 256 at 100M fp32 cold
-// (profiles/r01d_lerp_tune_cold_100m.log) and 2% slower at 11.2M (..._cold_11m.log).
-constexpr int64_t kLargeVectors = 8ll << 20;
+// The averaging and publish kernels run one-wave (64-lane) workgroups: inside the gossip
+// round (tools/block_sweep.sh, profiles/r01e_block_sweep_*.log) 64 beat 128/256/512 lanes
+// cold at 11.2M fp32 (21.7 vs 22.5 us) and at 100M (179-183 vs 182-194 us), and the round
+// with a 64-lane publish was the fastest or within noise of it at both sizes.
+constexpr int kStreamBlock = 64;
 constexpr int kAuxStream = 2;    // nt
 constexpr int kAuxStore = 16;    // sc1
 
@@ -213,8 +215,7 @@ __device__ __forceinline__ void span_store(__amdgpu_buffer_rsrc_t r, int lane_of
 
 // One 16-byte item per lane; items beyond n/PER (the ragged tail) go to block 0.
 // DUAL also stores the result into args.snap (write-through snapshot: the next publish of
-// these parameters then needs no copy).  BLOCK: 256 lanes (4 waves) by default, one wave
-// per workgroup for large vectors (see kLargeVectors).
+// these parameters then needs no copy).  BLOCK lanes per workgroup (kStreamBlock).
 template <class Ops, int MODE, bool DUAL, int BLOCK = kBlock>
 __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ param,
                                                 const typename Ops::V *__restrict__ peer, int64_t n, LerpArgs args)
@@ -318,29 +319,43 @@ __global__ __launch_bounds__(kBlock) void k_lerp_unaligned(typename Ops::S *__re
 
 static inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
+// Workgroup size of the averaging kernel; DPWA_LERP_BLOCK (64/128/256/512) forces another
+// (tuning).
+static int lerp_block()
+{
+    static const int forced = [] {
+        const char *e = getenv("DPWA_LERP_BLOCK");
+        const int b = e ? atoi(e) : 0;
+        return (b == 64 || b == 128 || b == 256 || b == 512) ? b : 0;
+    }();
+    return forced ? forced : kStreamBlock;
+}
+
+template <class Ops, int MODE, bool DUAL, int BLOCK>
+static hipError_t launch_blocks(void *param, const void *peer, int64_t n, const LerpArgs &args, hipStream_t s,
+                                const LaunchTiming *timing)
+{
+    const int64_t g = (n / Ops::PER) / BLOCK + 1;   // the last span may be empty (range-checked)
+    if (timing)   // the dispatch itself is timed (the kernel's begin/end, as a profiler sees it)
+        hipExtLaunchKernelGGL((k_lerp<Ops, MODE, DUAL, BLOCK>), dim3((uint32_t)g), dim3(BLOCK), 0, s, timing->start,
+                              timing->stop, 0, (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
+    else
+        hipLaunchKernelGGL((k_lerp<Ops, MODE, DUAL, BLOCK>), dim3((uint32_t)g), dim3(BLOCK), 0, s,
+                           (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
+    return hipGetLastError();
+}
+
 template <class Ops, int MODE, bool DUAL>
 static hipError_t launch_mode(void *param, const void *peer, int64_t n, const LerpArgs &args, hipStream_t s,
                               const LaunchTiming *timing)
 {
     if (aligned16(param) && aligned16(peer) && aligned16(args.snap)) {
-        const int64_t nv = n / Ops::PER;
-        if (nv >= kLargeVectors) {   // one-wave workgroups
-            const int64_t g = nv / 64 + 1;
-            if (timing)
-                hipExtLaunchKernelGGL((k_lerp<Ops, MODE, DUAL, 64>), dim3((uint32_t)g), dim3(64), 0, s, timing->start,
-                                      timing->stop, 0, (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
-            else
-                hipLaunchKernelGGL((k_lerp<Ops, MODE, DUAL, 64>), dim3((uint32_t)g), dim3(64), 0, s,
-                                   (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
-            return hipGetLastError();
+        switch (lerp_block()) {
+        case 64: return launch_blocks<Ops, MODE, DUAL, 64>(param, peer, n, args, s, timing);
+        case 128: return launch_blocks<Ops, MODE, DUAL, 128>(param, peer, n, args, s, timing);
+        case 512: return launch_blocks<Ops, MODE, DUAL, 512>(param, peer, n, args, s, timing);
+        default: return launch_blocks<Ops, MODE, DUAL, 256>(param, peer, n, args, s, timing);
         }
-        const int64_t g = blocks_for(nv);
-        if (timing)   // the dispatch itself is timed (the kernel's begin/end, as a profiler sees it)
-            hipExtLaunchKernelGGL((k_lerp<Ops, MODE, DUAL>), dim3((uint32_t)g), dim3(kBlock), 0, s, timing->start,
-                                  timing->stop, 0, (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
-        else
-            hipLaunchKernelGGL((k_lerp<Ops, MODE, DUAL>), dim3((uint32_t)g), dim3(kBlock), 0, s,
-                               (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
     } else {
         // (callers time only the aligned product kernel; an unaligned launch is not timed)
         int64_t g = blocks_for(n);
@@ -391,19 +406,20 @@ hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t 
 }
 
 // ---------------------------------------------------------------- publish
-template <bool VEC>
-__global__ __launch_bounds__(kBlock) void k_publish(char *__restrict__ slot, const char *__restrict__ flat,
-                                                    int64_t nbytes, int64_t n, int32_t dtype,
-                                                    double *__restrict__ clock, double loss_h,
-                                                    const double *__restrict__ loss_d, uint64_t version)
+template <bool VEC, int BLOCK = kBlock>
+__global__ __launch_bounds__(BLOCK) void k_publish(char *__restrict__ slot, const char *__restrict__ flat,
+                                                   int64_t nbytes, int64_t n, int32_t dtype,
+                                                   double *__restrict__ clock, double loss_h,
+                                                   const double *__restrict__ loss_d, uint64_t version)
 {
     char *payload = slot + sizeof(dpwa_header);
     if (VEC) {   // one 16-B item per lane, streaming policy of the lerp (nt loads, sc1 stores)
+        constexpr int SPAN = BLOCK * 16;
         const int64_t n16 = nbytes >> 4;
-        const int64_t span_off = (int64_t)blockIdx.x * kSpan;
+        const int64_t span_off = (int64_t)blockIdx.x * SPAN;
         const int lane_off = threadIdx.x * 16;
-        span_store(span_rsrc(payload, span_off, n16 * 16), lane_off,
-                   span_load<u32x4>(span_rsrc(flat, span_off, n16 * 16), lane_off));
+        span_store(span_rsrc<SPAN>(payload, span_off, n16 * 16), lane_off,
+                   span_load<u32x4>(span_rsrc<SPAN>(flat, span_off, n16 * 16), lane_off));
         if (blockIdx.x == 0 && threadIdx.x < (nbytes & 15)) {
             const int64_t j = (n16 << 4) + threadIdx.x;
             payload[j] = flat[j];
@@ -541,14 +557,34 @@ __global__ __launch_bounds__(64) void k_release_system()
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
+// Workgroup size of the snapshot copy; DPWA_PUBLISH_BLOCK (64/128/256) forces another.
+static int publish_block()
+{
+    static const int forced = [] {
+        const char *e = getenv("DPWA_PUBLISH_BLOCK");
+        const int b = e ? atoi(e) : 0;
+        return (b == 64 || b == 128 || b == 256) ? b : 0;
+    }();
+    return forced ? forced : kStreamBlock;
+}
+
 hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t n, int32_t dtype, double *clock,
                           double loss, const double *loss_dev, uint64_t version, bool system_release, hipStream_t s)
 {
     const char *src = (const char *)flat;
     if (aligned16(flat)) {
-        const int64_t g = blocks_for(nbytes >> 4);
-        hipLaunchKernelGGL((k_publish<true>), dim3((uint32_t)g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype, clock,
-                           loss, loss_dev, version);
+        const int64_t n16 = nbytes >> 4;
+        const int b = publish_block();
+        const int64_t g = n16 / b + 1;
+        if (b == 64)
+            hipLaunchKernelGGL((k_publish<true, 64>), dim3((uint32_t)g), dim3(64), 0, s, slot, src, nbytes, n, dtype,
+                               clock, loss, loss_dev, version);
+        else if (b == 128)
+            hipLaunchKernelGGL((k_publish<true, 128>), dim3((uint32_t)g), dim3(128), 0, s, slot, src, nbytes, n,
+                               dtype, clock, loss, loss_dev, version);
+        else
+            hipLaunchKernelGGL((k_publish<true>), dim3((uint32_t)g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype,
+                               clock, loss, loss_dev, version);
     } else {
         int64_t g = blocks_for(nbytes);
         if (g > 8192) g = 8192;
