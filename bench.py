@@ -79,7 +79,7 @@ def parse():
                          "board), or a short trial of both keeping the faster")
     ap.add_argument("--compute-us", type=float, default=1000.0,
                     help="per-learner synthetic training step (bf16 GEMM loop) for the 'overlap' field; 0 = skip")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01e.json"),
                     help="PMC traffic summary (rocprofv3 FETCH_SIZE/WRITE_SIZE passes) to report")
     return ap.parse_args()
 
@@ -125,6 +125,22 @@ def cpu_baseline(numel, seconds):
         "value": rounds * 3 * numel * 4 / el / 1e9, "unit": "GB/s", "cores": 1,
         "sample": "%d rounds of publish-copy + fp32 lerp over %d elements (oracle/dpwa_oracle.c, -O3, 1 thread, "
                   "%.1f s): the arithmetic alone, no transport" % (rounds, numel, el),
+        "ms_per_round": 1e3 * el / rounds}
+    # and the reference's own lerp statement (pytorch.py:68, torch eager) on every thread torch
+    # uses here: the multi-core CPU ceiling for the arithmetic
+    tp, tq = torch.from_numpy(param), torch.from_numpy(peer)
+    rounds = 0
+    t0 = time.perf_counter()
+    while True:
+        tp = 0.5 * tq + (1.0 - 0.5) * tp
+        rounds += 1
+        el = time.perf_counter() - t0
+        if el >= min(3.0, seconds / 3):
+            break
+    out["torch_cpu_lerp"] = {
+        "value": rounds * 3 * numel * 4 / el / 1e9, "unit": "GB/s", "cores": torch.get_num_threads(),
+        "sample": "%d evaluations of the reference's lerp statement (pytorch.py:68) as torch-CPU fp32 eager ops "
+                  "over %d elements, %.1f s" % (rounds, numel, el),
         "ms_per_round": 1e3 * el / rounds}
     return out
 

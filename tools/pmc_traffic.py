@@ -43,7 +43,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
-    ap.add_argument("--kernel", default="k_lerp<dpwa::OpsF32, 2, false>")
+    ap.add_argument("--kernel", default="k_lerp<dpwa::OpsF32, 2, false,")
     ap.add_argument("--numel", type=int, default=11_173_962)
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--gpus", type=int, default=1)
