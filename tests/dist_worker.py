@@ -116,6 +116,13 @@ def async_base(rank, r, n):
     return (np.arange(n, dtype=np.float32) * np.float32(1e-3) + np.float32(rank * 1000 + r)).astype(np.float32)
 
 
+def async_loss(rank, r, wait=False):
+    """The loss rank `rank` passes at its round r (update_send, or update_wait when `wait`):
+    decaying, so a divergence threshold is crossed mid-run."""
+    x = 2.0 * float(np.exp(-r / 8.0)) + 0.1 * rank + 0.05
+    return 0.9 * x if wait else x
+
+
 def async_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy", die_rank=-1, die_round=-1):
     """Free-running gossip (AsyncDistGroup): every round sets the parameters to
     async_base(rank, r), publishes, sleeps a rank- and round-dependent time on the GPU and
@@ -144,9 +151,9 @@ def async_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy", die_ra
             conn._group.leave(conn)    # leaves mid-run (the board entry closes, its readers drain)
             os._exit(0)                # ... and dies: no close(), no barrier
         flat.copy_(bases[r])
-        conn.update_send(flat, 1.0)
+        conn.update_send(flat, async_loss(rank, r))
         torch.cuda._sleep(int(rng.integers(0, 400_000)))     # uneven "training steps"
-        payload, _ = conn.update_wait_average(flat, 1.0)
+        payload, _ = conn.update_wait_average(flat, async_loss(rank, r, wait=True))
         peers.append(payload.peer if payload is not None else "")
         versions.append(conn._info()[2] if payload is not None else 0)
         params[r] = flat.cpu().numpy()

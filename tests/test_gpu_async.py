@@ -13,6 +13,7 @@ import pytest
 import torch.multiprocessing as mp
 
 from oracle import lerp as olerp
+from oracle.policy import factor_and_clock
 from tests import dist_worker
 
 pytestmark = pytest.mark.gpu
@@ -26,15 +27,15 @@ def free_port():
     return p
 
 
-def factor_of(interp, clock, pclock):
-    """interpolation.py:13-24 (constant 0.5 / clock-weighted)."""
-    return 0.5 if interp == "constant" else pclock / (clock + pclock)
-
-
-def check_run(tmp_path, world, n, T, ranks, interp="constant"):
+def check_run(tmp_path, world, n, T, ranks, interp="constant", thr=0.0):
     names = ["r%d" % i for i in range(world)]
     runs = {g: np.load(tmp_path / ("rank%d.npz" % g)) for g in ranks}
     c_after = {}
+
+    def policy(g, r):           # dpwa.py:143-155 for rank g's round r against what it read
+        q, v = names.index(str(runs[g]["peers"][r])), int(runs[g]["versions"][r])
+        return factor_and_clock(interp, 0.5, thr, c_pub(g, r), c_pub(q, v - 1), dist_worker.async_loss(g, r, True),
+                                dist_worker.async_loss(q, v - 1))
 
     def c_pub(g, r):            # the clock rank g published at its round r (dpwa.py:112)
         return (c_after_of(g, r - 1) if r > 0 else 0.0) + 1.0
@@ -45,9 +46,7 @@ def check_run(tmp_path, world, n, T, ranks, interp="constant"):
             if run["peers"][r] == "":
                 c_after[(g, r)] = c_pub(g, r)
             else:
-                q, v = names.index(str(run["peers"][r])), int(run["versions"][r])
-                factor = factor_of(interp, c_pub(g, r), c_pub(q, v - 1))
-                c_after[(g, r)] = factor * c_pub(q, v - 1) + (1 - factor) * c_pub(g, r)
+                c_after[(g, r)] = policy(g, r)[1]
         return c_after[(g, r)]
 
     averaged = 0
@@ -64,7 +63,11 @@ def check_run(tmp_path, world, n, T, ranks, interp="constant"):
                 assert 1 <= v, (g, r)
                 assert v >= last.get(q, 0), (g, r, "versions went backwards")
                 last[q] = v
-                factor = factor_of(interp, c_pub(g, r), c_pub(q, v - 1)) if len(runs) == world else 0.5
+                if len(runs) == world:
+                    factor = policy(g, r)[0]
+                else:           # a rank's clocks are unknown once it has gone: constant only
+                    assert interp == "constant" and thr == 0.0
+                    factor = 0.5
                 want = olerp.lerp_f32(mine, dist_worker.async_base(q, v - 1, n), factor)
                 averaged += 1
             assert olerp.bits_equal(run["params"][r], want), (g, r, peer)
@@ -73,17 +76,22 @@ def check_run(tmp_path, world, n, T, ranks, interp="constant"):
     return runs, averaged
 
 
-@pytest.mark.parametrize("world,pull,interp", [(2, "copy", "constant"), (3, "kernel:64", "constant"),
-                                               (3, "copy", "clock")])
-def test_async_gossip_reads_whole_snapshots(tmp_path, world, pull, interp):
+@pytest.mark.parametrize("world,pull,interp,fp,thr", [(2, "copy", "constant", 1.0, 0.0),
+                                                      (3, "kernel:64", "constant", 1.0, 0.0),
+                                                      (3, "copy", "clock", 1.0, 0.0),
+                                                      (3, "kernel", "loss", 0.7, 0.5)])
+def test_async_gossip_reads_whole_snapshots(tmp_path, world, pull, interp, fp, thr):
     n, T = 1_000_003, 40
     names = ["r%d" % i for i in range(world)]
     cfg = str(tmp_path / "async.yaml")
-    dist_worker.write_cfg(cfg, names, 1.0, interp, 0.0)
+    dist_worker.write_cfg(cfg, names, fp, interp, thr)
     mp.spawn(dist_worker.async_worker, args=(world, free_port(), cfg, str(tmp_path), n, T, pull), nprocs=world,
              join=True)
-    _, averaged = check_run(tmp_path, world, n, T, range(world), interp)
-    assert averaged >= world * (T - 3)     # only rounds before a peer's first publish may be empty
+    _, averaged = check_run(tmp_path, world, n, T, range(world), interp, thr)
+    if fp == 1.0:
+        assert averaged >= world * (T - 3)     # only rounds before a peer's first publish may be empty
+    else:
+        assert averaged >= world * T * fp * 0.5
 
 
 def test_async_gossip_survives_a_rank_that_leaves(tmp_path):
