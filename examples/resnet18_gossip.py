@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--batch-size", type=int, default=8)      # prepare.py:31
     ap.add_argument("--lr", type=float, default=0.01)         # prepare.py:31
     ap.add_argument("--interpolation", default="constant")
+    ap.add_argument("--gossip", default="lockstep", choices=["lockstep", "async"],
+                    help="under torchrun: lock-step rounds (DistGroup) or free-running ones (gossip board)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,7 +115,8 @@ def main():
 
     run(args.warmup, False)
     t_plain = run(args.steps, False)
-    adapters = [DpwaPyTorchAdapter(nets[i], names[g], cfg, seed=100 + g) for i, g in enumerate(mine)]
+    group = {"group": args.gossip} if world > 1 else {}
+    adapters = [DpwaPyTorchAdapter(nets[i], names[g], cfg, seed=100 + g, **group) for i, g in enumerate(mine)]
     run(args.warmup, True, adapters)
     t_gossip = run(args.steps, True, adapters)
     if world > 1:
