@@ -49,6 +49,14 @@ def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100
         assert olerp.bits_equal(got["params"], exp["params"][:, r]), r
 
 
+@pytest.mark.parametrize("pull", ["relay:8", "kernel"])
+def test_ipc_gossip_six_ranks(tmp_path, monkeypatch, pull):
+    """Six ranks (the relay's stripes over more than four peers).  Six processes on one card
+    oversubscribe its hardware queues with the default 4 per process, so the children get 2."""
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "2")
+    test_ipc_gossip_matches_oracle(tmp_path, 6, "clock", 0.8, 0.0, pull, n=65_537)
+
+
 def test_relay_tiny_payload(tmp_path):
     """5 parameters over 4 ranks: one 32-B stripe, three empty ones."""
     test_ipc_gossip_matches_oracle(tmp_path, 4, "constant", 1.0, 0.0, "relay:2", n=5)
