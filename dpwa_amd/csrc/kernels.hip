@@ -207,16 +207,24 @@ __device__ __forceinline__ V span_load(__amdgpu_buffer_rsrc_t r, int lane_off)
     return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, 0, AUX));
 }
 
-template <class V>
+template <class V, int AUX = kAuxStore>
 __device__ __forceinline__ void span_store(__amdgpu_buffer_rsrc_t r, int lane_off, V v)
 {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, lane_off, 0, kAuxStore);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, lane_off, 0, AUX);
 }
+
+// Cache policies of the averaging kernel (tuning; DPWA_LERP_POLICY): the peer snapshot is
+// always read `nt`; the parameters are read `nt` (0, 2) or with the default policy (1, 3);
+// the result is stored `sc1` (0, 1) or `sc0 sc1` (2, 3).
+template <int POLICY> struct LerpPolicy {
+    static constexpr int param_load = (POLICY & 1) ? 0 : kAuxStream;
+    static constexpr int store = (POLICY & 2) ? (kAuxStore | 1) : kAuxStore;
+};
 
 // One 16-byte item per lane; items beyond n/PER (the ragged tail) go to block 0.
 // DUAL also stores the result into args.snap (write-through snapshot: the next publish of
 // these parameters then needs no copy).  BLOCK lanes per workgroup (kStreamBlock).
-template <class Ops, int MODE, bool DUAL, int BLOCK = kBlock>
+template <class Ops, int MODE, bool DUAL, int BLOCK = kBlock, int POLICY = 0>
 __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ param,
                                                 const typename Ops::V *__restrict__ peer, int64_t n, LerpArgs args)
 {
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ pa
     const __amdgpu_buffer_rsrc_t rp = span_rsrc<SPAN>(param, span_off, nv * 16);
     // issue this lane's loads before anything else
     const V q = span_load<V>(rq, lane_off);
-    const V p = span_load<V>(rp, lane_off);
+    const V p = span_load<V, LerpPolicy<POLICY>::param_load>(rp, lane_off);
     float a, b;
     if (MODE == COEF_HOST) {
         a = args.a;
@@ -266,7 +274,7 @@ __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ pa
     }
     {
         const V r = Ops::lerp(a, b, q, p);
-        span_store(rp, lane_off, r);
+        span_store<V, LerpPolicy<POLICY>::store>(rp, lane_off, r);
         if (DUAL) span_store(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, r);
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
@@ -331,18 +339,29 @@ static int lerp_block()
     return forced ? forced : kStreamBlock;
 }
 
-template <class Ops, int MODE, bool DUAL, int BLOCK>
+template <class Ops, int MODE, bool DUAL, int BLOCK, int POLICY = 0>
 static hipError_t launch_blocks(void *param, const void *peer, int64_t n, const LerpArgs &args, hipStream_t s,
                                 const LaunchTiming *timing)
 {
     const int64_t g = (n / Ops::PER) / BLOCK + 1;   // the last span may be empty (range-checked)
     if (timing)   // the dispatch itself is timed (the kernel's begin/end, as a profiler sees it)
-        hipExtLaunchKernelGGL((k_lerp<Ops, MODE, DUAL, BLOCK>), dim3((uint32_t)g), dim3(BLOCK), 0, s, timing->start,
-                              timing->stop, 0, (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
+        hipExtLaunchKernelGGL((k_lerp<Ops, MODE, DUAL, BLOCK, POLICY>), dim3((uint32_t)g), dim3(BLOCK), 0, s,
+                              timing->start, timing->stop, 0, (typename Ops::V *)param,
+                              (const typename Ops::V *)peer, n, args);
     else
-        hipLaunchKernelGGL((k_lerp<Ops, MODE, DUAL, BLOCK>), dim3((uint32_t)g), dim3(BLOCK), 0, s,
+        hipLaunchKernelGGL((k_lerp<Ops, MODE, DUAL, BLOCK, POLICY>), dim3((uint32_t)g), dim3(BLOCK), 0, s,
                            (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
     return hipGetLastError();
+}
+
+static int lerp_policy()
+{
+    static const int forced = [] {
+        const char *e = getenv("DPWA_LERP_POLICY");
+        const int p = e ? atoi(e) : 0;
+        return (p >= 0 && p <= 3) ? p : 0;
+    }();
+    return forced;
 }
 
 template <class Ops, int MODE, bool DUAL>
@@ -351,7 +370,13 @@ static hipError_t launch_mode(void *param, const void *peer, int64_t n, const Le
 {
     if (aligned16(param) && aligned16(peer) && aligned16(args.snap)) {
         switch (lerp_block()) {
-        case 64: return launch_blocks<Ops, MODE, DUAL, 64>(param, peer, n, args, s, timing);
+        case 64:
+            switch (lerp_policy()) {
+            case 1: return launch_blocks<Ops, MODE, DUAL, 64, 1>(param, peer, n, args, s, timing);
+            case 2: return launch_blocks<Ops, MODE, DUAL, 64, 2>(param, peer, n, args, s, timing);
+            case 3: return launch_blocks<Ops, MODE, DUAL, 64, 3>(param, peer, n, args, s, timing);
+            default: return launch_blocks<Ops, MODE, DUAL, 64>(param, peer, n, args, s, timing);
+            }
         case 128: return launch_blocks<Ops, MODE, DUAL, 128>(param, peer, n, args, s, timing);
         case 512: return launch_blocks<Ops, MODE, DUAL, 512>(param, peer, n, args, s, timing);
         default: return launch_blocks<Ops, MODE, DUAL, 256>(param, peer, n, args, s, timing);

@@ -380,17 +380,16 @@ int main(int argc, char **argv)
     CHECK(hipStreamCreate(&s));
     CHECK(hipMalloc(&g_snap, bytes));
     std::vector<Variant> vs = {
-        one<256, false, false>("one256 (r01a product)"),
-        buf<256, 2, 2, 16>("buf256 nt loads sc1 store (product)"),
-        buf<256, 2, 2, 2>("buf256 nt loads nt store"),
-        buf<256, 2, 2, 0>("buf256 nt loads plain store"),
-        buf<64, 2, 2, 16>("buf64 nt loads sc1 store"),
-        buf<512, 2, 2, 16>("buf512 nt loads sc1 store"),
-        bufu<256, 2, 2, 16>("bufu256x2 nt loads sc1 store"),
-        bufu<256, 4, 2, 16>("bufu256x4 nt loads sc1 store"),
-        bufu<128, 2, 2, 16>("bufu128x2 nt loads sc1 store"),
-        bufu<64, 4, 2, 16>("bufu64x4 nt loads sc1 store"),
-        bufu<512, 2, 2, 16>("bufu512x2 nt loads sc1 store"),
+        buf<256, 2, 2, 16>("buf256 nt loads sc1 store (r01d product)"),
+        buf<64, 2, 2, 16>("buf64 nt loads sc1 store (product)"),
+        buf<64, 0, 0, 16>("buf64 plain loads sc1 store"),
+        buf<64, 2, 0, 16>("buf64 nt peer, plain param, sc1 store"),
+        buf<64, 2, 2, 2>("buf64 nt loads nt store"),
+        buf<64, 2, 2, 17>("buf64 nt loads sc0+sc1 store"),
+        buf<64, 2, 2, 0>("buf64 nt loads plain store"),
+        buf<64, 18, 18, 16>("buf64 nt+sc1 loads sc1 store"),
+        buf<128, 2, 2, 16>("buf128 nt loads sc1 store"),
+        bufu<64, 2, 2, 16>("bufu64x2 nt loads sc1 store"),
         copybuf<256, 2, 16>("copybuf256 nt load sc1 store (x2 bytes)"),
         copybuf<64, 2, 16>("copybuf64 nt load sc1 store (x2 bytes)"),
         {"hipMemcpyAsync D2D (x2 bytes)", 2.0,
