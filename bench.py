@@ -480,7 +480,9 @@ def main():
             "gossip_rounds_per_s": round(o_steps * len(learners) * world / t_both, 1),   # all learners, all ranks
             "transport": o_mode if world > 1 else "in-place HBM read (co-resident peer)",
             "note": "update_send -> synthetic training step -> update_wait_average (SURVEY §8d C4 "
-                    "weak scaling): the overhead the gossip round adds to a step of this length",
+                    "weak scaling): the overhead the gossip round adds to a step of this length. Scaling "
+                    "definition: per-learner compute is fixed, so gossip_rounds_per_s (all learners) "
+                    "compared across N is the weak-scaling figure; value above is the raw bandwidth loop",
         }
         if o_trials:
             overlap["trials_ms_per_step"] = {m: round(1e3 * t / o_steps, 4) for m, t in o_trials.items()}
