@@ -10,8 +10,8 @@
 //   * one POSIX shared-memory block per node set (all ranks of a node), mapped by every
 //     rank and registered with HIP so a stream can write into it;
 //   * version[p]   -- the newest *complete* snapshot of publisher p.  Written by p's stream
-//                     (hipStreamWriteValue64) after the publish kernel and its system-scope
-//                     release, so a reader never sees a version before its bytes;
+//                     (a one-wave release-store kernel) after the publish kernel and its
+//                     system-scope release, so a reader never sees a version before its bytes;
 //   * reading[p][r] -- the version of p that reader r is pulling (0 = none).  Set by r's
 //                     host before the pull is enqueued, cleared by r's side stream after
 //                     the pull has landed;
@@ -42,6 +42,7 @@
 #include <unistd.h>
 
 #include "common.hpp"
+#include "kernels.hpp"
 
 using namespace dpwa;
 
@@ -106,6 +107,18 @@ struct dpwa_board {
         return !(kill(pid, 0) == -1 && errno == ESRCH);
     }
 };
+
+// Stream-ordered store into the board: a one-wave kernel (a release store at system scope)
+// by default; DPWA_BOARD_WRITE=value uses hipStreamWriteValue64 instead (comparison).
+static hipError_t stream_store(uint64_t *dev_ptr, uint64_t v, hipStream_t s)
+{
+    static const bool write_value = [] {
+        const char *e = getenv("DPWA_BOARD_WRITE");
+        return e && std::string(e) == "value";
+    }();
+    if (write_value) return hipStreamWriteValue64(s, dev_ptr, v, 0);
+    return launch_store_u64(dev_ptr, v, s);
+}
 
 extern "C" {
 
@@ -272,7 +285,7 @@ int dpwa_board_release(dpwa_board *b, int r, dpwa_stream_t stream, int host)
         return DPWA_OK;
     }
     if (!b->dev_base) return set_error(DPWA_ERR_STATE, "dpwa_board_release: board not registered with a device");
-    HIP_TRY(hipStreamWriteValue64((hipStream_t)stream, b->dev(mark), 0, 0));
+    HIP_TRY(stream_store(b->dev(mark), 0, (hipStream_t)stream));
     return DPWA_OK;
 }
 
@@ -321,7 +334,7 @@ int dpwa_board_advertise(dpwa_board *b, uint64_t version, dpwa_stream_t stream, 
         return DPWA_OK;
     }
     if (!b->dev_base) return set_error(DPWA_ERR_STATE, "dpwa_board_advertise: board not registered with a device");
-    HIP_TRY(hipStreamWriteValue64((hipStream_t)stream, b->dev(v), version, 0));
+    HIP_TRY(stream_store(b->dev(v), version, (hipStream_t)stream));
     return DPWA_OK;
 }
 

@@ -644,4 +644,18 @@ hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *c
     return hipGetLastError();
 }
 
+// One 64-bit word into (host-mapped) memory after everything before it on the stream: a
+// system-scope release store, so the bytes written before it are visible first.  Used by
+// the gossip board (board.cpp) for versions and read marks.
+__global__ void k_store_u64(uint64_t *p, uint64_t v)
+{
+    if (threadIdx.x == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_store_u64(uint64_t *p, uint64_t v, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_store_u64, dim3(1), dim3(64), 0, s, p, v);
+    return hipGetLastError();
+}
+
 }  // namespace dpwa

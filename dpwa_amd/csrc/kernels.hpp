@@ -76,4 +76,7 @@ hipError_t launch_relay(int phase, const RelayArgs &a, int blocks_per_part, hipS
 hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *clock, double loss,
                                  const double *loss_dev, uint64_t version, bool system_release, hipStream_t s);
 
+// A system-scope release store of one 64-bit word after the work already on `s`.
+hipError_t launch_store_u64(uint64_t *p, uint64_t v, hipStream_t s);
+
 }  // namespace dpwa
