@@ -79,7 +79,7 @@ def parse():
                          "board), or a short trial of both keeping the faster")
     ap.add_argument("--compute-us", type=float, default=1000.0,
                     help="per-learner synthetic training step (bf16 GEMM loop) for the 'overlap' field; 0 = skip")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01e.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01f.json"),
                     help="PMC traffic summary (rocprofv3 FETCH_SIZE/WRITE_SIZE passes) to report")
     return ap.parse_args()
 
