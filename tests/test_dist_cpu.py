@@ -1,4 +1,4 @@
-"""Multi-process control plane on the CPU (gloo, world size 2 and 3): every rank builds its
+"""Multi-process control plane on the CPU (gloo, world size 2, 3 and 8 -- the full-node rank count): every rank builds its
 DpwaConnection exactly as under torchrun, gets the DistGroup, maps node index <-> rank,
 and its native scheduler drives lock-step rounds whose Bernoulli draws and peer choices
 must equal the oracle's (CPython random, dpwa/conn.py:224-317).  The data path needs a
@@ -60,7 +60,7 @@ def control_worker(rank, world, port, cfg, out_dir, T):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,fp", [(2, 1.0), (3, 0.7)])
+@pytest.mark.parametrize("world,fp", [(2, 1.0), (3, 0.7), (8, 0.7)])
 def test_dist_control_plane_matches_oracle(tmp_path, world, fp):
     import json
 
