@@ -61,7 +61,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
     ap.add_argument("--no-sweep", action="store_true", help="skip the cold kernel sweep over the north_star sizes")
-    ap.add_argument("--no-write-through", action="store_true", help="skip the write-through variant")
+    ap.add_argument("--publish", choices=["write-through", "full"], default="write-through",
+                    help="how update_send publishes in the timed loop: write-through (the adapter's default: "
+                         "the averaging kernel also writes the next snapshot, the publish moves the header only) "
+                         "or full (a 2*N*s snapshot copy every round); free-running rounds always publish in full")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the run of the other publish form")
+    ap.add_argument("--no-write-through", action="store_true", help="same as --publish full --no-secondary")
     ap.add_argument("--sample-every", type=int, default=8,
                     help="time the averaging kernel every k-th step (a timed launch costs a few µs)")
     ap.add_argument("--timing", choices=["dispatch", "bracket", "both"], default="dispatch",
@@ -79,9 +84,14 @@ def parse():
                          "board), or a short trial of both keeping the faster")
     ap.add_argument("--compute-us", type=float, default=1000.0,
                     help="per-learner synthetic training step (bf16 GEMM loop) for the 'overlap' field; 0 = skip")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the parity leg (a short gossip through every transport, checked against the oracle)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01f.json"),
                     help="PMC traffic summary (rocprofv3 FETCH_SIZE/WRITE_SIZE passes) to report")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.no_write_through:
+        args.publish, args.no_secondary = "full", True
+    return args
 
 
 def write_config(path, names, interp, fetch_probability=1.0, divergence_threshold=0.0):
@@ -145,45 +155,225 @@ def cpu_baseline(numel, seconds):
     return out
 
 
-def cold_kernel(numel, dtype, device, launches=64):
-    """The fused average kernel alone over rotating buffers (> 1 GiB between reuses, so no
-    Infinity-Cache hits), launched back to back; one event pair around the whole batch."""
+# ---------------------------------------------------------------- parity leg (checker)
+# After the timed region: a short deterministic gossip through every transport the run
+# used, checked bit for bit against the oracle (oracle/ is imported only here and by the
+# cpu_baseline leg, as the checker -- never on the measured path).
+PARITY_N, PARITY_T, PARITY_FP = 1_000_003, 12, 0.7
+PARITY_ASYNC_T = 16
+
+
+def parity_init(g, n):
+    return np.random.default_rng([31, g]).standard_normal(n).astype(np.float32)
+
+
+def parity_delta(g, r, n):
+    return (0.01 * np.random.default_rng([32, r, g]).standard_normal(n)).astype(np.float32)
+
+
+def parity_loss(g, r, wait):
+    x = 2.0 * float(np.exp(-r / 4.0)) + 0.01 * g + 0.003
+    return 0.95 * x if wait else x
+
+
+def parity_lockstep(names, mine, cfg, group, pull, device, n=PARITY_N, T=PARITY_T):
+    """T lock-step rounds (clock interpolation, fetch_probability PARITY_FP) of the learners
+    `mine` = [(name, g)] through the drop-in API: the training step adds a seeded delta; two
+    of three rounds average with the fused kernel and write-through snapshots (the adapter's
+    default), every third through the split update_wait + average.  Returns per learner g the
+    per-round (sha1 of the parameters, clock, peer averaged with)."""
+    import hashlib
+    from dpwa_amd import DpwaConnection
+    conns, flats = [], []
+    for name, g in mine:
+        conns.append(DpwaConnection(name, cfg, seed=900 + g, group=group, pull=pull))
+        flats.append(torch.from_numpy(parity_init(g, n)).to(device))
+    rec = {g: [] for _, g in mine}
+    for r in range(T):
+        wt_prev = r % 3 != 0        # the previous round averaged write-through (r % 3 == 2 is split)
+        for conn, flat, (_, g) in zip(conns, flats, mine):
+            conn.update_send(flat, parity_loss(g, r, False), reuse_snapshot=wt_prev and r > 0)
+        for flat, (_, g) in zip(flats, mine):
+            flat.add_(torch.from_numpy(parity_delta(g, r, n)).to(device))
+        got = []
+        for conn, flat, (_, g) in zip(conns, flats, mine):
+            if r % 3 == 2:
+                payload, factor = conn.update_wait(parity_loss(g, r, True))
+                if payload is not None:
+                    conn.average(flat)
+            else:
+                payload, _ = conn.update_wait_average(flat, parity_loss(g, r, True), write_through=True)
+            got.append(payload.peer if payload is not None else "")
+        for conn, flat, (_, g), peer in zip(conns, flats, mine, got):
+            rec[g].append((hashlib.sha1(flat.cpu().numpy().tobytes()).hexdigest(), conn.clock, peer))
+    torch.cuda.synchronize()
+    return conns, rec
+
+
+def parity_lockstep_expected(names, n=PARITY_N, T=PARITY_T):
+    """The oracle's trajectory of parity_lockstep (oracle/gossip.py, pinned to the reference)."""
+    import hashlib
+    from oracle import gossip as ogossip
+    G = len(names)
+    init = np.stack([parity_init(g, n) for g in range(G)])
+    deltas = np.stack([np.stack([parity_delta(g, r, n) for g in range(G)]) for r in range(T)])
+    send = [[parity_loss(g, r, False) for g in range(G)] for r in range(T)]
+    wait = [[parity_loss(g, r, True) for g in range(G)] for r in range(T)]
+    exp = ogossip.simulate(names, init, deltas, send, wait, "clock", None, 0.0, PARITY_FP,
+                           [900 + g for g in range(G)])
+    return {g: [(hashlib.sha1(exp["params"][r, g].tobytes()).hexdigest(), float(exp["clocks"][r, g]),
+                 (exp["picks"][r][g][-1] if exp["picks"][r][g] else ""))
+                for r in range(T)] for g in range(G)}
+
+
+def parity_async(names, rank, cfg, pull, device, n=PARITY_N, T=PARITY_ASYNC_T):
+    """Free-running rounds over the gossip board (AsyncDistGroup): each round publishes the
+    checker's known parameters for (rank, round), runs an uneven synthetic step and averages
+    with whatever version the board hands out.  Returns (conn, params, clocks, peers, versions)."""
+    from dpwa_amd import DpwaConnection
+    from oracle.async_check import async_base, async_loss
+    conn = DpwaConnection(names[rank], cfg, seed=700 + rank, group="async", pull=pull)
+    rng = np.random.default_rng(rank)
+    flat = torch.empty(n, device=device, dtype=torch.float32)
+    bases = [torch.from_numpy(async_base(rank, r, n)).to(device) for r in range(T)]
+    params, clocks, peers, versions = np.zeros((T, n), np.float32), np.zeros(T), [], []
+    for r in range(T):
+        flat.copy_(bases[r])
+        conn.update_send(flat, async_loss(rank, r))
+        torch.cuda._sleep(int(rng.integers(0, 200_000)))       # uneven "training steps"
+        payload, _ = conn.update_wait_average(flat, async_loss(rank, r, wait=True))
+        peers.append(payload.peer if payload is not None else "")
+        versions.append(conn._info()[2] if payload is not None else 0)
+        params[r] = flat.cpu().numpy()
+        clocks[r] = conn.clock
+    torch.cuda.synchronize()
+    return conn, params, clocks, peers, versions
+
+
+def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backend):
+    """Runs the parity workload through `transports` and returns {transport: bool} on every
+    rank (rank 0 compares the lock-step digests with the oracle; each rank checks its own
+    free-running rounds)."""
+    names = ["w%d" % (g + 1) for g in range(max(world, 2))]
+    cfg = os.path.join(cfg_dir, "parity.yaml")
+    write_config(cfg, names, "clock", PARITY_FP, 0.0)
+    result = {}
+    expected = parity_lockstep_expected(names) if rank == 0 else None
+    for t in transports:
+        kind, _, pull = t.partition("/")
+        if kind == "local":                   # one GPU: both learners in this process
+            from dpwa_amd.group import LocalGroup
+            conns, rec = parity_lockstep(names, [(names[0], 0), (names[1], 1)], cfg, LocalGroup(), None, device)
+            result[t] = rec == expected
+        elif kind == "lockstep":
+            conns, rec = parity_lockstep(names, [(names[rank], rank)], cfg, "lockstep", pull, device)
+            got = [None] * world
+            dist.all_gather_object(got, rec[rank])
+            ok = torch.tensor([1 if rank != 0 or all(got[g] == expected[g] for g in range(world)) else 0],
+                              dtype=torch.int32, device=device if dist_backend == "nccl" else "cpu")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            result[t] = bool(ok.item())
+        else:                                  # async: free-running over the gossip board
+            from oracle.async_check import AsyncRuns
+            conn, params, clocks, peers, versions = parity_async(names, rank, cfg, pull, device)
+            conns = [conn]
+            got = [None] * world
+            dist.all_gather_object(got, (peers, versions))
+            check = AsyncRuns(names, {g: got[g][0] for g in range(world)}, {g: got[g][1] for g in range(world)},
+                              "clock", None, 0.0)
+            bad = check.check_rank(rank, params, clocks, PARITY_N)
+            if bad:
+                print("parity %s rank %d: %s" % (t, rank, bad[:3]), file=sys.stderr, flush=True)
+            ok = torch.tensor([0 if bad else 1], dtype=torch.int32,
+                              device=device if dist_backend == "nccl" else "cpu")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            result[t] = bool(ok.item())
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        for c in conns:
+            c.close()
+        if world > 1:
+            dist.barrier()
+    return result
+
+
+def cold_kernel(numel, dtype, device, write_through=False, launches=64):
+    """The product averaging kernel (dpwa_average: k_lerp<Ops, COEF_FUSED, write_through> -- fp64
+    device factor + lerp in place, and with write_through the result also stored into a
+    snapshot payload) alone, over rotating buffers (> 1.2 GB of other traffic between
+    two uses of a buffer, so nothing is served from the 256 MiB Infinity Cache).  Every launch
+    is timed by its own dispatch begin/end events (hipExtLaunchKernelGGL), as rocprofv3 times
+    a kernel: the inter-kernel gaps of a back-to-back batch are not counted.  Also returns the
+    rate of one event pair around the whole batch (which does include the gaps)."""
     from dpwa_amd import _lib
     esize = 4 if dtype == torch.float32 else 2
-    pairs = max(2, int(np.ceil(1.2e9 / (2 * numel * esize))))
+    nbuf = 3 if write_through else 2
+    pairs = max(2, int(np.ceil(1.2e9 / (nbuf * numel * esize))))
     launches = max(2 * pairs, min(launches, int(np.ceil(64 * 134e6 / (3 * numel * esize)))))
-    bufs = [(torch.empty(numel, device=device, dtype=dtype).normal_(),
-             torch.empty(numel, device=device, dtype=dtype).normal_()) for _ in range(pairs)]
-    fn = "dpwa_lerp_f32_host" if dtype == torch.float32 else "dpwa_lerp_bf16_host"
+    hdr = 256 // esize
+    params, slots, snaps = [], [], []
+    for _ in range(pairs):
+        params.append(torch.empty(numel, device=device, dtype=dtype).normal_())
+        slot = torch.zeros(hdr + numel, device=device, dtype=dtype)     # 256-B header (zeros) + payload
+        slot[hdr:].normal_()
+        slots.append(slot)
+        snaps.append(torch.empty(numel, device=device, dtype=dtype) if write_through else None)
+    clock = torch.zeros(2, device=device, dtype=torch.float64)
+    coef = torch.zeros(4, device=device, dtype=torch.float64)           # dpwa_coef, 32 B
+    cfg = _lib.Interp(_lib.INTERP_CONSTANT, 0, 0.5, 0.0)
+    dt = _lib.F32 if dtype == torch.float32 else _lib.BF16
     s = _lib.stream_handle(None)
-    f = getattr(_lib.load(), fn)
+    f = _lib.load().dpwa_average
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    for a, b in ev:          # create the events (the kernel dispatch then records into them)
+        a.record()
+        b.record()
 
-    def run(i):
-        p, q = bufs[i % pairs]
-        f(p.data_ptr(), q.data_ptr(), numel, 0.5, s)
+    def run(i, timed):
+        a, b = ev[i] if timed else (None, None)
+        snap = snaps[i % pairs]
+        rc = f(dt, params[i % pairs].data_ptr(), slots[i % pairs].data_ptr(), numel, ctypes.byref(cfg),
+               clock.data_ptr(), 1.0, coef.data_ptr(), snap.data_ptr() if snap is not None else None, s,
+               a.cuda_event if timed else None, b.cuda_event if timed else None)
+        if rc:
+            raise _lib.DpwaError("dpwa_average", rc, _lib.load().dpwa_last_error().decode())
 
     for i in range(pairs):
-        run(i)
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        run(i, False)
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda._sleep(50_000_000)          # let the host queue the whole batch first
-    a.record()
+    t0.record()
     for i in range(launches):
-        run(i)
-    b.record()
+        run(i, True)
+    t1.record()
     torch.cuda.synchronize()
-    us = a.elapsed_time(b) * 1e3 / launches
-    del bufs
+    us = np.array([a.elapsed_time(b) * 1e3 for a, b in ev])
+    batch_us = t0.elapsed_time(t1) * 1e3 / launches
+    del params, slots, snaps
     torch.cuda.empty_cache()
-    return 3 * numel * esize / (us * 1e-6) / 1e9, us, pairs
+    return {"avg_launch_us": float(us.mean()), "median_launch_us": float(np.median(us)),
+            "min_launch_us": float(us.min()), "max_launch_us": float(us.max()), "launches": launches,
+            "rotating_buffer_pairs": pairs, "batch_bracket_us": float(batch_us)}
 
 
 def size_sweep(device):
-    """The averaging kernel, cold, at every north_star size (11.17M/100M fp32, 1B/7B bf16)."""
+    """The averaging kernel, cold, per launch, at every north_star size (11.17M/100M fp32,
+    1B/7B bf16), in both publish forms: plain (3*N*s bytes per launch) and write-through
+    (4*N*s: the next snapshot is written by the same pass)."""
     rows = []
     for numel, dt in SWEEP:
-        gbs, us, pairs = cold_kernel(numel, torch.float32 if dt == "f32" else torch.bfloat16, device)
-        rows.append({"numel": numel, "dtype": dt, "avg_launch_us": round(us, 2), "achieved": round(gbs, 1),
-                     "frac": round(gbs / HBM_PEAK_GBS, 4), "rotating_buffer_pairs": pairs})
+        esize = 4 if dt == "f32" else 2
+        for wt in (False, True):
+            c = cold_kernel(numel, torch.float32 if dt == "f32" else torch.bfloat16, device, wt)
+            nbytes = (4 if wt else 3) * numel * esize
+            gbs = nbytes / (c["avg_launch_us"] * 1e-6) / 1e9
+            rows.append({"numel": numel, "dtype": dt, "publish": "write-through" if wt else "full",
+                         "bytes_per_launch": nbytes, "avg_launch_us": round(c["avg_launch_us"], 2),
+                         "median_launch_us": round(c["median_launch_us"], 2), "achieved": round(gbs, 1),
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "launches": c["launches"],
+                         "rotating_buffer_sets": c["rotating_buffer_pairs"],
+                         "batch_bracket_us": round(c["batch_bracket_us"], 2)})
     return rows
 
 
@@ -358,12 +548,12 @@ def main():
             loss_t[0] += 1
             if gossip:
                 for i, (conn, flat) in enumerate(learners):
-                    conn.update_send(flat, losses[i])
+                    conn.update_send(flat, losses[i], reuse_snapshot=wt_main)
             for _ in learners:
                 compute()
             if gossip:
                 for i, (conn, flat) in enumerate(learners):
-                    payload, _ = conn.update_wait_average(flat, losses[i])
+                    payload, _ = conn.update_wait_average(flat, losses[i], write_through=wt_main)
                     done += payload is not None
             return done
 
@@ -392,6 +582,7 @@ def main():
 
     pull_trials = {}
     pull = args.pull
+    wt_lockstep = args.publish == "write-through"     # free-running rounds always publish in full
     lockstep_learners = list(learners)
     async_learners = []
     if world > 1:
@@ -402,7 +593,7 @@ def main():
         if args.gossip != "async":
             for mode in modes:       # short timed trial of each transport; the fastest is used below
                 set_pull(mode)
-                el, av, _, _ = run(trial_steps, 2, False, 1000)
+                el, av, _, _ = run(trial_steps, 2, wt_lockstep, 1000)
                 pull_trials[mode] = round(av * 3 * args.numel * esize / el / 1e9, 2)
         if args.gossip != "lockstep":
             # free-running rounds over the gossip board, same learners' parameters (a second
@@ -428,14 +619,15 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
             set_pull(pull)
-    elapsed, averaged, rounds, (lerp_ms, bracket_ms) = run(args.steps, args.warmup, False, args.sample_every)
+    wt_main = wt_lockstep and not pull.startswith("async/")
+    elapsed, averaged, rounds, (lerp_ms, bracket_ms) = run(args.steps, args.warmup, wt_main, args.sample_every)
     pull_us = []
     if world > 1 and not pull.split("/")[-1].startswith("relay"):
         # the pull alone (side-stream events around each copying fetch), in a short extra run
         p_steps = max(20, args.steps // 4)
         for conn, _ in learners:
             _lib.call("dpwa_learner_time_fetches", conn._learner.handle, p_steps + 4)
-        run(p_steps, 2, False, 1000)
+        run(p_steps, 2, wt_main, 1000)
         for conn, _ in learners:
             buf = (ctypes.c_float * (p_steps + 4))()
             cnt = ctypes.c_int()
@@ -446,11 +638,13 @@ def main():
                          device=device if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         pull_us = [float(t.item()) / world]
-    wt = None
-    if not args.no_write_through and (world == 1 or args.gossip != "async"):
+    secondary = None
+    if not args.no_secondary and (not wt_main or world == 1 or args.gossip != "async"):
+        # the other publish form, for comparison (write-through snapshots need lock-step rounds)
         chosen = list(learners)
-        learners[:] = lockstep_learners     # write-through snapshots need lock-step rounds
-        wt = run(args.steps, args.warmup, True, args.sample_every)
+        if not wt_main:
+            learners[:] = lockstep_learners
+        secondary = (not wt_main, run(args.steps, args.warmup, not wt_main, args.sample_every))
         learners[:] = chosen
     overlap = None
     if args.compute_us > 0:
@@ -487,17 +681,42 @@ def main():
         if o_trials:
             overlap["trials_ms_per_step"] = {m: round(1e3 * t / o_steps, 4) for m, t in o_trials.items()}
 
+    parity = None
+    if not args.no_parity:
+        if world == 1:
+            transports = ["local"]
+        else:
+            transports = []
+            if args.gossip != "async":
+                transports += ["lockstep/copy", "lockstep/kernel:256", "lockstep/relay:32"]
+            if args.gossip != "lockstep":
+                transports += ["async/copy", "async/kernel:256"]
+        parity = parity_leg(world, rank, local_rank, device, tmp, transports, args.dist_backend)
+        parity["workload"] = ("%d-element fp32 vector per learner, %d lock-step rounds (clock interpolation, "
+                              "fetch_probability %g, seeded training-step deltas, write-through and split rounds "
+                              "mixed), %d free-running rounds over the gossip board; every learner's parameters, "
+                              "clocks and peers compared bit for bit with oracle/gossip.py (lock-step) and "
+                              "oracle/async_check.py (per version read)"
+                              % (PARITY_N, PARITY_T, PARITY_FP, PARITY_ASYNC_T))
+
     unit_bytes = 3 * args.numel * esize
+    kbytes = (4 if wt_main else 3) * args.numel * esize     # the timed loop's averaging kernel, per launch
+    # the same kernel alone, cold (rotating buffers, per-launch dispatch events): the roofline's basis
+    cold = cold_kernel(args.numel, dtype, device, wt_main) if not args.no_cold else None
     if rank == 0:
         value = averaged * unit_bytes / elapsed / 1e9
         lerp_us = float(np.nanmean(lerp_ms) * 1e3)
-        achieved = unit_bytes / (lerp_us * 1e-6) / 1e9
+        live_gbs = kbytes / (lerp_us * 1e-6) / 1e9
+        k_us = cold["avg_launch_us"] if cold else lerp_us
+        achieved = kbytes / (k_us * 1e-6) / 1e9
+        variant = "write-through" if wt_main else "full"
         traffic = None
         traffic_src = None
         if os.path.exists(args.traffic):
             with open(args.traffic) as f:
                 tr = json.load(f)
-            if tr.get("numel") == args.numel and tr.get("dtype") == args.dtype and tr.get("gpus", 1) == world:
+            if (tr.get("numel") == args.numel and tr.get("dtype") == args.dtype and
+                    tr.get("publish", "full") == variant and tr.get("basis", "in-loop") == ("cold" if cold else "in-loop")):
                 traffic = tr.get("hbm_bytes_per_launch")
                 traffic_src = os.path.relpath(args.traffic, ROOT)
         out = {
@@ -515,13 +734,15 @@ def main():
             "data": "synthetic N(0,1) flat parameter vectors (no dataset needed)",
             "config": {
                 "workload": ("%ssynthetic %d-element %s vector per learner%s, %s interpolation, "
-                             "fetch_probability %g, divergence_threshold %g, %s loss, lock-step gossip rounds"
+                             "fetch_probability %g, divergence_threshold %g, %s loss, %s gossip rounds, %s publish"
                              % ("configs[1]: " if args.numel == RESNET18_NUMEL else "", args.numel, args.dtype,
                                 " (ResNet-18 size)" if args.numel == RESNET18_NUMEL else "", args.interpolation,
-                                args.fetch_probability, args.divergence_threshold, args.loss_schedule)),
+                                args.fetch_probability, args.divergence_threshold, args.loss_schedule,
+                                "free-running" if pull.startswith("async/") else "lock-step", variant)),
                 "learners": int(rounds / args.steps),
                 "learners_per_gpu": len(learners),
                 "numel": args.numel,
+                "publish": variant,
                 "transport": "in-place HBM read (co-resident peer)" if world == 1 else
                              "hipIpc-mapped slot pulled over xGMI on a side stream (%s, %s rounds)"
                              % (pull.split("/")[-1], "free-running" if pull.startswith("async/") else "lock-step"),
@@ -538,16 +759,34 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "dpwa::k_lerp<Ops%s, COEF_FUSED> (fused factor + lerp)" % args.dtype.upper(),
-                "bytes_per_launch": unit_bytes,
-                "avg_launch_us": round(lerp_us, 2),
-                "launches_timed": int(np.isfinite(lerp_ms).sum()),
-                "timing": ("kernel dispatch begin/end events (hipExtLaunchKernelGGL) on the averaging "
-                           "kernel's own stream" if args.timing != "bracket" else
-                           "HIP event pair recorded around the launch on its stream")
-                          + ", every %d-th step" % args.sample_every,
-                "event_bracket_us": (round(float(np.nanmean(bracket_ms) * 1e3), 2)
-                                     if args.timing != "dispatch" else None),
+                "kernel": "dpwa::k_lerp<Ops%s, COEF_FUSED, %s> (fused device factor + lerp%s)"
+                          % (args.dtype.upper(), "true" if wt_main else "false",
+                             " + write-through of the next snapshot" if wt_main else ""),
+                "bytes_per_launch": kbytes,
+                "bytes_note": ("4*N*s: read parameters, read peer snapshot, write parameters, write the next "
+                               "snapshot (which the publish then does not copy)" if wt_main else
+                               "3*N*s: read parameters, read peer snapshot, write parameters"),
+                "avg_launch_us": round(k_us, 2),
+                "basis": ("cold: the kernel alone over rotating buffers (> 1.2 GB between reuses, no "
+                          "Infinity-Cache hits), every launch timed by its own dispatch begin/end events "
+                          "(hipExtLaunchKernelGGL), mean over %d launches" % cold["launches"]) if cold else
+                         "in-loop (--no-cold)",
+                "cold": ({k: (round(v, 2) if isinstance(v, float) else v) for k, v in cold.items()}
+                         if cold else None),
+                "in_loop": {
+                    "achieved": round(live_gbs, 1),
+                    "frac": round(live_gbs / HBM_PEAK_GBS, 4),
+                    "avg_launch_us": round(lerp_us, 2),
+                    "launches_timed": int(np.isfinite(lerp_ms).sum()),
+                    "timing": ("kernel dispatch begin/end events (hipExtLaunchKernelGGL) on the averaging "
+                               "kernel's own stream" if args.timing != "bracket" else
+                               "HIP event pair recorded around the launch on its stream")
+                              + ", every %d-th step of the timed loop" % args.sample_every,
+                    "event_bracket_us": (round(float(np.nanmean(bracket_ms) * 1e3), 2)
+                                         if args.timing != "dispatch" else None),
+                    "note": "inside the gossip round the peer snapshot was written just before the average and "
+                            "is partly Infinity-Cache resident, so this live figure is warmer than the basis",
+                },
                 "traffic_source": traffic_src,
             },
         }
@@ -565,34 +804,40 @@ def main():
                         "side-stream events around each copying fetch (mean over ranks; null for the relay); "
                         "peak = MI355X xGMI spec per link, both directions together",
             }
-        if wt is not None:
-            w_el, w_avg, w_rounds, (w_ms, _) = wt
+        if secondary is not None:
+            s_wt, (w_el, w_avg, w_rounds, (w_ms, _)) = secondary
             w_us = float(np.nanmean(w_ms) * 1e3)
-            out["write_through"] = {
+            w_bytes = (4 if s_wt else 3) * args.numel * esize
+            out["secondary_publish"] = {
+                "publish": "write-through" if s_wt else "full",
                 "value": round(w_avg * unit_bytes / w_el / 1e9, 2),
                 "ms_per_step": round(1e3 * w_el / args.steps, 4),
-                "note": "update_wait_average(write_through=True) + update_send(reuse_snapshot=True): the "
-                        "averaging kernel also writes the next snapshot (4*N*s bytes), the publish moves only "
-                        "the 256-B header; valid when nothing modifies the parameters between update_wait and "
-                        "the next update_send (the README loop)",
                 "avg_launch_us": round(w_us, 2),
-                "kernel_gbs_4ns": round(4 * args.numel * esize / (w_us * 1e-6) / 1e9, 1),
+                "kernel_gbs": round(w_bytes / (w_us * 1e-6) / 1e9, 1),
+                "note": "the same rounds with the other publish form. write-through: the averaging kernel also "
+                        "writes the next snapshot (4*N*s) and the publish moves only the 256-B header; full: "
+                        "every publish copies the 2*N*s snapshot. Write-through is valid when nothing modifies "
+                        "the parameters between update_wait and the next update_send (the reference's loop, "
+                        "examples/pytorch-cifar/main.py:130-145); the adapter checks the parameters' version "
+                        "counters and storage before reusing a snapshot",
             }
         if overlap is not None:
             out["overlap"] = overlap
-        if world == 1 and not args.no_cold:
-            gbs, us, pairs = cold_kernel(args.numel, dtype, device)
-            out["roofline"]["cold_cache"] = {"achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                             "avg_launch_us": round(us, 2), "rotating_buffer_pairs": pairs}
         if world == 1 and not args.no_sweep:
             out["roofline"]["size_sweep"] = size_sweep(device)
         out["cpu_baseline"] = cpu
+        if parity is not None:
+            out["parity"] = parity
         print(json.dumps(out), flush=True)
     for conn, _ in lockstep_learners + async_learners:
         conn.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if parity is not None and not all(v for k, v in parity.items() if k != "workload"):
+        print("bench.py: parity check FAILED: %s" % {k: v for k, v in parity.items() if k != "workload"},
+              file=sys.stderr, flush=True)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -77,6 +77,9 @@ SIGNATURES = {
     "dpwa_lerp_f32_host": [_vp, _vp, _i64, _dbl, _vp],
     "dpwa_lerp_bf16_host": [_vp, _vp, _i64, _dbl, _vp],
     "dpwa_factor": [ctypes.POINTER(Interp), _vp, _vp, _dbl, _vp, _vp, _vp],
+    "dpwa_average": [_i32, _vp, _vp, _i64, ctypes.POINTER(Interp), _vp, _dbl, _vp, _vp, _vp, _vp, _vp],
+    "dpwa_learner_copy_factor": [_vp, _vp, _vp],
+    "dpwa_learner_copy_fetched": [_vp, _vp, _vp],
     "dpwa_learner_create": [ctypes.POINTER(_vp), _int, _i64, _i32, ctypes.POINTER(Interp)],
     "dpwa_learner_destroy": [_vp],
     "dpwa_learner_publish": [_vp, _vp, _dbl, _vp, _vp],
@@ -147,6 +150,7 @@ SIGNATURES = {
     "dpwa_sched_fetch": [_vp, ctypes.POINTER(_i32), _int, _pint, _pint],
     "dpwa_sched_score": [_vp, _int, _pint],
     "dpwa_sched_remove": [_vp, _int],
+    "dpwa_sched_add": [_vp, _int],
     "dpwa_sched_n_live": [_vp, _pint],
     "dpwa_sched_random": [_vp, ctypes.POINTER(_dbl)],
     "dpwa_sched_randint": [_vp, _i64, _i64, ctypes.POINTER(_i64)],

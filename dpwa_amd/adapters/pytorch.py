@@ -19,15 +19,19 @@ LOGGER = logging.getLogger(__name__)
 
 
 class DpwaPyTorchAdapter:
-    """write_through (extension, default off): the averaging kernel also writes the next
-    snapshot, and the next update_send publishes only the header when no parameter was
-    modified in between.  Modifications through autograd-visible in-place ops (optimizers,
-    ``param.add_``) are detected from the parameters' version counters and force a full
-    publish; writes through ``param.data`` are invisible to that check, so enable this only
-    for loops that do not touch ``.data`` between update_wait and update_send (the README
-    loop and the reference's example trainer do not)."""
+    """write_through (extension, default on): the averaging kernel also writes the next
+    snapshot, and the next update_send publishes only the header when nothing was modified in
+    between -- 4*N*s bytes for the averaging and the publish instead of 5*N*s.  The reference
+    loop never touches the parameters between update_wait and the next update_send (README.md
+    and examples/pytorch-cifar/main.py:130-145: update_send, forward/backward/step, update_wait).
+    Before reusing a snapshot the adapter checks that no parameter was re-homed
+    (``param.data = ...``), that no parameter's version counter moved (optimizer steps,
+    ``param.add_``, ``load_state_dict``) and that the flat buffer's own counter did not move;
+    any of these forces a full publish.  In-place writes through ``param.data`` bypass version
+    counters: a loop that does that between update_wait and update_send must pass
+    ``write_through=False``.  Free-running (gossip-board) rounds always publish in full."""
 
-    def __init__(self, net, name, config_file, write_through=False, transport="device", **connection_kwargs):
+    def __init__(self, net, name, config_file, write_through=True, transport="device", **connection_kwargs):
         """transport: "device" (peers are learners of this process or of the torch.distributed
         job, pulled from HBM/over xGMI) or "wire" (peers are reached over TCP at the YAML's
         host/port with the reference's protocol -- e.g. reference CPU nodes; dpwa_amd/bridge.py)."""
@@ -41,11 +45,13 @@ class DpwaPyTorchAdapter:
             self._conn = DpwaConnection(name, config_file, **connection_kwargs)
         else:
             raise ValueError("transport must be 'device' or 'wire'")
-        self._write_through = write_through
+        from ..group import AsyncDistGroup
+        self._write_through = bool(write_through) and transport == "device" and \
+            not isinstance(getattr(self._conn, "_group", None), AsyncDistGroup)
         self._versions = None
 
     def _param_versions(self):
-        return [p._version for p in self._flat.params]
+        return [p._version for p in self._flat.params] + [self._flat.buffer._version]
 
     def update_send(self, loss):
         """pytorch.py:42-53: publish the parameters and maybe start a fetch."""

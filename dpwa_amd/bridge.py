@@ -253,7 +253,7 @@ class WireConnection(DpwaConnection):
 
     def update_send(self, parameters, loss, reuse_snapshot=False):
         if parameters.dtype != torch.float32:
-            raise TypeError("the wire bridge carries float32 parameters only (pytorch.py:11-14)")
+            raise KeyError("the wire bridge carries float32 parameters only (pytorch.py:11-14)")
         self._join()
         super().update_send(parameters, loss, reuse_snapshot)
         self._result = None

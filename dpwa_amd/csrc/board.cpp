@@ -26,6 +26,14 @@
 // slot) without having seen our mark, so the reader retries with the newer version; if it
 // is still v, p has not finished publishing v+1, so its check for v+2 comes later and
 // sees the mark.
+//
+// A reader clears its mark from its side stream, after the pull, while its host may already
+// be in the next round.  If the next round picks the same publisher, the new mark must not
+// be wiped by that still-queued clear of the old one (the old store of 0 would land after
+// the new mark and let the publisher rewrite the slot mid-pull).  So every stream-ordered
+// release records an event, and the next acquire of the same publisher first waits for it:
+// a reader holds at most one mark per publisher, and marks are only ever cleared by the
+// release of the acquisition that set them.
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
@@ -40,6 +48,7 @@
 #include <sys/stat.h>
 #include <thread>
 #include <unistd.h>
+#include <vector>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -93,6 +102,9 @@ struct dpwa_board {
     uint64_t *reading = nullptr;   // [publisher * world + reader]
     char *dev_base = nullptr;      // device alias of `base` once registered
     int device = -1;
+    // per publisher: the event recorded after our last stream-ordered release of its mark
+    std::vector<hipEvent_t> released;
+    std::vector<char> release_pending;
 
     uint64_t *dev(const void *host_ptr) const
     {
@@ -197,6 +209,11 @@ int dpwa_board_close(dpwa_board *b)
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(b->device);
+        for (hipEvent_t ev : b->released)
+            if (ev) {
+                (void)hipEventSynchronize(ev);
+                (void)hipEventDestroy(ev);
+            }
         (void)hipHostUnregister(b->base);
         (void)hipSetDevice(prev);
     }
@@ -219,6 +236,8 @@ int dpwa_board_register(dpwa_board *b, int device)
     if (e != hipSuccess) return set_error(DPWA_ERR_HIP, "dpwa_board_register: %s", hipGetErrorString(e));
     b->dev_base = (char *)d;
     b->device = device;
+    b->released.assign((size_t)b->world, nullptr);
+    b->release_pending.assign((size_t)b->world, 0);
     return DPWA_OK;
 }
 
@@ -250,6 +269,12 @@ int dpwa_board_acquire(dpwa_board *b, int r, uint64_t *version)
     if (!b || r < 0 || r >= b->world || r == b->rank || !version)
         return set_error(DPWA_ERR_ARG, "dpwa_board_acquire: bad arguments");
     uint64_t *mark = &b->reading[(size_t)r * b->world + b->rank];
+    if (!b->release_pending.empty() && b->release_pending[r]) {
+        // our previous mark on r is cleared by a store still queued on a stream: let it land
+        // first, or it would wipe the mark set below
+        HIP_TRY(hipEventSynchronize(b->released[r]));
+        b->release_pending[r] = 0;
+    }
     uint64_t v = load(&b->nodes[r].version);
     for (int tries = 0; tries < 1000000; ++tries) {
         if (v == 0) {
@@ -286,6 +311,16 @@ int dpwa_board_release(dpwa_board *b, int r, dpwa_stream_t stream, int host)
     }
     if (!b->dev_base) return set_error(DPWA_ERR_STATE, "dpwa_board_release: board not registered with a device");
     HIP_TRY(stream_store(b->dev(mark), 0, (hipStream_t)stream));
+    if (!b->released[r]) {
+        int prev = 0;
+        HIP_TRY(hipGetDevice(&prev));
+        HIP_TRY(hipSetDevice(b->device));
+        const hipError_t e = hipEventCreateWithFlags(&b->released[r], hipEventDisableTiming);
+        (void)hipSetDevice(prev);
+        if (e != hipSuccess) return set_error(DPWA_ERR_HIP, "dpwa_board_release: %s", hipGetErrorString(e));
+    }
+    HIP_TRY(hipEventRecord(b->released[r], (hipStream_t)stream));
+    b->release_pending[r] = 1;
     return DPWA_OK;
 }
 

@@ -228,6 +228,21 @@ int dpwa_factor(const dpwa_interp *cfg, double *clock_dev, const dpwa_header *pe
     return DPWA_OK;
 }
 
+int dpwa_average(int32_t dtype, void *param, const void *peer_slot, int64_t n, const dpwa_interp *cfg,
+                 double *clock_dev, double loss, dpwa_coef *coef_dev, void *snap_payload, dpwa_stream_t stream,
+                 void *start_event, void *stop_event)
+{
+    if (!cfg || !clock_dev || !coef_dev || !peer_slot || n < 0 || (n > 0 && !param) || dtype_size(dtype) == 0 ||
+        (!start_event) != (!stop_event))
+        return set_error(DPWA_ERR_ARG, "dpwa_average: bad arguments");
+    if (cfg->method < 0 || cfg->method > 2) return set_error(DPWA_ERR_ARG, "dpwa_average: unknown method %d", cfg->method);
+    FusedArgs fa{*cfg, clock_dev, clock_dev + 1, (const dpwa_header *)peer_slot, loss, nullptr, coef_dev, nullptr};
+    LaunchTiming t{(hipEvent_t)start_event, (hipEvent_t)stop_event};
+    HIP_TRY(launch_average(dtype, param, (const char *)peer_slot + kHeader, n, fa, snap_payload, (hipStream_t)stream,
+                           start_event ? &t : nullptr));
+    return DPWA_OK;
+}
+
 int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype, const dpwa_interp *cfg)
 {
     if (!out || n < 0 || !cfg || dtype_size(dtype) == 0) return set_error(DPWA_ERR_ARG, "dpwa_learner_create: bad arguments");
@@ -918,6 +933,29 @@ int dpwa_learner_set_pull(dpwa_learner *l, int mode, int max_blocks)
         return set_error(DPWA_ERR_ARG, "dpwa_learner_set_pull: bad arguments");
     l->pull_mode = mode;
     l->pull_blocks = max_blocks;
+    return DPWA_OK;
+}
+
+int dpwa_learner_copy_factor(dpwa_learner *l, double *dst_dev, dpwa_stream_t stream)
+{
+    if (!l || !dst_dev) return set_error(DPWA_ERR_ARG, "dpwa_learner_copy_factor: NULL argument");
+    DeviceGuard dg(l->device);
+    HIP_TRY(hipMemcpyAsync(dst_dev, &l->ctl->coef.factor, sizeof(double), hipMemcpyDeviceToDevice,
+                           (hipStream_t)stream));
+    return DPWA_OK;
+}
+
+int dpwa_learner_copy_fetched(dpwa_learner *l, void *dst_dev, dpwa_stream_t stream)
+{
+    if (!l || (!dst_dev && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_copy_fetched: NULL argument");
+    if (!l->have_fetch || !l->src) return set_error(DPWA_ERR_STATE, "dpwa_learner_copy_fetched: no fetch in flight");
+    DeviceGuard dg(l->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));
+    if (l->payload_bytes)
+        HIP_TRY(hipMemcpyAsync(dst_dev, l->src + kHeader, l->payload_bytes, hipMemcpyDeviceToDevice, s));
+    l->consume_stream = s;   // the staging buffer / peer slot is read on s
+    l->consumed_once = true;
     return DPWA_OK;
 }
 

@@ -48,6 +48,10 @@ struct dpwa_node {
 
 using namespace dpwa;
 
+// TxThread's loop ends only on data, on "no peer" or when every peer is gone (conn.py:286-313);
+// with every live peer answering empty it would spin for ever: bounded here.
+constexpr int kMaxFetchAttempts = 100000;
+
 static uint64_t learner_version(dpwa_learner *l)
 {
     uint64_t v = 0;
@@ -148,6 +152,56 @@ static int32_t peer_status(const dpwa_node *n, size_t k)
     return DPWA_PEER_READY;
 }
 
+// Free-running rounds: TxThread's loop (conn.py:277-315, as dpwa_sched_fetch runs it) with
+// the board standing in for the peers' RxThreads.  A READY peer's snapshot is acquired
+// *before* the outcome is reported, so a peer that closed between its status read and the
+// acquire counts as gone -- refused when not yet connected (conn.py:253-256), an error when
+// it was (conn.py:311-313) -- and never as a reply with data.
+static int board_fetch(dpwa_node *n, int flags, int *peer_out, uint64_t *version_out, int *attempts_out)
+{
+    *peer_out = -1;
+    *version_out = 0;
+    int attempts = 0;
+    while (attempts < kMaxFetchAttempts) {
+        int peer, connected, done = 0, data = 0;
+        int rc = dpwa_sched_pick(n->sched, &peer, &connected);
+        if (rc) return rc;
+        if (peer < 0) break;
+        attempts++;
+        int32_t st = n->status[peer];
+        uint64_t v = 0;
+        if (st == DPWA_PEER_READY && n->peers[peer].kind == PEER_REMOTE) {
+            if (flags & DPWA_FLAG_PICK_ONLY)
+                return set_error(DPWA_ERR_STATE, "the relay transport needs lock-step rounds, not a board");
+            if ((rc = dpwa_board_acquire(n->board, n->board_rank[peer], &v))) return rc;
+            if (v == 0) st = DPWA_PEER_DOWN;      // closed since its status was read
+        }
+        if (!connected) {
+            int c = DPWA_CONNECT_OK;
+            if (st == DPWA_PEER_DOWN) c = DPWA_CONNECT_REFUSED;
+            else if (st == DPWA_PEER_DEAD) c = DPWA_CONNECT_ERROR;
+            if ((rc = dpwa_sched_report(n->sched, peer, c, &done, &data))) return rc;
+            if (done) break;
+        }
+        int r;
+        switch (st) {
+        case DPWA_PEER_READY: r = DPWA_REPLY_PAYLOAD; break;
+        case DPWA_PEER_NO_STATE: r = DPWA_REPLY_EMPTY; break;
+        case DPWA_PEER_SLOW: r = DPWA_REPLY_TIMEOUT; break;
+        default: r = DPWA_REPLY_ERROR; break;
+        }
+        if ((rc = dpwa_sched_report(n->sched, peer, r, &done, &data))) return rc;
+        if (data) {
+            *peer_out = peer;
+            *version_out = v;
+            break;
+        }
+        if (done) break;
+    }
+    *attempts_out = attempts;
+    return DPWA_OK;
+}
+
 static int start_fetch(dpwa_node *n, int flags, dpwa_stream_t stream)
 {
     int zero_copy = (flags & DPWA_FLAG_ZERO_COPY) ? 1 : 0;
@@ -155,26 +209,14 @@ static int start_fetch(dpwa_node *n, int flags, dpwa_stream_t stream)
     n->fetch_peer = -1;
     for (size_t k = 0; k < n->peers.size(); ++k) n->status[k] = peer_status(n, k);
     int peer = -1, attempts = 0;
-    int rc = dpwa_sched_fetch(n->sched, n->status.data(), 100000, &peer, &attempts);
-    if (rc) return rc;
-    n->last_attempts = attempts;
-    if (peer < 0) return DPWA_OK;
-    PeerRef &p = n->peers[peer];
-    uint64_t version;
-    if (p.kind == PEER_LOCAL) {
-        dpwa_learner *pl = p.node->learner;
-        if (n->attached_to[peer] != pl) {
-            if ((rc = dpwa_learner_attach_local(n->learner, peer, pl))) return rc;
-            n->attached_to[peer] = pl;
-        }
-        version = learner_version(pl);
-    } else if (n->board) {
+    int rc;
+    if (n->board) {
         // free-running: the newest complete publish, held against rewrite until our pull lands
-        if (flags & DPWA_FLAG_PICK_ONLY)
-            return set_error(DPWA_ERR_STATE, "the relay transport needs lock-step rounds, not a board");
+        uint64_t version = 0;
+        if ((rc = board_fetch(n, flags, &peer, &version, &attempts))) return rc;
+        n->last_attempts = attempts;
+        if (peer < 0) return DPWA_OK;
         const int r = n->board_rank[peer];
-        if ((rc = dpwa_board_acquire(n->board, r, &version))) return rc;
-        if (version == 0) return DPWA_OK;   // closed between the pick and now: no data
         if ((rc = dpwa_learner_fetch(n->learner, peer, version, 0, stream))) {
             dpwa_board_release(n->board, r, nullptr, 1);
             return rc;
@@ -186,6 +228,19 @@ static int start_fetch(dpwa_node *n, int flags, dpwa_stream_t stream)
         n->fetch_peer = peer;
         n->fetch_version = version;
         return DPWA_OK;
+    }
+    if ((rc = dpwa_sched_fetch(n->sched, n->status.data(), kMaxFetchAttempts, &peer, &attempts))) return rc;
+    n->last_attempts = attempts;
+    if (peer < 0) return DPWA_OK;
+    PeerRef &p = n->peers[peer];
+    uint64_t version;
+    if (p.kind == PEER_LOCAL) {
+        dpwa_learner *pl = p.node->learner;
+        if (n->attached_to[peer] != pl) {
+            if ((rc = dpwa_learner_attach_local(n->learner, peer, pl))) return rc;
+            n->attached_to[peer] = pl;
+        }
+        version = learner_version(pl);
     } else {
         version = learner_version(n->learner);   // lock-step: every node publishes once per round
         zero_copy = 0;

@@ -3,6 +3,7 @@
 // (dpwa/dpwa.py:101-102, 118-123), driven by an MT19937 that reproduces CPython 3.10's
 // `random` module draw for draw (Modules/_randommodule.c + Lib/random.py), so a learner
 // seeded like `random.seed(seed)` picks exactly the peers the reference picks.
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <new>
@@ -133,7 +134,9 @@ struct PeerEntry {
 struct dpwa_sched {
     dpwa::PyMT rng;
     double fetch_probability = 1.0;
-    std::vector<dpwa::PeerEntry> peers;   // insertion order == YAML order minus self
+    std::vector<dpwa::PeerEntry> peers;   // indexed by peer id (YAML order minus self)
+    std::vector<int> order;               // live peers in TxThread.peers' dict order: YAML order,
+                                          // removals dropped, re-added peers at the end
     std::vector<int64_t> draw;            // scratch: scores of this pick
 };
 
@@ -158,6 +161,7 @@ int dpwa_sched_create(dpwa_sched **out, int n_peers, const uint32_t *seed_key, i
     }
     s->fetch_probability = fetch_probability;
     s->peers.assign((size_t)n_peers, PeerEntry());
+    for (int k = 0; k < n_peers; ++k) s->order.push_back(k);
     *out = s;
     return DPWA_OK;
 }
@@ -178,12 +182,11 @@ int dpwa_sched_bernoulli(dpwa_sched *s, int *fetching)
 int dpwa_sched_pick(dpwa_sched *s, int *peer, int *connected)
 {
     if (!s || !peer || !connected) return set_error(DPWA_ERR_ARG, "dpwa_sched_pick: NULL argument");
-    // conn.py:227-229: one randint(10, 1000) per live peer, in insertion order
+    // conn.py:227-229: one randint(10, 1000) per live peer, in dict (insertion) order
     int64_t best = -1;
     int n_best = 0;
     s->draw.assign(s->peers.size(), -1);
-    for (size_t k = 0; k < s->peers.size(); ++k) {
-        if (!s->peers[k].live) continue;
+    for (int k : s->order) {
         int64_t v = s->peers[k].score + s->rng.randint(kFlowMin, kFlowMax);
         s->draw[k] = v;
         if (v > best) {
@@ -200,10 +203,10 @@ int dpwa_sched_pick(dpwa_sched *s, int *peer, int *connected)
     }
     // conn.py:238-239: ties in insertion order, chosen by randint(0, k-1) (always drawn)
     int64_t which = s->rng.randint(0, n_best - 1);
-    for (size_t k = 0; k < s->peers.size(); ++k) {
+    for (int k : s->order) {
         if (s->draw[k] == best) {
             if (which == 0) {
-                *peer = (int)k;
+                *peer = k;
                 *connected = s->peers[k].connected ? 1 : 0;
                 return DPWA_OK;
             }
@@ -211,6 +214,14 @@ int dpwa_sched_pick(dpwa_sched *s, int *peer, int *connected)
         }
     }
     return set_error(DPWA_ERR_STATE, "dpwa_sched_pick: internal error");
+}
+
+// TxThread.remove_peer (conn.py:215-222): `del self.peers[name]`.
+static void drop_peer(dpwa_sched *s, int peer)
+{
+    s->peers[peer].live = false;
+    s->peers[peer].connected = false;
+    s->order.erase(std::remove(s->order.begin(), s->order.end(), peer), s->order.end());
 }
 
 int dpwa_sched_report(dpwa_sched *s, int peer, int outcome, int *round_done, int *got_data)
@@ -229,8 +240,7 @@ int dpwa_sched_report(dpwa_sched *s, int peer, int outcome, int *round_done, int
         *round_done = 1;
         break;
     case DPWA_CONNECT_ERROR:     // conn.py:257-260
-        p.live = false;
-        p.connected = false;
+        drop_peer(s, peer);
         *round_done = 1;
         break;
     case DPWA_REPLY_PAYLOAD:     // conn.py:301-302
@@ -246,8 +256,7 @@ int dpwa_sched_report(dpwa_sched *s, int peer, int outcome, int *round_done, int
         p.connected = false;
         break;
     case DPWA_REPLY_ERROR:       // conn.py:311-313
-        p.live = false;
-        p.connected = false;
+        drop_peer(s, peer);
         break;
     default:
         return set_error(DPWA_ERR_ARG, "dpwa_sched_report: unknown outcome");
@@ -306,8 +315,19 @@ int dpwa_sched_remove(dpwa_sched *s, int peer)
 {
     if (!s || peer < 0 || (size_t)peer >= s->peers.size() || !s->peers[peer].live)
         return set_error(DPWA_ERR_ARG, "dpwa_sched_remove: bad peer");
-    s->peers[peer].live = false;
-    s->peers[peer].connected = false;
+    drop_peer(s, peer);
+    return DPWA_OK;
+}
+
+// TxThread.add_peer (conn.py:208-213): `self.peers[name] = WorkerConn(...)` -- a fresh record
+// (score 1000, not connected).  A live peer keeps its place in the dict order; a removed one
+// is inserted again, at the end.
+int dpwa_sched_add(dpwa_sched *s, int peer)
+{
+    if (!s || peer < 0 || (size_t)peer >= s->peers.size()) return set_error(DPWA_ERR_ARG, "dpwa_sched_add: bad peer");
+    PeerEntry &p = s->peers[peer];
+    if (!p.live) s->order.push_back(peer);
+    p = PeerEntry();
     return DPWA_OK;
 }
 

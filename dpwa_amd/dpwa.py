@@ -80,13 +80,26 @@ class DpwaConfiguration:
 
 class PeerSnapshot:
     """What update_wait returns in place of the reference's pickled payload bytes: the
-    fetched snapshot, resident on the learner's GPU."""
+    fetched snapshot, resident on the learner's GPU.  ``tensor()`` materialises it (a
+    stream-ordered device copy) for callers that do the reference adapter's arithmetic
+    themselves (pytorch.py:64-68); it is valid until the fetch is averaged or abandoned."""
 
     def __init__(self, conn, peer_index, version):
         self.peer = conn.peers[peer_index].name
         self.version = version
         self.numel = conn._learner.numel
         self.dtype = conn._learner.dtype
+        self._learner = conn._learner
+        self._round = conn._learner.version
+
+    def tensor(self):
+        learner = self._learner
+        if learner._h is None or learner.version != self._round:
+            raise RuntimeError("this snapshot's fetch is no longer in flight (a later update_send started a new one)")
+        out = torch.empty(self.numel, dtype=self.dtype, device=learner.device)
+        _lib.call("dpwa_learner_copy_fetched", learner.handle, ctypes.c_void_p(out.data_ptr()),
+                  ctypes.c_void_p(torch.cuda.current_stream(learner.device).cuda_stream))
+        return out
 
     def __repr__(self):
         return "PeerSnapshot(peer=%r, version=%d, numel=%d, dtype=%s)" % (self.peer, self.version, self.numel,
@@ -94,13 +107,62 @@ class PeerSnapshot:
 
 
 class DeviceFactor:
-    """The interpolation factor, computed on the device.  ``float(f)`` synchronises."""
+    """The interpolation factor of dpwa.py:143-147, computed on the device.
+
+    It stands in for the Python float the reference returns (dpwa.py:156), so the adapter's
+    statement ``factor * t + (1 - factor) * param`` (pytorch.py:68) works unchanged: in
+    arithmetic it becomes a 0-d float64 tensor on the learner's device, copied from the
+    coefficient block in stream order (no host sync).  ``1 - factor`` is then computed in
+    float64 and each product rounds the scalar to the tensor's dtype, exactly as ATen treats
+    the reference's Python float.  ``float(f)`` synchronises and returns the exact double."""
 
     def __init__(self, learner):
         self._learner = learner
+        self._round = learner.version
+        self._t = None
+
+    def tensor(self):
+        if self._t is None:
+            learner = self._learner
+            if learner._h is None or learner.version != self._round:
+                raise RuntimeError("stale factor: a later update_send has started a new round")
+            t = torch.empty((), dtype=torch.float64, device=learner.device)
+            _lib.call("dpwa_learner_copy_factor", learner.handle, ctypes.c_void_p(t.data_ptr()),
+                      ctypes.c_void_p(torch.cuda.current_stream(learner.device).cuda_stream))
+            self._t = t
+        return self._t
 
     def __float__(self):
+        if self._t is not None:
+            return float(self._t.item())
         return float(self._learner.read_coef().factor)
+
+    def __mul__(self, other):
+        return self.tensor() * other
+
+    def __rmul__(self, other):
+        return other * self.tensor()
+
+    def __add__(self, other):
+        return self.tensor() + other
+
+    def __radd__(self, other):
+        return other + self.tensor()
+
+    def __sub__(self, other):
+        return self.tensor() - other
+
+    def __rsub__(self, other):
+        return other - self.tensor()
+
+    def __truediv__(self, other):
+        return self.tensor() / other
+
+    def __rtruediv__(self, other):
+        return other / self.tensor()
+
+    def __neg__(self):
+        return -self.tensor()
 
     def coefficients(self):
         c = self._learner.read_coef()
@@ -185,8 +247,13 @@ class DpwaConnection:
 
     # ---------------------------------------------------------------- reference API
     def add_peer(self, name, host, port):
-        raise NotImplementedError("peers come from the YAML node list (dpwa.py:88-89); "
-                                  "re-adding a removed peer is not supported")
+        """dpwa.py:95-96 -> TxThread.add_peer (conn.py:208-213): the peer gets a fresh record
+        (flow-control score 1000, not connected); a removed peer is picked again, after the
+        others in pick order, as a re-inserted dict key is.  On MI355X a peer is reached through
+        the group, so `name` must be a node of the config (host/port are the reference's
+        addressing and are kept only for the call's shape); unknown names raise KeyError."""
+        k = self._peer_by_name(name)
+        self._sched.add(k)
 
     def remove_peer(self, name):
         """dpwa.py:98-99 -> TxThread.remove_peer (conn.py:215-222): permanent."""
@@ -349,7 +416,8 @@ class DpwaConnection:
         if not isinstance(parameters, torch.Tensor) or parameters.device.type != "cuda":
             raise TypeError("DpwaConnection.update_send expects the flat parameter buffer as a GPU tensor")
         if parameters.dtype not in DTYPES:
-            raise TypeError("dpwa averages float32 or bfloat16 parameters, got %s" % parameters.dtype)
+            # the reference's TYPE_CONVERSION lookup raises KeyError (pytorch.py:11-14, 22)
+            raise KeyError("dpwa averages float32 or bfloat16 parameters, got %s" % parameters.dtype)
         _lib.call("dpwa_node_bind", self._node, parameters.device.index, parameters.numel(),
                   DTYPES[parameters.dtype])
         h = ctypes.c_void_p()

@@ -99,6 +99,10 @@ class DistGroup:
         if nodes[self.rank]["name"] != name:
             raise ValueError("DistGroup: rank %d is node %r in the config, not %r"
                              % (self.rank, nodes[self.rank]["name"], name))
+        if not _single_host(dist, process_group):
+            raise ValueError("the torch.distributed job spans several hosts: the device transport maps peers' "
+                             "snapshot slots over IPC/xGMI within one node only; use "
+                             "DpwaPyTorchAdapter(..., transport='wire') (the reference's TCP protocol) across hosts")
         self.backend = dist.get_backend(process_group)
         self._flag = None
         self.relay_blocks = 0        # > 0: relay transport (set by the connection's pull mode)
@@ -249,7 +253,29 @@ class AsyncDistGroup(DistGroup):
             _lib.call("dpwa_board_close", board)
 
 
+def _single_host(dist, process_group=None):
+    """Every rank of the group runs on this host (the IPC/xGMI groups map peers' HBM with
+    hipIpcOpenMemHandle, which only works within one node).  torchrun says so through
+    LOCAL_WORLD_SIZE; otherwise the ranks compare host identities (a collective)."""
+    world = dist.get_world_size(process_group)
+    lws = os.environ.get("LOCAL_WORLD_SIZE")
+    if process_group is None and lws is not None and os.environ.get("WORLD_SIZE") == str(world):
+        return int(lws) == world
+    import socket
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            ident = socket.gethostname() + "/" + f.read().strip()
+    except OSError:
+        ident = socket.gethostname()
+    ids = [None] * world
+    dist.all_gather_object(ids, ident, group=process_group)
+    return len(set(ids)) == 1
+
+
 def default_group(config_file, nodes, name):
+    """LocalGroup when this process holds every node; DistGroup when torch.distributed runs
+    one rank per node of the config on ONE host.  A multi-host job cannot map peers' HBM:
+    it must use the reference's TCP protocol (transport='wire', dpwa_amd/bridge.py)."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() == len(nodes) > 1:
         return DistGroup(nodes, name)

@@ -31,7 +31,7 @@ class Learner:
     def __init__(self, device, numel, dtype, interp_cfg=None, handle=None):
         """Creates a learner, or wraps (without owning) `handle` from dpwa_node_handles."""
         if dtype not in DTYPES:
-            raise TypeError("dpwa averages float32 or bfloat16 parameters, got %s" % dtype)
+            raise KeyError("dpwa averages float32 or bfloat16 parameters, got %s" % dtype)
         self.device = torch.device(device)
         self.numel = int(numel)
         self.dtype = dtype

@@ -88,6 +88,13 @@ class Scheduler:
             raise _lib.DpwaError("dpwa_sched_fetch", rc, _lib.load().dpwa_last_error().decode(errors="replace"))
         return peer.value, att.value
 
+    def add(self, peer):
+        """TxThread.add_peer (conn.py:208-213): fresh record, score 1000, not connected."""
+        _lib.call("dpwa_sched_add", self._h, peer)
+
+    def remove(self, peer):
+        _lib.call("dpwa_sched_remove", self._h, peer)
+
     def score(self, peer):
         out = ctypes.c_int()
         _lib.call("dpwa_sched_score", self._h, peer, ctypes.byref(out))

@@ -103,6 +103,16 @@ int dpwa_lerp_f32_host(float *param, const float *peer, int64_t n, double factor
 int dpwa_lerp_bf16_host(uint16_t *param, const uint16_t *peer, int64_t n, double factor,
                         dpwa_stream_t stream);
 
+/* The fused average of dpwa_learner_average without a learner (the product kernel over
+ * caller-owned buffers): reads clock_dev[0] and the 256-B dpwa_header at `peer_slot`, lerps the
+ * n elements following that header into `param` in place, writes clock_dev[1] = new clock and
+ * *coef_dev.  snap_payload (NULL or n elements): the write-through form, which also stores the
+ * result there (dpwa_learner_average_through).  start_event/stop_event (hipEvent_t, both or neither): the kernel is launched with
+ * hipExtLaunchKernelGGL so they record its own begin and end (measurement). */
+int dpwa_average(int32_t dtype, void *param, const void *peer_slot, int64_t n, const dpwa_interp *cfg,
+                 double *clock_dev, double loss, dpwa_coef *coef_dev, void *snap_payload, dpwa_stream_t stream,
+                 void *start_event, void *stop_event);
+
 /* Factor + clock on the device (dpwa.py:139-155 + interpolation.py): reads *clock_dev and the
  * peer's header, writes *coef_dev and, unless the status is an error, *clock_dev = new_clock.
  * `loss` is used when loss_dev is NULL, else *loss_dev (a device float64). */
@@ -222,6 +232,13 @@ int dpwa_learner_wait_fetch(dpwa_learner *l, dpwa_stream_t stream);
 #define DPWA_PULL_KERNEL 1
 int dpwa_learner_set_pull(dpwa_learner *l, int mode, int max_blocks);
 
+/* Reference-style seam (dpwa.py:156 returns (payload, factor) and pytorch.py:68 does the
+ * arithmetic itself): copy_factor enqueues a copy of the last factor (float64) to dst_dev on
+ * `stream`; copy_fetched enqueues, after the pull has landed, a copy of the payload of the fetch
+ * in flight (between update_wait and the lerp) to dst_dev (n elements). */
+int dpwa_learner_copy_factor(dpwa_learner *l, double *dst_dev, dpwa_stream_t stream);
+int dpwa_learner_copy_fetched(dpwa_learner *l, void *dst_dev, dpwa_stream_t stream);
+
 /* Abandons a fetch whose factor was computed but whose lerp will never be issued (the
  * caller of update_wait chose not to average); the snapshot it read may then be reused. */
 int dpwa_learner_cancel(dpwa_learner *l);
@@ -287,6 +304,9 @@ int dpwa_sched_fetch(dpwa_sched *s, const int32_t *peer_status, int max_attempts
 int dpwa_sched_score(const dpwa_sched *s, int peer, int *score);
 /* DpwaConnection.remove_peer (dpwa.py:98-99 -> conn.py:215-222): drop a peer for good. */
 int dpwa_sched_remove(dpwa_sched *s, int peer);
+/* DpwaConnection.add_peer (dpwa.py:95-96 -> conn.py:208-213): a fresh record for the peer
+ * (score 1000, not connected); a removed peer is inserted again at the end of the pick order. */
+int dpwa_sched_add(dpwa_sched *s, int peer);
 int dpwa_sched_n_live(const dpwa_sched *s, int *n_live);
 /* raw CPython-equivalent draws, for tests: random.random(), random.randint(a, b) */
 int dpwa_sched_random(dpwa_sched *s, double *out);

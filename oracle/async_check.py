@@ -1,0 +1,110 @@
+"""Checker for free-running (gossip-board) rounds -- TEST INFRASTRUCTURE ONLY (see
+oracle/__init__.py).  Used by tests/test_gpu_async.py and by bench.py's parity leg, after
+the timed region, never as the thing measured.
+
+In a free-running round the version of a peer that gets averaged depends on timing, so there
+is no fixed trajectory to replay.  Instead every rank publishes parameters that are a known
+function of (rank, round) -- ``async_base`` -- and losses ``async_loss``; then a round that
+read version v of peer q must equal the oracle lerp (pytorch.py:68) of this round's base
+with q's base of round v-1 under the factor of dpwa.py:143-147, and the clocks must follow
+dpwa.py:112 and 150-155 through exactly the versions that were read.  A torn or overwritten
+snapshot, a version handed out before its bytes landed or a stale clock cannot pass.
+"""
+import numpy as np
+
+from .lerp import lerp_f32
+from .policy import factor_and_clock
+
+
+def async_base(rank, r, n):
+    """The parameters rank `rank` publishes at its round r (publish number r + 1)."""
+    return (np.arange(n, dtype=np.float32) * np.float32(1e-3) + np.float32(rank * 1000 + r)).astype(np.float32)
+
+
+def async_loss(rank, r, wait=False):
+    """The loss rank `rank` passes at its round r (update_send, or update_wait when `wait`):
+    decaying, so a divergence threshold is crossed mid-run."""
+    x = 2.0 * float(np.exp(-r / 8.0)) + 0.1 * rank + 0.05
+    return 0.9 * x if wait else x
+
+
+class AsyncRuns:
+    """Recomputes the clocks and factors of a set of free-running runs.
+
+    peers[g][r]    name of the peer rank g averaged with at its round r ("" = none)
+    versions[g][r] the version (1-based publish number) of that peer it read
+    names          node names, index = rank
+    Only ranks present in `peers` are known; a rank that left early is absent."""
+
+    def __init__(self, names, peers, versions, interp="constant", value=0.5, thr=0.0):
+        self.names = list(names)
+        self.peers = {g: [str(p) for p in v] for g, v in peers.items()}
+        self.versions = {g: [int(x) for x in v] for g, v in versions.items()}
+        self.interp, self.value, self.thr = interp, value, thr
+        self._after = {}
+
+    def complete(self):
+        return all(g in self.peers for g in range(len(self.names)))
+
+    def read(self, g, r):
+        """(peer rank, version) read by rank g at round r, or None."""
+        p = self.peers[g][r]
+        if p == "":
+            return None
+        return self.names.index(p), self.versions[g][r]
+
+    def policy(self, g, r):
+        """dpwa.py:143-155 for rank g's round r against what it read: (factor, new clock)."""
+        q, v = self.read(g, r)
+        return factor_and_clock(self.interp, self.value, self.thr, self.clock_published(g, r),
+                                self.clock_published(q, v - 1), async_loss(g, r, True), async_loss(q, v - 1))
+
+    def clock_published(self, g, r):
+        """The clock rank g published at its round r (dpwa.py:112: clock += 1)."""
+        return (self.clock_after(g, r - 1) if r > 0 else 0.0) + 1.0
+
+    def clock_after(self, g, r):
+        """Rank g's clock after its round r's update_wait (dpwa.py:155; unchanged with no data)."""
+        key = (g, r)
+        if key not in self._after:
+            if self.read(g, r) is None:
+                self._after[key] = self.clock_published(g, r)
+            else:
+                self._after[key] = self.policy(g, r)[1]
+        return self._after[key]
+
+    def expected_params(self, g, r, n):
+        """What rank g's parameters must be after round r."""
+        mine = async_base(g, r, n)
+        got = self.read(g, r)
+        if got is None:
+            return mine
+        q, v = got
+        if self.complete():
+            factor = self.policy(g, r)[0]
+        else:           # a departed rank's clocks are unknown: constant interpolation only
+            if not (self.interp == "constant" and self.thr == 0.0):
+                raise ValueError("incomplete runs can only be checked under constant interpolation")
+            factor = self.value
+        return lerp_f32(mine, async_base(q, v - 1, n), factor)
+
+    def check_rank(self, g, params, clocks, n):
+        """Checks rank g's recorded params (T x n) and clocks (T) round by round; returns a list
+        of failure strings (empty = every round matched bit for bit)."""
+        bad = []
+        last = {}
+        for r in range(len(self.peers[g])):
+            got = self.read(g, r)
+            if got is not None:
+                q, v = got
+                if v < 1:
+                    bad.append("round %d: version %d" % (r, v))
+                if v < last.get(q, 0):
+                    bad.append("round %d: versions of %s went backwards" % (r, self.names[q]))
+                last[q] = v
+            want = self.expected_params(g, r, n)
+            if not np.array_equal(np.asarray(params[r]).view(np.uint32), want.view(np.uint32)):
+                bad.append("round %d: parameters differ from the oracle (peer %s)" % (r, self.peers[g][r] or "-"))
+            if self.complete() and float(clocks[r]) != self.clock_after(g, r):
+                bad.append("round %d: clock %r != %r" % (r, float(clocks[r]), self.clock_after(g, r)))
+        return bad

@@ -124,5 +124,11 @@ class OracleLearner:
         self.clock = new_clock
         return True, factor
 
+    # -- dpwa.py:95-96 -> conn.py:208-213 ----------------------------------------
+    def add_peer(self, name):
+        """A fresh WorkerConn under `name`: an existing key keeps its dict position, a
+        removed one is inserted again at the end."""
+        self.peers[name] = Peer(name)
+
     def scores(self, names):
         return [self.peers[n].score if n in self.peers else None for n in names]

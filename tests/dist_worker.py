@@ -111,16 +111,7 @@ def fault_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy"):
     dist.destroy_process_group()
 
 
-def async_base(rank, r, n):
-    """The parameters rank `rank` publishes at its round r (publish number r + 1)."""
-    return (np.arange(n, dtype=np.float32) * np.float32(1e-3) + np.float32(rank * 1000 + r)).astype(np.float32)
-
-
-def async_loss(rank, r, wait=False):
-    """The loss rank `rank` passes at its round r (update_send, or update_wait when `wait`):
-    decaying, so a divergence threshold is crossed mid-run."""
-    x = 2.0 * float(np.exp(-r / 8.0)) + 0.1 * rank + 0.05
-    return 0.9 * x if wait else x
+from oracle.async_check import async_base, async_loss  # noqa: E402  (checker's published values)
 
 
 def async_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy", die_rank=-1, die_round=-1):

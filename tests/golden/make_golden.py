@@ -23,6 +23,7 @@ Outputs (all small; see tests/golden/README.md):
   lerp_bf16.npz         torch-eager bf16 form (reference has no bf16 path: pytorch.py:11-14)
   policy.json           factor / clock / Bernoulli traces (dpwa/dpwa.py:101-156, interpolation.py)
   peer_select.json      TxThread peer choice + flow control under scripted faults (conn.py:224-317)
+  peer_add.json         the same with removed peers put back by add_peer (dpwa.py:95-96, conn.py:208-213)
   gossip.npz/.json      lock-step G-learner gossip through the real adapter + connection + TxThread
   wire.json             <HLL + pickle frames (dpwa/messaging.py:24-94)
   config.json           YAML parsing (dpwa/dpwa.py:29-93)
@@ -482,6 +483,64 @@ def gen_peer_select(tmp):
     print("peer_select: %d cases" % len(out))
 
 
+def gen_peer_add(tmp):
+    """TxThread with peers removed by errors and put back by DpwaConnection.add_peer
+    (dpwa.py:95-96 -> conn.py:208-213): a re-added peer is a fresh WorkerConn (score 1000,
+    not connected) and a removed one re-enters the dict -- and so the per-pick randint
+    order -- at the end."""
+    out = []
+    ci = 0
+    for G in (3, 5):
+        for prof in ("dying", "flaky"):
+            for seed in (3, 11):
+                ci += 1
+                nodes = make_nodes(G, base_port=48000 + 16 * ci)
+                for n in nodes:
+                    ADDR2NAME[(n["host"], n["port"])] = n["name"]
+                cfg = os.path.join(tmp, "add_%d.yaml" % ci)
+                write_config(cfg, nodes, 1.0, "clock", 0.0)
+                me = "w%d" % (1 + (seed % G))
+                conn = new_connection(cfg, me, seed, real_tx=True)
+                peers = [n["name"] for n in nodes if n["name"] != me]
+                env_rng = random.Random(seed * 104729 + G)
+                (pc, pr, pe), (qp, qe, qt, qx) = PROFILES[prof]
+                ENV.gate = None
+                ENV.connect_fn = lambda peer: pick(env_rng, ["ok", "refused", "error"], [pc, pr, pe])
+                ENV.request_fn = lambda peer: pick(env_rng, ["payload", "empty", "timeout", "error"],
+                                                   [qp, qe, qt, qx])
+                ENV.reply_fn = lambda peer: ({"clock": 1 + int(peer[1:]), "loss": 0.5}, b"payload")
+                rounds = []
+                for r in range(40):
+                    adds = []
+                    if r in (8, 16, 24, 32):        # put every removed peer back
+                        adds = [p for p in peers if p not in conn.tx.peers]
+                    if r in (12, 28):               # re-add a live peer: its record is reset
+                        live = [p for p in peers if p in conn.tx.peers]
+                        adds += live[-1:]
+                    for p in adds:
+                        node = [n for n in nodes if n["name"] == p][0]
+                        conn.add_peer(p, node["host"], node["port"])
+                    RNG.set_current(me)
+                    ENV.logs[me] = []
+                    conn.update_send(b"mine", 1.0)
+                    fetching = conn.fetching
+                    payload, factor = conn.update_wait(1.0)
+                    scores = []
+                    for p in peers:
+                        w = conn.tx.peers.get(p)
+                        scores.append(None if w is None else w.flow_control_score)
+                    rounds.append({"add_peer": adds, "fetching": fetching, "attempts": list(ENV.logs[me]),
+                                   "data": payload is not None, "scores": scores,
+                                   "order": list(conn.tx.peers.keys())})
+                conn.tx._queue.put(False)
+                out.append({"G": G, "me": me, "peers": peers, "fetch_probability": 1.0,
+                            "profile": prof, "seed": seed, "rounds": rounds})
+    with open(os.path.join(OUT, "peer_add.json"), "wt") as f:
+        json.dump({"source": "reference dpwa/dpwa.py:95-99 add_peer/remove_peer + dpwa/conn.py:208-317 TxThread",
+                   "cases": out}, f, indent=0)
+    print("peer_add: %d cases" % len(out))
+
+
 # ----------------------------------------------------------------------------
 # E. lock-step G-learner gossip with data through the real adapter
 # ----------------------------------------------------------------------------
@@ -717,11 +776,19 @@ def gen_config(tmp):
 
 
 def main():
+    only = sys.argv[1:]
+    if only:     # regenerate just the named fixtures, e.g. `make_golden.py peer_add`
+        with tempfile.TemporaryDirectory() as tmp:
+            for name in only:
+                fn = globals()["gen_" + name]
+                fn(tmp) if fn.__code__.co_argcount else fn()
+        os._exit(0)
     with tempfile.TemporaryDirectory() as tmp:
         gen_lerp_f32()
         gen_lerp_bf16()
         gen_policy(tmp)
         gen_peer_select(tmp)
+        gen_peer_add(tmp)
         gen_gossip(tmp)
         gen_wire()
         gen_wire_adapter()

@@ -82,3 +82,30 @@ def test_dist_control_plane_matches_oracle(tmp_path, world, fp):
             else:
                 want.append(None)
         assert traces[r] == want, r
+
+
+def multihost_worker(rank, world, port, cfg):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    # what torchrun exports for a job of `world` ranks spread one per host
+    os.environ["WORLD_SIZE"] = str(world)
+    os.environ["LOCAL_WORLD_SIZE"] = "1"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dpwa_amd import DpwaConnection
+    try:
+        DpwaConnection("r%d" % rank, cfg, seed=1)
+    except ValueError as e:
+        assert "several hosts" in str(e) and "transport='wire'" in str(e), e
+    else:
+        raise AssertionError("a multi-host job must not get the IPC/xGMI group")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_multi_host_job_is_refused_the_ipc_group(tmp_path):
+    """A torchrun job spanning hosts cannot map peers' HBM: it gets a clear error naming the
+    wire transport instead of a hipIpcOpenMemHandle failure at the first publish."""
+    cfg = str(tmp_path / "mh.yaml")
+    dist_worker.write_cfg(cfg, ["r0", "r1"], 1.0, "constant", 0.0)
+    mp.spawn(multihost_worker, args=(2, free_port(), cfg), nprocs=2, join=True)

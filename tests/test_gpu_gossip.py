@@ -259,9 +259,10 @@ def test_update_wait_without_average_then_continue(tmp_path):
     assert a.clock == 4.0    # the clock still follows dpwa.py:150 (factor 0.5 between equal clocks)
 
 
-def test_write_through_matches_reference_trajectories(tmp_path):
-    """Adapter with write_through=True: the next snapshot is written by the averaging kernel
-    and the publish moves only the header -- trajectories stay bit-identical."""
+def test_full_publish_matches_reference_trajectories(tmp_path):
+    """The adapter's default is write-through (the trajectory tests above run it); with
+    write_through=False every publish copies the full snapshot -- trajectories are the same
+    bits."""
     meta = load_json("gossip.json")
     z = load_npz("gossip.npz")
     case = meta["cases"][1]
@@ -270,7 +271,7 @@ def test_write_through_matches_reference_trajectories(tmp_path):
     orig = ap.DpwaPyTorchAdapter.__init__
 
     def init_wt(self, net, name, cfg, **kw):
-        orig(self, net, name, cfg, write_through=True, **kw)
+        orig(self, net, name, cfg, write_through=False, **kw)
 
     ap.DpwaPyTorchAdapter.__init__ = init_wt
     try:

@@ -135,3 +135,45 @@ def test_fixture_files_are_data_only():
         assert fn.endswith((".json", ".npz", ".py", ".md")), fn
         if fn.endswith(".json"):
             json.load(open(os.path.join(GOLDEN, fn)))
+
+
+def test_async_checker_accepts_a_consistent_run_and_rejects_a_torn_one():
+    """oracle/async_check.py (the free-running checker used by test_gpu_async.py and bench.py's
+    parity leg): a CPU-made run in which every round reads a published version passes; a
+    snapshot with one element of a different version, or a stale clock, fails."""
+    from oracle.async_check import AsyncRuns, async_base
+    names = ["r0", "r1", "r2"]
+    n, T = 257, 9
+    rng = np.random.default_rng(4)
+    peers, versions = {}, {}
+    for g in range(3):
+        peers[g], versions[g] = [], []
+        for r in range(T):
+            if r == 0:
+                peers[g].append("")
+                versions[g].append(0)
+                continue
+            q = int(rng.choice([x for x in range(3) if x != g]))
+            peers[g].append(names[q])
+            versions[g].append(int(rng.integers(max(1, r - 1), r + 1)))    # q's publish r-1 or r
+    for g in range(3):          # versions per peer must not go backwards
+        last = {}
+        for r in range(T):
+            if peers[g][r]:
+                q = peers[g][r]
+                versions[g][r] = max(versions[g][r], last.get(q, 0))
+                last[q] = versions[g][r]
+    for interp, thr in (("constant", 0.0), ("clock", 0.0), ("loss", 0.5)):
+        check = AsyncRuns(names, peers, versions, interp, 0.5, thr)
+        for g in range(3):
+            params = np.stack([check.expected_params(g, r, n) for r in range(T)])
+            clocks = np.array([check.clock_after(g, r) for r in range(T)])
+            assert check.check_rank(g, params, clocks, n) == []
+            torn = params.copy()
+            q, v = check.read(g, 5)
+            torn[5, 100] = olerp.lerp_f32(async_base(g, 5, n), async_base(q, v, n), check.policy(g, 5)[0])[100]
+            assert any("round 5" in b for b in check.check_rank(g, torn, clocks, n))
+            if interp != "constant":
+                stale = clocks.copy()
+                stale[6] += 1.0
+                assert any("round 6: clock" in b for b in check.check_rank(g, params, stale, n))

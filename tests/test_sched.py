@@ -134,3 +134,58 @@ def test_flow_control_bounds_and_removal():
         s.report(1, "payload")
     _lib.call("dpwa_sched_remove", s._h, 0)
     assert s.pick() == (-1, False)
+
+
+def test_add_peer_matches_reference():
+    """Peers removed by errors and put back with add_peer (dpwa.py:95-96 -> conn.py:208-213):
+    fresh score, not connected, and a re-added peer draws its randint after the others --
+    replayed against the real TxThread's picks and scores."""
+    data = load_json("peer_add.json")
+    reorders = 0
+    for case in data["cases"]:
+        peers = case["peers"]
+        s = Scheduler(len(peers), case["seed"], case["fetch_probability"])
+        for r in case["rounds"]:
+            for name in r["add_peer"]:
+                s.add(peers.index(name))
+            fetching = s.bernoulli()
+            assert fetching == r["fetching"]
+            if fetching:
+                picks, got = replay_round(s, r["attempts"])
+                assert [peers[k] for k in picks] == [a["peer"] for a in r["attempts"]]
+                assert got == r["data"]
+            assert s.scores() == r["scores"]
+            reorders += r["order"] != [p for p in peers if p in r["order"]]
+    assert reorders > 0        # the fixture does exercise a changed pick order
+
+
+def test_oracle_add_peer_matches_reference():
+    from oracle.policy import OracleLearner
+    data = load_json("peer_add.json")
+    for case in data["cases"]:
+        L = OracleLearner(case["me"], case["peers"], 1.0, "clock", None, 0.0, case["seed"])
+        for r in case["rounds"]:
+            for name in r["add_peer"]:
+                L.add_peer(name)
+            L.update_send(1.0)
+            it = iter(r["attempts"])
+            pending = []           # the attempt whose connect outcome was just replayed
+
+            def conn_fn(peer):
+                a = next(it)
+                assert a["peer"] == peer
+                if a["connect"] == "ok":
+                    pending.append(a)
+                return a["connect"]
+
+            def req_fn(peer):
+                a = pending.pop() if pending else next(it)
+                assert a["peer"] == peer
+                out = a["request"]
+                return (out, {"clock": 1, "loss": 0.5}, b"x") if out == "payload" else (out, None, None)
+
+            _, payload, att = L.fetch(conn_fn, req_fn)
+            assert [a["peer"] for a in att] == [a["peer"] for a in r["attempts"]]
+            assert (payload is not None) == r["data"]
+            assert L.scores(case["peers"]) == r["scores"]
+            assert list(L.peers) == r["order"]
