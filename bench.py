@@ -113,10 +113,20 @@ def cpu_baseline(numel, seconds):
     same round's arithmetic on one host core (publish copy + averaging)."""
     from oracle import lerp as olerp
     from oracle import ref_round
-    # one reference round at 100M fp32 already takes ~9 s here: larger vectors are sampled
+    # one reference round at 100M fp32 already takes seconds: larger vectors are sampled
     out = ref_round.run(min(numel, REF_SAMPLE_MAX), seconds)
     if numel > REF_SAMPLE_MAX:
         out["sample"] += " (bounded sample of a %d-element workload)" % numel
+    # BASELINE.md's second size: the same round at 100M fp32 (a few rounds; the reference's
+    # 1B fp32 frame takes minutes per round and 1B/7B bf16 are not representable: N/A)
+    out["rows"] = [ref_round.run(100_000_000, seconds / 2, min_rounds=3)] if numel != 100_000_000 else []
+    out["rows_note"] = ("1B fp32: reference frame 4.0 GB, minutes per round (quadratic receive, messaging.py:55), not "
+                        "sampled; 1B/7B bf16: not representable by the reference (pytorch.py:11-14, messaging.py:16)")
+    ref_file = os.path.join(ROOT, "profiles", "reference_cpu_r02.json")
+    if os.path.exists(ref_file):
+        with open(ref_file) as f:
+            ref = json.load(f)
+        out["port_vs_reference"] = ref.get("port_vs_reference")
     lib = olerp.clib()
     rng = np.random.default_rng(0)
     param = rng.standard_normal(numel).astype(np.float32)

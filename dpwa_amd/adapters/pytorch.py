@@ -12,7 +12,9 @@ rebinds ``param.data`` to a new tensor), and float32 *and* bfloat16 models are a
 """
 import logging
 
-from ..dpwa import DpwaConnection
+import torch
+
+from ..dpwa import DpwaConfiguration, DpwaConnection
 from ..flat import FlatParameters
 
 LOGGER = logging.getLogger(__name__)
@@ -36,7 +38,8 @@ class DpwaPyTorchAdapter:
         job, pulled from HBM/over xGMI) or "wire" (peers are reached over TCP at the YAML's
         host/port with the reference's protocol -- e.g. reference CPU nodes; dpwa_amd/bridge.py)."""
         self._net = net
-        self._flat = FlatParameters(net.named_parameters())
+        gpu = DpwaConfiguration(config_file).get_gpu(name)      # optional per-node placement
+        self._flat = FlatParameters(net.named_parameters(), device=None if gpu is None else torch.device("cuda", gpu))
         if transport == "wire":
             from ..bridge import SnapshotCodec, WireConnection
             self._conn = WireConnection(name, config_file, codec=SnapshotCodec.from_flat(self._flat),

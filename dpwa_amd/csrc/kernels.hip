@@ -213,12 +213,12 @@ __device__ __forceinline__ void span_store(__amdgpu_buffer_rsrc_t r, int lane_of
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, lane_off, 0, AUX);
 }
 
-// Cache policies of the averaging kernel (tuning; DPWA_LERP_POLICY): the peer snapshot is
-// always read `nt`; the parameters are read `nt` (0, 2) or with the default policy (1, 3);
-// the result is stored `sc1` (0, 1) or `sc0 sc1` (2, 3).
+// Cache policies of the averaging kernel (tuning; DPWA_LERP_POLICY, a bit set): the peer
+// snapshot is always read `nt`; the parameters are read `nt` or, with bit 1, with the default
+// policy; the result is stored `sc1`, with bit 2 `sc0 sc1`, with bit 4 `nt sc1`.
 template <int POLICY> struct LerpPolicy {
     static constexpr int param_load = (POLICY & 1) ? 0 : kAuxStream;
-    static constexpr int store = (POLICY & 2) ? (kAuxStore | 1) : kAuxStore;
+    static constexpr int store = kAuxStore | ((POLICY & 2) ? 1 : 0) | ((POLICY & 4) ? kAuxStream : 0);
 };
 
 // One 16-byte item per lane; items beyond n/PER (the ragged tail) go to block 0.
@@ -262,7 +262,8 @@ __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ pa
         }
         __syncthreads();
         if (!s_ok) {          // no-op round; a write-through snapshot still gets the parameters
-            if (DUAL) span_store(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, p);
+            if (DUAL)
+                span_store<V, LerpPolicy<POLICY>::store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, p);
             if (DUAL && blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
                 const int64_t j = nv * Ops::PER + threadIdx.x;
                 reinterpret_cast<typename Ops::S *>(args.snap)[j] = reinterpret_cast<typename Ops::S *>(param)[j];
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ pa
     {
         const V r = Ops::lerp(a, b, q, p);
         span_store<V, LerpPolicy<POLICY>::store>(rp, lane_off, r);
-        if (DUAL) span_store(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, r);
+        if (DUAL) span_store<V, LerpPolicy<POLICY>::store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, r);
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
         typename Ops::S *ps = reinterpret_cast<typename Ops::S *>(param);
@@ -359,7 +360,7 @@ static int lerp_policy()
     static const int forced = [] {
         const char *e = getenv("DPWA_LERP_POLICY");
         const int p = e ? atoi(e) : 0;
-        return (p >= 0 && p <= 3) ? p : 0;
+        return (p >= 0 && p <= 7) ? p : 0;
     }();
     return forced;
 }
@@ -375,6 +376,8 @@ static hipError_t launch_mode(void *param, const void *peer, int64_t n, const Le
             case 1: return launch_blocks<Ops, MODE, DUAL, 64, 1>(param, peer, n, args, s, timing);
             case 2: return launch_blocks<Ops, MODE, DUAL, 64, 2>(param, peer, n, args, s, timing);
             case 3: return launch_blocks<Ops, MODE, DUAL, 64, 3>(param, peer, n, args, s, timing);
+            case 4: return launch_blocks<Ops, MODE, DUAL, 64, 4>(param, peer, n, args, s, timing);
+            case 5: return launch_blocks<Ops, MODE, DUAL, 64, 5>(param, peer, n, args, s, timing);
             default: return launch_blocks<Ops, MODE, DUAL, 64>(param, peer, n, args, s, timing);
             }
         case 128: return launch_blocks<Ops, MODE, DUAL, 128>(param, peer, n, args, s, timing);

@@ -69,6 +69,15 @@ class DpwaConfiguration:
         return self.config['divergence_threshold']
 
     # -- extensions (absent keys keep the reference behaviour) ------------------------
+    def get_gpu(self, name):
+        """Per-node `gpu:` key (the device index the node's learner runs on), else None.  The
+        reference ignores unknown node keys (dpwa.py:66-72 turns each node into a Struct), so
+        a config carrying them still loads there."""
+        for node in self.get_nodes():
+            if node.get('name') == name and 'gpu' in node:
+                return int(node['gpu'])
+        return None
+
     def get_seed(self, name):
         """Per-node `seed:` key, else a top-level `- seed:` entry, else None (OS entropy,
         as the reference, which never seeds `random`)."""
@@ -413,6 +422,11 @@ class DpwaConnection:
         raise _lib.DpwaError(name, rc, self._lib.dpwa_last_error().decode(errors="replace"))
 
     def _bind(self, parameters):
+        gpu = self.config.get_gpu(self.name)
+        if gpu is not None and isinstance(parameters, torch.Tensor) and \
+                (parameters.device.type != "cuda" or parameters.device.index != gpu):
+            raise ValueError("node %r is placed on gpu %d by its config, but its parameters are on %s"
+                             % (self.name, gpu, parameters.device))
         if not isinstance(parameters, torch.Tensor) or parameters.device.type != "cuda":
             raise TypeError("DpwaConnection.update_send expects the flat parameter buffer as a GPU tensor")
         if parameters.dtype not in DTYPES:

@@ -13,7 +13,10 @@ ALIGN_BYTES = 256
 
 
 class FlatParameters:
-    def __init__(self, named_parameters):
+    def __init__(self, named_parameters, device=None):
+        """device: where the flat buffer lives (a config's per-node `gpu:` key); parameters on
+        another device are moved there (create the optimizer afterwards, as the reference's
+        trainer does: examples/pytorch-cifar/main.py:109-116)."""
         params = list(named_parameters)
         if not params:
             raise ValueError("the model has no parameters")
@@ -23,7 +26,7 @@ class FlatParameters:
             raise TypeError("all parameters must share one dtype and one device, got %s on %s"
                             % (sorted(map(str, dtypes)), sorted(map(str, devices))))
         self.dtype = dtypes.pop()
-        self.device = devices.pop()
+        self.device = devices.pop() if device is None else torch.device(device)
         esize = torch.empty((), dtype=self.dtype).element_size()
         align = ALIGN_BYTES // esize
         self.names, self.params, self.offsets = [], [], []

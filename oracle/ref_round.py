@@ -136,7 +136,9 @@ class _Server(threading.Thread):
         conn.close()
 
 
-def _learner(idx, numel, seconds, port_q, peer_q, start, out_q):
+def _learner(idx, numel, seconds, min_rounds, core, port_q, peer_q, start, out_q, finish):
+    if core is not None:
+        os.sched_setaffinity(0, {core})        # taskset -c <core> (prepare.py:31)
     rng = np.random.default_rng(idx)
     params = {"p%d" % i: rng.standard_normal(k).astype(np.float32) for i, k in enumerate(_sizes(numel))}
     server = _Server()
@@ -146,39 +148,55 @@ def _learner(idx, numel, seconds, port_q, peer_q, start, out_q):
     client.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
     clock, factor, loss = 0.0, 0.5, 1.0
     rounds, busy = 0, 0.0
+    phases = []          # per averaged round: (pickle, fetch, unpickle, lerp) seconds
     start.wait()
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
+    while time.perf_counter() - t0 < seconds or rounds < min_rounds:
         t = time.perf_counter()
         blob = pickle.dumps({k: bytes(v) for k, v in params.items()})      # update_send
         clock += 1
         server.publish({"clock": clock, "loss": loss}, blob)
+        t1 = time.perf_counter()
         send_message(client, FETCH)                                           # fetch
         _, state, payload = recv_message(client)
+        t2 = time.perf_counter()
         if payload is not None:                                               # update_wait
             clock = factor * state["clock"] + (1 - factor) * clock
             other = pickle.loads(payload)
+            t3 = time.perf_counter()
             for k in params:
                 params[k] = lerp_f32(params[k], np.frombuffer(other[k], dtype=np.float32), factor)
+            t4 = time.perf_counter()
             rounds += 1
+            phases.append((t1 - t, t2 - t1, t3 - t2, t4 - t3))
         busy += time.perf_counter() - t
-    out_q.put((idx, rounds, busy, time.perf_counter() - t0))
-    time.sleep(1.0)      # keep serving while the other learner finishes its last round
+    out_q.put((idx, rounds, busy, time.perf_counter() - t0, phases))
+    finish.wait(timeout=3600)   # keep serving (server thread) until the other learner is done too
     client.close()
 
 
-def run(numel=11_173_962, seconds=10.0):
-    """Two learner processes on localhost for about `seconds` of rounds each; returns the
-    cpu_baseline dict: aggregate averaged GB/s (3*numel*4 bytes per completed averaging,
-    both learners, over the wall time) and the mean round time."""
+def _cores():
+    """Two distinct cores this process may run on (the learners are pinned one each)."""
+    allowed = sorted(os.sched_getaffinity(0))
+    return (allowed[0], allowed[1]) if len(allowed) >= 2 else (None, None)
+
+
+def run(numel=11_173_962, seconds=10.0, min_rounds=0):
+    """Two learner processes on localhost, each pinned to its own core, for about `seconds` of
+    rounds each (and at least `min_rounds` averagings); returns the cpu_baseline dict:
+    aggregate averaged GB/s (3*numel*4 bytes per completed averaging, both learners, over the
+    wall time), the mean and median round time and the per-phase split of a round."""
     ctx = mp.get_context("spawn")
     port_q, out_q = ctx.Queue(), ctx.Queue()
     peer_qs = [ctx.Queue(), ctx.Queue()]
     start = ctx.Event()
+    finish = ctx.Barrier(2)
     env = dict(os.environ)
     os.environ["OMP_NUM_THREADS"] = "1"          # one core per learner, as prepare.py:31 pins them
+    cores = _cores()
     try:
-        procs = [ctx.Process(target=_learner, args=(i, numel, seconds, port_q, peer_qs[i], start, out_q), daemon=True)
+        procs = [ctx.Process(target=_learner, args=(i, numel, seconds, min_rounds, cores[i], port_q, peer_qs[i],
+                                                    start, out_q, finish), daemon=True)
                  for i in range(2)]
         for p in procs:
             p.start()
@@ -189,16 +207,33 @@ def run(numel=11_173_962, seconds=10.0):
     peer_qs[0].put(ports[1])
     peer_qs[1].put(ports[0])
     start.set()
-    res = [out_q.get(timeout=seconds * 30 + 300) for _ in procs]
+    res = [out_q.get(timeout=seconds * 30 + 600) for _ in procs]
     for p in procs:
         p.join(timeout=30)
         if p.is_alive():
             p.terminate()
     rounds = sum(r[1] for r in res)
     wall = max(r[3] for r in res)
+    phases = np.array([ph for r in res for ph in r[4]]) if rounds else np.zeros((1, 4))
+    med = np.median(phases, axis=0) * 1e3
+    per_round = phases.sum(axis=1) * 1e3
     return {"value": rounds * 3 * numel * 4 / wall / 1e9, "unit": "GB/s", "cores": 2, "kind": "port",
-            "sample": "the reference's CPU round restated (oracle/ref_round.py): 2 learner processes, localhost TCP, "
-                      "pickle + <HLL framing + numpy fp32 lerp over %s (%d elements); %d averagings in %.1f s"
-                      % ("ResNet-18's 62 tensors" if len(_sizes(numel)) > 1 else "one flat tensor", numel, rounds,
-                         wall),
-            "ms_per_round": round(1e3 * sum(r[2] for r in res) / max(1, rounds), 2)}
+            "sample": "the reference's CPU round restated (oracle/ref_round.py): 2 learner processes, each pinned to "
+                      "one core (taskset -c %s / %s, OMP_NUM_THREADS=1, as prepare.py:31), localhost TCP, pickle + "
+                      "<HLL framing + numpy fp32 lerp over %s (%d elements); %d averagings in %.1f s"
+                      % (cores[0], cores[1], "ResNet-18's 62 tensors" if len(_sizes(numel)) > 1 else "one flat tensor",
+                         numel, rounds, wall),
+            "numel": numel,
+            "ms_per_round": round(1e3 * sum(r[2] for r in res) / max(1, rounds), 2),
+            "median_round_ms": round(float(np.median(per_round)), 2),
+            "rounds": rounds,
+            "phases_median_ms": {"pickle": round(float(med[0]), 2), "fetch": round(float(med[1]), 2),
+                                 "unpickle": round(float(med[2]), 2), "lerp": round(float(med[3]), 2)},
+            "phases_note": "per averaged round of one learner: pickle = update_send's bytes() + pickle.dumps + "
+                           "publish under the server lock (pytorch.py:49-53, conn.py:73-79); fetch = request + the "
+                           "peer's reply over TCP incl. its chunked send and the blob += chunk receive (conn.py:"
+                           "297-298, messaging.py:36-94); unpickle = pickle.loads (pytorch.py:64); lerp = per-tensor "
+                           "f32(a*t)+f32(b*p) (pytorch.py:66-68)",
+            "taskset": [cores[0], cores[1]],
+            "cpu_count": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0))}

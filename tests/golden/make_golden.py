@@ -732,9 +732,19 @@ CONFIGS = {
 }
 
 
+def _generated_configs():
+    """Node lists written by dpwa_amd.launch (this repository's launcher, with the per-node
+    gpu: key): the reference must load them (tests/test_config.py)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from dpwa_amd.launch import config_text
+    return {"launch_gpu.yaml": config_text(["w0", "w1", "w2"], gpus=[0, 1, 2], interpolation="clock",
+                                           divergence_threshold=0.5),
+            "launch_plain.yaml": config_text(["w1", "w2"], fetch_probability=0.7, interpolation="loss")}
+
+
 def gen_config(tmp):
     out = {}
-    for fname, text in CONFIGS.items():
+    for fname, text in list(CONFIGS.items()) + list(_generated_configs().items()):
         path = os.path.join(tmp, fname)
         with open(path, "wt") as f:
             f.write(text)

@@ -115,10 +115,55 @@ def test_launch_make_config_roundtrip(tmp_path):
 
 
 def test_reference_loads_generated_config(tmp_path):
-    """The generated file follows the reference schema: the reference's own parser
-    (re-stated in config.json's fixtures) yields the same dict as ours for the same text."""
+    """What dpwa_amd.launch writes -- the reference schema plus the per-node gpu: key -- is
+    what the reference itself parsed into tests/golden/config.json (launch_*.yaml entries,
+    made by tests/golden/make_golden.py through the reference's DpwaConfiguration and
+    DpwaConnection): the same text, and our parse equals the reference's."""
+    from dpwa_amd.launch import config_text
+    files = load_json("config.json")["files"]
+    assert config_text(["w0", "w1", "w2"], gpus=[0, 1, 2], interpolation="clock",
+                       divergence_threshold=0.5) == files["launch_gpu.yaml"]["text"]
+    assert config_text(["w1", "w2"], fetch_probability=0.7, interpolation="loss") == files["launch_plain.yaml"]["text"]
+    rec = files["launch_gpu.yaml"]
+    assert [n["gpu"] for n in rec["nodes"]] == [0, 1, 2]
+    assert rec["connections"]["w2"]["me"] == {"name": "w2", "host": "localhost", "port": 45002, "gpu": 2}
+    p = tmp_path / "g.yaml"
+    p.write_text(rec["text"])
+    c = DpwaConfiguration(str(p))
+    assert c.config == rec["config"]
+    assert [c.get_gpu(n) for n in ("w0", "w1", "w2")] == [0, 1, 2]
+
+
+def test_prepare_writes_config_and_torchrun_script(tmp_path):
+    """prepare.py:17-40 for a GPU node: one node per GPU with its gpu: key, and a run.sh that
+    starts one rank per GPU; rank r finds node r and its device."""
+    import os
+    import stat
+    from dpwa_amd.launch import main, node_for_rank
+    assert main(["prepare", "--gpus", "4", "--out-dir", str(tmp_path), "--script", "main.py",
+                 "--interpolation", "clock", "--", "--lr=0.01", "--batch-size", "8"]) == 0
+    cfg = tmp_path / "dpwa.yaml"
+    c = DpwaConfiguration(str(cfg))
+    assert [n["name"] for n in c.get_nodes()] == ["w0", "w1", "w2", "w3"]
+    assert [c.get_gpu("w%d" % g) for g in range(4)] == [0, 1, 2, 3]
+    run = (tmp_path / "run.sh").read_text()
+    assert run.startswith("#!/bin/bash")
+    assert ("torchrun --nnodes 1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29500 main.py "
+            "--lr=0.01 --batch-size 8 --config-file ./dpwa.yaml") in run
+    assert os.stat(tmp_path / "run.sh").st_mode & stat.S_IEXEC
+    name, dev = node_for_rank(str(cfg), rank=2)
+    assert name == "w2" and dev.index == 2
+    with pytest.raises(ValueError):
+        node_for_rank(str(cfg), rank=4)
+
+
+def test_gpu_key_places_the_node(tmp_path):
+    """A node's gpu: key is checked against its parameters' device at bind time (on the GPU
+    box, tests/test_gpu_configs.py checks the adapter moving a model onto that device)."""
+    import torch
     from dpwa_amd.launch import write_config
-    p = write_config(str(tmp_path / "g.yaml"), ["a", "b"], interpolation="loss", divergence_threshold=0.5)
-    c = DpwaConfiguration(p)
-    assert set(c.config) == {"nodes", "fetch_probability", "timeout_ms", "interpolation", "divergence_threshold",
-                             "constant", "clock", "loss"}
+    p = write_config(str(tmp_path / "g.yaml"), ["a", "b"], gpus=[1, 0])
+    conn = DpwaConnection("a", p, group=LocalGroup())
+    with pytest.raises(ValueError, match="gpu 1"):
+        conn.update_send(torch.zeros(4, device="meta"), 1.0)
+    conn.close()

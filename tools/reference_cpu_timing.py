@@ -22,7 +22,9 @@ import time
 REF = os.environ.get("DPWA_REFERENCE", "/root/reference")
 
 
-def learner(name, cfg, numel, rounds, q, threads):
+def learner(name, cfg, numel, rounds, q, threads, core=None):
+    if core is not None:
+        os.sched_setaffinity(0, {core})      # taskset -c <core> (prepare.py:31)
     os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
     sys.dont_write_bytecode = True
     sys.path.insert(0, REF)
@@ -62,7 +64,7 @@ def learner(name, cfg, numel, rounds, q, threads):
     os._exit(0)                          # reference threads never exit (conn.py:170-172)
 
 
-def run(numel, rounds, threads):
+def run(numel, rounds, threads, pin=False):
     with tempfile.TemporaryDirectory() as tmp:
         cfg = os.path.join(tmp, "c.yaml")
         base = 46100 + (numel % 500)
@@ -72,7 +74,9 @@ def run(numel, rounds, threads):
                     "- divergence_threshold: 0\n- constant: { value: 0.5 }\n- clock: 0\n- loss: 0\n" % (base, base + 1))
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
-        ps = [ctx.Process(target=learner, args=(n, cfg, numel, rounds, q, threads)) for n in ("w1", "w2")]
+        cores = sorted(os.sched_getaffinity(0))[:2] if pin else [None, None]
+        ps = [ctx.Process(target=learner, args=(n, cfg, numel, rounds, q, threads, c))
+              for n, c in zip(("w1", "w2"), cores)]
         for p in ps:
             p.start()
         res = {}
@@ -85,6 +89,8 @@ def run(numel, rounds, threads):
     med = times[len(times) // 2]
     return {"numel": numel, "rounds_per_learner": rounds, "median_round_s": med,
             "averaged_GBps": 3 * numel * 4 / med / 1e9,
+            "averaged_GBps_both_learners": 2 * 3 * numel * 4 / med / 1e9,
+            "pinned_cores": cores,
             "mean_send_s": (res["w1"][1]["send"] + res["w2"][1]["send"]) / (2 * rounds),
             "mean_wait_s": (res["w1"][1]["wait"] + res["w2"][1]["wait"]) / (2 * rounds)}
 
@@ -95,14 +101,29 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--threads", type=int, default=1, help="torch threads per learner (prepare.py:31 uses 1)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--pin", action="store_true", help="pin each learner to its own core (taskset, prepare.py:31)")
+    ap.add_argument("--port-seconds", type=float, default=0.0,
+                    help="also time oracle/ref_round.py (the restatement bench.py runs on the GPU box) at the same "
+                         "sizes, and report the port/reference round-time ratio")
     args = ap.parse_args()
-    rows = [run(n, args.rounds if n < 50_000_000 else max(3, args.rounds // 2), args.threads) for n in args.numel]
+    rows = [run(n, args.rounds if n < 50_000_000 else max(3, args.rounds // 2), args.threads, args.pin)
+            for n in args.numel]
     out = {"what": "reference dpwa CPU round (update_send + update_wait) between 2 localhost learners: "
                    "TCP + pickle + torch-CPU lerp, fp32, constant 0.5, fetch_probability 1",
            "source": "dpwa/adapters/pytorch.py:42-68, dpwa/dpwa.py:104-156, dpwa/conn.py:98-329",
            "host": {"cpus": os.cpu_count(), "machine": platform.processor() or platform.machine(),
                     "torch_threads_per_learner": args.threads},
            "rows": rows}
+    if args.port_seconds > 0:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from oracle import ref_round
+        ports = [ref_round.run(r["numel"], args.port_seconds, min_rounds=3) for r in rows]
+        out["port_rows"] = ports
+        out["port_vs_reference"] = [
+            {"numel": r["numel"], "reference_median_round_ms": round(1e3 * r["median_round_s"], 2),
+             "port_median_round_ms": p["median_round_ms"],
+             "port_over_reference_rate": round(1e3 * r["median_round_s"] / p["median_round_ms"], 3)}
+            for r, p in zip(rows, ports)]
     print(json.dumps(out, indent=1))
     if args.out:
         with open(args.out, "w") as f:
