@@ -150,6 +150,16 @@ __device__ __forceinline__ void factor_commit(const FusedArgs &fa, const dpwa_co
     *fa.clock_out = c.new_clock;                       // dpwa.py:155 (unchanged on error)
     *fa.coef_out = c;
     if (fa.status_mirror && c.status != DPWA_STATUS_OK) *fa.status_mirror = c.status;   // sticky
+    if (fa.next_header) {                              // the next publish's state, written ahead
+        const double next = c.new_clock + 1.0;         // dpwa.py:112 of that publish
+        *fa.clock_next = next;
+        dpwa_header *h = fa.next_header;
+        h->clock = next;
+        h->loss = __builtin_nan("");
+        h->version = fa.next_version;
+        h->n = fa.n;
+        h->dtype = fa.dtype;
+    }
 }
 
 __global__ void k_factor(FusedArgs fa)
@@ -583,6 +593,12 @@ hipError_t launch_relay(int phase, const RelayArgs &a, int blocks_per_part, hipS
 __global__ __launch_bounds__(64) void k_release_system()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+hipError_t launch_release_system(hipStream_t s)
+{
+    hipLaunchKernelGGL(k_release_system, dim3(256), dim3(64), 0, s);
+    return hipGetLastError();
 }
 
 // Workgroup size of the snapshot copy; DPWA_PUBLISH_BLOCK (64/128/256) forces another.

@@ -26,6 +26,15 @@ struct FusedArgs {
     const double *loss_d;
     dpwa_coef *coef_out;
     int32_t *status_mirror;     // nullable device-visible pinned host word (sticky errors)
+    // Write-through averages (the next publish then moves no bytes): the header of the next
+    // snapshot {new clock + 1, version, n, dtype; loss NaN -- the peers' factor math reads a
+    // peer's loss only under loss interpolation, which keeps the header publish} and that
+    // clock into *clock_next.  Null: nothing beyond the average.
+    dpwa_header *next_header;
+    double *clock_next;
+    uint64_t next_version;
+    int64_t n;
+    int32_t dtype;
 };
 
 // Lerp over n elements; coefficients from `coef` (device) or, when coef is null, from (a, b).
@@ -75,6 +84,10 @@ hipError_t launch_relay(int phase, const RelayArgs &a, int blocks_per_part, hipS
 // Publish of the header only (the payload was written through by the last average).
 hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *clock, double loss,
                                  const double *loss_dev, uint64_t version, bool system_release, hipStream_t s);
+
+// A system-scope L2 write-back on every XCD after the work already on `s` (a publish whose
+// bytes were written by an earlier kernel, read by other devices).
+hipError_t launch_release_system(hipStream_t s);
 
 // A system-scope release store of one 64-bit word after the work already on `s`.
 hipError_t launch_store_u64(uint64_t *p, uint64_t v, hipStream_t s);

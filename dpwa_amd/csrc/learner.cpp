@@ -67,7 +67,9 @@ struct IpcBlob {
 static_assert(sizeof(IpcBlob) <= DPWA_IPC_HANDLE_BYTES, "IPC blob too large");
 
 struct Ctl {            // device control block
-    double clock[2];    // double-buffered: a factor reads clock[cur] and writes clock[cur^1]
+    double clock[4];    // a ring: a factor reads clock[cur] and writes clock[cur+1]; a
+                        // write-through average also writes the next publish's clock+1 into
+                        // clock[cur+2], which that publish then selects without a kernel
     dpwa_coef coef;
 };
 
@@ -117,7 +119,7 @@ struct dpwa_learner {
     char *staging = nullptr;        // 1 slot
     Ctl *ctl = nullptr;
     uint64_t version = 0;
-    int cur = 0;                        // index of the live clock in ctl->clock
+    int cur = 0;                        // index of the live clock in ctl->clock (mod 4)
     bool exported = false;
     hipStream_t side = nullptr;
     // Cross-stream ordering is recorded lazily: the stream of every publish / consumption is
@@ -138,6 +140,7 @@ struct dpwa_learner {
     int pull_mode = DPWA_PULL_COPY_ENGINE;   // how cross-device fetches move bytes
     int pull_blocks = 512;
     bool wt_valid = false;
+    bool wt_header = false;             // the write-through average also wrote the next header
     const void *wt_flat = nullptr;
     hipStream_t wt_stream = nullptr;
     hipEvent_t ev_wt = nullptr;
@@ -223,7 +226,14 @@ int dpwa_factor(const dpwa_interp *cfg, double *clock_dev, const dpwa_header *pe
 {
     if (!cfg || !clock_dev || !peer_header_dev || !coef_dev) return set_error(DPWA_ERR_ARG, "dpwa_factor: NULL argument");
     if (cfg->method < 0 || cfg->method > 2) return set_error(DPWA_ERR_ARG, "dpwa_factor: unknown method %d", cfg->method);
-    FusedArgs fa{*cfg, clock_dev, clock_dev, peer_header_dev, loss, loss_dev, coef_dev, nullptr};
+    FusedArgs fa{};
+    fa.cfg = *cfg;
+    fa.clock_in = clock_dev;
+    fa.clock_out = clock_dev;
+    fa.hdr = peer_header_dev;
+    fa.loss_h = loss;
+    fa.loss_d = loss_dev;
+    fa.coef_out = coef_dev;
     HIP_TRY(launch_factor(fa, (hipStream_t)stream));
     return DPWA_OK;
 }
@@ -236,7 +246,13 @@ int dpwa_average(int32_t dtype, void *param, const void *peer_slot, int64_t n, c
         (!start_event) != (!stop_event))
         return set_error(DPWA_ERR_ARG, "dpwa_average: bad arguments");
     if (cfg->method < 0 || cfg->method > 2) return set_error(DPWA_ERR_ARG, "dpwa_average: unknown method %d", cfg->method);
-    FusedArgs fa{*cfg, clock_dev, clock_dev + 1, (const dpwa_header *)peer_slot, loss, nullptr, coef_dev, nullptr};
+    FusedArgs fa{};
+    fa.cfg = *cfg;
+    fa.clock_in = clock_dev;
+    fa.clock_out = clock_dev + 1;
+    fa.hdr = (const dpwa_header *)peer_slot;
+    fa.loss_h = loss;
+    fa.coef_out = coef_dev;
     LaunchTiming t{(hipEvent_t)start_event, (hipEvent_t)stop_event};
     HIP_TRY(launch_average(dtype, param, (const char *)peer_slot + kHeader, n, fa, snap_payload, (hipStream_t)stream,
                            start_event ? &t : nullptr));
@@ -367,7 +383,21 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
     const int k = (int)(l->version % 2);   // slot of publish number version+1
     char *slot = l->slots + (size_t)k * l->slot_stride;
     const bool header_only = reuse && l->wt_valid && l->wt_flat == flat;
-    if (header_only) {
+    hipStream_t produced_on = s;
+    if (header_only && l->wt_header) {
+        // payload, header and clock of this publish were written by the last average: nothing
+        // moves (IPC-exported slots still get their system-scope write-back)
+        if (l->exported) {
+            if (l->wt_stream != s) {
+                HIP_TRY(hipEventRecord(l->ev_wt, l->wt_stream));
+                HIP_TRY(hipStreamWaitEvent(s, l->ev_wt, 0));
+            }
+            HIP_TRY(launch_release_system(s));
+        } else {
+            produced_on = l->wt_stream;
+        }
+        l->cur = (l->cur + 1) & 3;
+    } else if (header_only) {
         // the payload was written by the last average (readers of slot k were waited for then)
         if (l->wt_stream != s) {
             HIP_TRY(hipEventRecord(l->ev_wt, l->wt_stream));
@@ -382,8 +412,9 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
                                loss_dev, l->version + 1, l->exported, s));
     }
     l->wt_valid = false;
+    l->wt_header = false;
     std::lock_guard<std::mutex> g(l->pub_mu);
-    l->publish_stream[k] = s;
+    l->publish_stream[k] = produced_on;
     l->published[k] = true;
     l->version++;
     return DPWA_OK;
@@ -543,8 +574,16 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
 
 static FusedArgs fused_args(dpwa_learner *l, double loss, const double *loss_dev)
 {
-    return FusedArgs{l->cfg, &l->ctl->clock[l->cur], &l->ctl->clock[l->cur ^ 1], (const dpwa_header *)l->src,
-                     loss, loss_dev, &l->ctl->coef, l->host_status_dev};
+    FusedArgs fa{};
+    fa.cfg = l->cfg;
+    fa.clock_in = &l->ctl->clock[l->cur];
+    fa.clock_out = &l->ctl->clock[(l->cur + 1) & 3];
+    fa.hdr = (const dpwa_header *)l->src;
+    fa.loss_h = loss;
+    fa.loss_d = loss_dev;
+    fa.coef_out = &l->ctl->coef;
+    fa.status_mirror = l->host_status_dev;
+    return fa;
 }
 
 int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dpwa_stream_t stream)
@@ -559,7 +598,7 @@ int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dp
     HIP_TRY(hipEventRecord(l->ev_factor, s));
     l->consume_stream = s;   // the header has been read on s
     l->consumed_once = true;
-    l->cur ^= 1;
+    l->cur = (l->cur + 1) & 3;
     l->have_factor = true;
     return DPWA_OK;
 }
@@ -590,22 +629,31 @@ static int average_impl(dpwa_learner *l, void *flat, double loss, const double *
 {
     if (!l->have_fetch || l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_average: no fetch in flight");
     char *snap = nullptr;
+    FusedArgs fa = fused_args(l, loss, loss_dev);
     if (write_through) {
         const int k = (int)(l->version % 2);   // slot of the next publish
         int rc = wait_slot_readers(l, k, s);
         if (rc) return rc;
         snap = l->slots + (size_t)k * l->slot_stride + kHeader;
+        if (l->cfg.method != DPWA_INTERP_LOSS) {   // peers never read this header's loss
+            fa.next_header = (dpwa_header *)(snap - kHeader);
+            fa.clock_next = &l->ctl->clock[(l->cur + 2) & 3];
+            fa.next_version = l->version + 1;
+            fa.n = l->n;
+            fa.dtype = l->dtype;
+        }
     }
     if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
     const LaunchTiming *timing = nullptr;
     if (l->timing_armed && l->timing_used < (int)l->timing.size() && ((uintptr_t)flat & 15) == 0)
         timing = &l->timing[l->timing_used++];
     l->timing_armed = false;
-    HIP_TRY(launch_average(l->dtype, flat, l->src + kHeader, l->n, fused_args(l, loss, loss_dev), snap, s, timing));
+    HIP_TRY(launch_average(l->dtype, flat, l->src + kHeader, l->n, fa, snap, s, timing));
     l->consume_stream = s;
     l->consumed_once = true;
-    l->cur ^= 1;
+    l->cur = (l->cur + 1) & 3;
     l->wt_valid = write_through;
+    l->wt_header = fa.next_header != nullptr;
     l->wt_flat = flat;
     l->wt_stream = s;
     finish_fetch(l);
