@@ -138,6 +138,7 @@ SIGNATURES = {
     "dpwa_node_update_send": [_vp, _vp, _dbl, _vp, _int, _vp, _pint],
     "dpwa_node_publish": [_vp, _vp, _dbl, _vp, _int, _vp],
     "dpwa_node_gate": [_vp, _int, _vp, _pint],
+    "dpwa_node_start_fetch": [_vp, _int, _vp],
     "dpwa_node_update_wait": [_vp, _dbl, _vp, _int, _vp, _pint],
     "dpwa_node_lerp": [_vp, _vp, _vp],
     "dpwa_node_update_wait_average": [_vp, _vp, _dbl, _vp, _int, _vp, _pint],

@@ -299,6 +299,13 @@ int dpwa_node_update_send(dpwa_node *n, const void *flat, double loss, const dou
     return dpwa_node_gate(n, flags, stream, fetching);
 }
 
+int dpwa_node_start_fetch(dpwa_node *n, int flags, dpwa_stream_t stream)
+{
+    if (!n || !n->learner) return set_error(DPWA_ERR_STATE, "dpwa_node_start_fetch: node not bound");
+    if (!n->fetching || n->fetch_started) return DPWA_OK;
+    return start_fetch(n, flags, stream);
+}
+
 // dpwa.py:130-137: *peer = -1 means (None, 0).
 static int finish_fetch(dpwa_node *n, int flags, dpwa_stream_t stream, int *peer)
 {

@@ -299,6 +299,8 @@ class DpwaConnection:
             self._fail("dpwa_node_update_send", rc)
         learner.version += 1
         self.fetching = bool(self._out.value)
+        if not self._eager and getattr(self._group, "prefetch", False):
+            self._group.after_update_send(self)
 
     def update_wait(self, loss):
         """dpwa.py:125-156: (None, 0) when not fetching or no peer delivered; otherwise the

@@ -28,8 +28,11 @@ from . import _lib
 
 
 class LocalGroup:
+    """prefetch: once every learner of the group has published the round, start all granted
+    fetches at once on the learners' side streams, so the pulls overlap the training step that
+    follows (worth it when peers live on other GPUs of this process; lock-step semantics are
+    unchanged).  zero_copy=False makes same-device fetches copy into staging too."""
     eager_fetch = False
-    zero_copy = True
     _registry = {}
     _lock = threading.Lock()
 
@@ -42,8 +45,10 @@ class LocalGroup:
                 g = cls._registry[key] = cls()
             return g
 
-    def __init__(self):
+    def __init__(self, prefetch=False, zero_copy=True):
         self.members = {}
+        self.prefetch = prefetch
+        self.zero_copy = zero_copy
 
     def member(self, name):
         ref = self.members.get(name)
@@ -81,6 +86,20 @@ class LocalGroup:
 
     def after_gate(self, conn):
         pass
+
+    def after_update_send(self, conn):
+        if not self.prefetch:
+            return
+        members = [self.member(n) for n in list(self.members)]
+        members = [m for m in members if m is not None]
+        if any(m._learner is None for m in members):
+            return
+        v = conn._learner.version
+        if any(m._learner.version != v for m in members):
+            return                      # someone has not published this round yet
+        for m in members:
+            if m.fetching:
+                _lib.call("dpwa_node_start_fetch", m._node, m._flags, m._raw_stream(m._learner.device.index))
 
 
 class DistGroup:

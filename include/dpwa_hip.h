@@ -358,6 +358,10 @@ int dpwa_node_update_send(dpwa_node *n, const void *flat, double loss, const dou
 int dpwa_node_publish(dpwa_node *n, const void *flat, double loss, const double *loss_dev, int flags,
                       dpwa_stream_t stream);
 int dpwa_node_gate(dpwa_node *n, int flags, dpwa_stream_t stream, int *fetching);
+/* Starts the fetch a non-eager gate granted (TxThread.run, conn.py:277-315), now instead of at
+ * update_wait: a group of co-resident learners calls it once every learner of the round has
+ * published, so the pull overlaps the training step (no-op when nothing is pending). */
+int dpwa_node_start_fetch(dpwa_node *n, int flags, dpwa_stream_t stream);
 /* update_wait (dpwa.py:125-156): *peer = the peer averaged with, or -1 for (None, 0).
  * _average fuses the adapter's lerp (pytorch.py:66-68) into the same kernel; the split
  * form computes the factor only and dpwa_node_lerp applies it. */

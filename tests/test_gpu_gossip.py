@@ -383,3 +383,37 @@ def test_kernel_dispatch_timing(tmp_path):
     _lib.call("dpwa_learner_time_averages", h, 0)
     for c in conns:
         c.close()
+
+
+@pytest.mark.parametrize("zero_copy,pull", [(False, "kernel:256"), (False, "copy"), (True, "copy")])
+def test_prefetching_local_group_matches_oracle(tmp_path, zero_copy, pull):
+    """LocalGroup(prefetch=True): every granted fetch starts on the learners' side streams as
+    soon as the whole round has published, so it overlaps the training step that follows
+    (tools/overlap_trace.py); the trajectory stays the lock-step one."""
+    rng = np.random.default_rng(19)
+    G, n, T = 3, 200_003, 8
+    names = ["p%d" % g for g in range(G)]
+    init = rng.standard_normal((G, n)).astype(np.float32)
+    deltas = (0.01 * rng.standard_normal((T, G, n))).astype(np.float32)
+    send = [[1.0 + 0.1 * g + r for g in range(G)] for r in range(T)]
+    wait = [[1.5 + 0.1 * g + r for g in range(G)] for r in range(T)]
+    seeds = [41 + g for g in range(G)]
+    exp = ogossip.simulate(names, init, deltas, send, wait, "clock", None, 0.0, 0.8, seeds)
+    cfg = tmp_path / "pre.yaml"
+    write_cfg(cfg, names, 0.8, "clock", 0.0, None)
+    group = LocalGroup(prefetch=True, zero_copy=zero_copy)
+    flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
+    conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group, pull=pull) for g in range(G)]
+    for r in range(T):
+        for g in range(G):
+            conns[g].update_send(flats[g], send[r][g], reuse_snapshot=r > 0)
+        for g in range(G):
+            torch.cuda._sleep(200_000)                       # a "training step" behind the pulls
+            flats[g].add_(torch.from_numpy(deltas[r, g]).to(DEV))
+        for g in range(G):
+            conns[g].update_wait_average(flats[g], wait[r][g], write_through=True)
+        for g in range(G):
+            assert olerp.bits_equal(flats[g].cpu().numpy(), exp["params"][r, g]), (r, g)
+            assert conns[g].clock == exp["clocks"][r, g]
+    for c in conns:
+        c.close()
