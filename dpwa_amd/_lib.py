@@ -20,7 +20,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dpwa_hip.h")
 # Constants mirrored from include/dpwa_hip.h
 ABI_VERSION = 1
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_NOMEM = 0, -1, -2, -3, -4
-F32, BF16 = 0, 1
+F32, BF16, F64 = 0, 1, 2
 INTERP_CONSTANT, INTERP_CLOCK, INTERP_LOSS = 0, 1, 2
 STATUS_OK, STATUS_ZERO_DIVISION = 0, 1
 IPC_HANDLE_BYTES = 128
@@ -95,6 +95,7 @@ SIGNATURES = {
     "dpwa_learner_lerp": [_vp, _vp, _vp],
     "dpwa_learner_cancel": [_vp],
     "dpwa_learner_set_pull": [_vp, _int, _int],
+    "dpwa_learner_set_loss_dtype": [_vp, _i32],
     "dpwa_learner_wait_fetch": [_vp, _vp],
     "dpwa_learner_read_snapshot": [_vp, _vp, _vp, _i64, ctypes.POINTER(_u64)],
     "dpwa_learner_relay_enable": [_vp, _int, _int],

@@ -105,6 +105,14 @@ struct OpsBF16 {
     }
 };
 
+// The loss given to update_send / update_wait: a host double, or read on the device from a
+// float64 or float32 scalar (a loss tensor, so the host never synchronises).
+__device__ __forceinline__ double read_loss(const double *d, int32_t f32, double h)
+{
+    if (!d) return h;
+    return f32 ? (double)*reinterpret_cast<const float *>(d) : *d;
+}
+
 // ---------------------------------------------------------------- factor math
 // dpwa.py:139-155 in IEEE double with every operation separately rounded, exactly as
 // CPython evaluates it.  Python raises ZeroDivisionError on x/0.0; here that is status 1,
@@ -165,7 +173,7 @@ __device__ __forceinline__ void factor_commit(const FusedArgs &fa, const dpwa_co
 __global__ void k_factor(FusedArgs fa)
 {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    const double loss = fa.loss_d ? *fa.loss_d : fa.loss_h;
+    const double loss = read_loss(fa.loss_d, fa.loss_f32, fa.loss_h);
     const dpwa_coef c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, loss);
     factor_commit(fa, c);
 }
@@ -261,7 +269,7 @@ __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ pa
         __shared__ int s_ok;
         if (threadIdx.x < 64) {  // wave 0: fp64 factor while the loads are in flight
             const FusedArgs &fa = args.fused;
-            const double loss = fa.loss_d ? *fa.loss_d : fa.loss_h;
+            const double loss = read_loss(fa.loss_d, fa.loss_f32, fa.loss_h);
             const dpwa_coef c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, loss);
             if (threadIdx.x == 0) {
                 s_a = c.a;
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(kBlock) void k_lerp_unaligned(typename Ops::S *__re
         b = args.coef->b;
     } else {
         const FusedArgs &fa = args.fused;
-        const double loss = fa.loss_d ? *fa.loss_d : fa.loss_h;
+        const double loss = read_loss(fa.loss_d, fa.loss_f32, fa.loss_h);
         const dpwa_coef c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, loss);
         if (blockIdx.x == 0 && threadIdx.x == 0) factor_commit(fa, c);
         if (c.status != DPWA_STATUS_OK) {
@@ -448,7 +456,8 @@ template <bool VEC, int BLOCK = kBlock>
 __global__ __launch_bounds__(BLOCK) void k_publish(char *__restrict__ slot, const char *__restrict__ flat,
                                                    int64_t nbytes, int64_t n, int32_t dtype,
                                                    double *__restrict__ clock, double loss_h,
-                                                   const double *__restrict__ loss_d, uint64_t version)
+                                                   const double *__restrict__ loss_d, int32_t loss_f32,
+                                                   uint64_t version)
 {
     char *payload = slot + sizeof(dpwa_header);
     if (VEC) {   // one 16-B item per lane, streaming policy of the lerp (nt loads, sc1 stores)
@@ -471,7 +480,7 @@ __global__ __launch_bounds__(BLOCK) void k_publish(char *__restrict__ slot, cons
         const double c = *clock + 1.0;                 // dpwa.py:112  self.clock += 1
         *clock = c;
         h->clock = c;                                  // dpwa.py:115  state = {'clock', 'loss'}
-        h->loss = loss_d ? *loss_d : loss_h;
+        h->loss = read_loss(loss_d, loss_f32, loss_h);
         h->version = version;
         h->n = n;
         h->dtype = dtype;
@@ -613,7 +622,8 @@ static int publish_block()
 }
 
 hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t n, int32_t dtype, double *clock,
-                          double loss, const double *loss_dev, uint64_t version, bool system_release, hipStream_t s)
+                          double loss, const double *loss_dev, bool loss_f32, uint64_t version, bool system_release,
+                          hipStream_t s)
 {
     const char *src = (const char *)flat;
     if (aligned16(flat)) {
@@ -622,18 +632,18 @@ hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t 
         const int64_t g = n16 / b + 1;
         if (b == 64)
             hipLaunchKernelGGL((k_publish<true, 64>), dim3((uint32_t)g), dim3(64), 0, s, slot, src, nbytes, n, dtype,
-                               clock, loss, loss_dev, version);
+                               clock, loss, loss_dev, (int32_t)loss_f32, version);
         else if (b == 128)
             hipLaunchKernelGGL((k_publish<true, 128>), dim3((uint32_t)g), dim3(128), 0, s, slot, src, nbytes, n,
-                               dtype, clock, loss, loss_dev, version);
+                               dtype, clock, loss, loss_dev, (int32_t)loss_f32, version);
         else
             hipLaunchKernelGGL((k_publish<true>), dim3((uint32_t)g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype,
-                               clock, loss, loss_dev, version);
+                               clock, loss, loss_dev, (int32_t)loss_f32, version);
     } else {
         int64_t g = blocks_for(nbytes);
         if (g > 8192) g = 8192;
         hipLaunchKernelGGL((k_publish<false>), dim3((uint32_t)g), dim3(kBlock), 0, s, slot, src, nbytes, n, dtype,
-                           clock, loss, loss_dev, version);
+                           clock, loss, loss_dev, (int32_t)loss_f32, version);
     }
     if (system_release) hipLaunchKernelGGL(k_release_system, dim3(256), dim3(64), 0, s);
     return hipGetLastError();
@@ -642,23 +652,24 @@ hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t 
 // Header-only publish: the payload of `slot` was already written by a write-through
 // average of exactly these parameters.
 __global__ void k_publish_header(char *__restrict__ slot, int64_t n, int32_t dtype, double *__restrict__ clock,
-                                 double loss_h, const double *__restrict__ loss_d, uint64_t version)
+                                 double loss_h, const double *__restrict__ loss_d, int32_t loss_f32, uint64_t version)
 {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     dpwa_header *h = reinterpret_cast<dpwa_header *>(slot);
     const double c = *clock + 1.0;                     // dpwa.py:112
     *clock = c;
     h->clock = c;
-    h->loss = loss_d ? *loss_d : loss_h;
+    h->loss = read_loss(loss_d, loss_f32, loss_h);
     h->version = version;
     h->n = n;
     h->dtype = dtype;
 }
 
 hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *clock, double loss,
-                                 const double *loss_dev, uint64_t version, bool system_release, hipStream_t s)
+                                 const double *loss_dev, bool loss_f32, uint64_t version, bool system_release,
+                                 hipStream_t s)
 {
-    hipLaunchKernelGGL(k_publish_header, dim3(1), dim3(64), 0, s, slot, n, dtype, clock, loss, loss_dev, version);
+    hipLaunchKernelGGL(k_publish_header, dim3(1), dim3(64), 0, s, slot, n, dtype, clock, loss, loss_dev, (int32_t)loss_f32, version);
     if (system_release) hipLaunchKernelGGL(k_release_system, dim3(256), dim3(64), 0, s);
     return hipGetLastError();
 }

@@ -23,7 +23,8 @@ struct FusedArgs {
     double *clock_out;
     const dpwa_header *hdr;     // the peer's published state
     double loss_h;              // used when loss_d is null
-    const double *loss_d;
+    const double *loss_d;       // a device float64, or a float32 when loss_f32
+    int32_t loss_f32;
     dpwa_coef *coef_out;
     int32_t *status_mirror;     // nullable device-visible pinned host word (sticky errors)
     // Write-through averages (the next publish then moves no bytes): the header of the next
@@ -59,7 +60,7 @@ hipError_t launch_factor(const FusedArgs &fa, hipStream_t s);
 // `system_release` follows it with a system-scope L2 write-back on every XCD so other
 // devices (IPC peers) read the bytes from HBM.
 hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t n, int32_t dtype,
-                          double *clock, double loss, const double *loss_dev, uint64_t version,
+                          double *clock, double loss, const double *loss_dev, bool loss_f32, uint64_t version,
                           bool system_release, hipStream_t s);
 // Pull of `nbytes` (multiple of 16, 16-B aligned) from a peer's slot into local staging with
 // a copy kernel of at most `max_blocks` workgroups.  `remote`: the source is another GPU's
@@ -83,7 +84,8 @@ struct RelayArgs {
 hipError_t launch_relay(int phase, const RelayArgs &a, int blocks_per_part, hipStream_t s);
 // Publish of the header only (the payload was written through by the last average).
 hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *clock, double loss,
-                                 const double *loss_dev, uint64_t version, bool system_release, hipStream_t s);
+                                 const double *loss_dev, bool loss_f32, uint64_t version, bool system_release,
+                                 hipStream_t s);
 
 // A system-scope L2 write-back on every XCD after the work already on `s` (a publish whose
 // bytes were written by an earlier kernel, read by other devices).

@@ -139,6 +139,7 @@ struct dpwa_learner {
     // next publish (for the flat buffer `wt_flat`, on stream `wt_stream`)
     int pull_mode = DPWA_PULL_COPY_ENGINE;   // how cross-device fetches move bytes
     int pull_blocks = 512;
+    bool loss_f32 = false;              // device loss pointers point at a float32
     bool wt_valid = false;
     bool wt_header = false;             // the write-through average also wrote the next header
     const void *wt_flat = nullptr;
@@ -403,13 +404,13 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
             HIP_TRY(hipEventRecord(l->ev_wt, l->wt_stream));
             HIP_TRY(hipStreamWaitEvent(s, l->ev_wt, 0));
         }
-        HIP_TRY(launch_publish_header(slot, l->n, l->dtype, &l->ctl->clock[l->cur], loss, loss_dev, l->version + 1,
-                                      l->exported, s));
+        HIP_TRY(launch_publish_header(slot, l->n, l->dtype, &l->ctl->clock[l->cur], loss, loss_dev, l->loss_f32,
+                                      l->version + 1, l->exported, s));
     } else {
         int rc = wait_slot_readers(l, k, s);
         if (rc) return rc;
         HIP_TRY(launch_publish(slot, flat, (int64_t)l->payload_bytes, l->n, l->dtype, &l->ctl->clock[l->cur], loss,
-                               loss_dev, l->version + 1, l->exported, s));
+                               loss_dev, l->loss_f32, l->version + 1, l->exported, s));
     }
     l->wt_valid = false;
     l->wt_header = false;
@@ -581,6 +582,7 @@ static FusedArgs fused_args(dpwa_learner *l, double loss, const double *loss_dev
     fa.hdr = (const dpwa_header *)l->src;
     fa.loss_h = loss;
     fa.loss_d = loss_dev;
+    fa.loss_f32 = l->loss_f32 ? 1 : 0;
     fa.coef_out = &l->ctl->coef;
     fa.status_mirror = l->host_status_dev;
     return fa;
@@ -972,6 +974,13 @@ int dpwa_learner_wait_fetch(dpwa_learner *l, dpwa_stream_t stream)
         DeviceGuard dg(l->device);
         HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, l->ev_fetched, 0));
     }
+    return DPWA_OK;
+}
+
+int dpwa_learner_set_loss_dtype(dpwa_learner *l, int32_t dtype)
+{
+    if (!l || (dtype != DPWA_F32 && dtype != DPWA_F64)) return set_error(DPWA_ERR_ARG, "dpwa_learner_set_loss_dtype: bad arguments");
+    l->loss_f32 = dtype == DPWA_F32;
     return DPWA_OK;
 }
 

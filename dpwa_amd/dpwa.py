@@ -281,7 +281,7 @@ class DpwaConnection:
         elif learner.take_status():
             self._zero_division()
         p = learner._ptr(parameters)
-        h, d, learner._keep = loss_args(loss, learner.device)
+        h, d, learner._keep = learner.loss_args(loss)
         s = self._raw_stream(learner.device.index)
         flags = self._flags | (_lib.FLAG_REUSE_SNAPSHOT if reuse_snapshot else 0)
         if self._eager:      # DistGroup: publish, stream-ordered barrier, gate + eager pull
@@ -310,7 +310,7 @@ class DpwaConnection:
             return None, 0
         if learner.take_status():
             self._zero_division()
-        h, d, learner._keep = loss_args(loss, learner.device)
+        h, d, learner._keep = learner.loss_args(loss)
         rc = self._f_wait(self._node, h, d, self._flags, self._raw_stream(learner.device.index), self._out_ref)
         if rc:
             self._fail("dpwa_node_update_wait", rc)
@@ -331,7 +331,7 @@ class DpwaConnection:
         if learner.take_status():
             self._zero_division()
         p = learner._ptr(parameters)
-        h, d, learner._keep = loss_args(loss, learner.device)
+        h, d, learner._keep = learner.loss_args(loss)
         flags = self._flags | (_lib.FLAG_WRITE_THROUGH if write_through else 0)
         rc = self._f_wait_avg(self._node, p, h, d, flags, self._raw_stream(learner.device.index), self._out_ref)
         if rc:

@@ -52,6 +52,8 @@ class FlatParameters:
     def resync(self):
         """Re-homes parameters whose ``.data`` was replaced since the last call (e.g. a
         user assigned ``param.data = ...``); returns the number re-homed."""
+        if [p.data_ptr() for p in self.params] == self._ptrs:
+            return 0          # the common case: one pointer read per parameter
         moved = 0
         with torch.no_grad():
             for i, (p, o) in enumerate(zip(self.params, self.offsets)):

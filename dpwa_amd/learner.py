@@ -54,6 +54,7 @@ class Learner:
         self._status = ctypes.c_int32.from_address(word.value)
         self.version = 0                 # publishes so far (mirrors dpwa_learner_version)
         self._keep = None
+        self._loss_dtype = _lib.F64      # what device loss pointers point at (native side)
         self._checked = None             # (id, data_ptr) of the last validated flat tensor
         self._f_publish = lib.dpwa_learner_publish
         self._f_fetch = lib.dpwa_learner_fetch
@@ -64,6 +65,23 @@ class Learner:
     @property
     def handle(self):
         return self._h
+
+    def loss_args(self, loss):
+        """(host double, device pointer or None, keep-alive) for a loss given as a number or a
+        device tensor.  A one-element float32/float64 tensor on this learner's device is read
+        by the kernels in place (no conversion kernel, no host sync); anything else on a GPU
+        is converted to a float64 scalar first."""
+        if isinstance(loss, torch.Tensor) and loss.device.type == "cuda":
+            if loss.device == self.device and loss.numel() == 1 and loss.dtype in (torch.float32, torch.float64):
+                want = _lib.F32 if loss.dtype == torch.float32 else _lib.F64
+                if want != self._loss_dtype:
+                    _lib.call("dpwa_learner_set_loss_dtype", self._h, want)
+                    self._loss_dtype = want
+                return 0.0, _c_void_p(loss.data_ptr()), loss
+            if self._loss_dtype != _lib.F64:
+                _lib.call("dpwa_learner_set_loss_dtype", self._h, _lib.F64)
+                self._loss_dtype = _lib.F64
+        return loss_args(loss, self.device)
 
     def close(self):
         if self._owned and self._h is not None and self._h.value and _lib._lib is not None:
@@ -91,7 +109,7 @@ class Learner:
 
     def publish(self, flat, loss, stream):
         p = self._ptr(flat)
-        h, d, self._keep = loss_args(loss, self.device)
+        h, d, self._keep = self.loss_args(loss)
         rc = self._f_publish(self._h, p, h, d, stream.cuda_stream)
         if rc:
             self._fail("dpwa_learner_publish", rc)
@@ -121,7 +139,7 @@ class Learner:
             self._fail("dpwa_learner_fetch", rc)
 
     def factor(self, loss, stream):
-        h, d, self._keep = loss_args(loss, self.device)
+        h, d, self._keep = self.loss_args(loss)
         rc = self._f_factor(self._h, h, d, stream.cuda_stream)
         if rc:
             self._fail("dpwa_learner_factor", rc)
@@ -137,7 +155,7 @@ class Learner:
     def average(self, flat, loss, stream):
         """Fused factor + lerp (one kernel)."""
         p = self._ptr(flat)
-        h, d, self._keep = loss_args(loss, self.device)
+        h, d, self._keep = self.loss_args(loss)
         rc = self._f_average(self._h, p, h, d, stream.cuda_stream)
         if rc:
             self._fail("dpwa_learner_average", rc)

@@ -38,6 +38,7 @@ extern "C" {
 /* element types of the flat parameter buffer */
 #define DPWA_F32 0            /* the reference's only type: TYPE_CONVERSION, pytorch.py:11-14 */
 #define DPWA_BF16 1           /* extension: torch-eager bf16 rounding, no reference path      */
+#define DPWA_F64 2            /* loss scalars only (dpwa_learner_set_loss_dtype)              */
 
 /* interpolation methods: INTERPOLATION_METHODS, dpwa/dpwa.py:11-15 */
 #define DPWA_INTERP_CONSTANT 0   /* interpolation.py:8-15  factor = value                       */
@@ -228,6 +229,11 @@ int dpwa_learner_wait_fetch(dpwa_learner *l, dpwa_stream_t stream);
 /* How a copying fetch (any non-zero-copy fetch) moves its bytes: DPWA_PULL_COPY_ENGINE
  * (hipMemcpyAsync on the side stream, the default) or DPWA_PULL_KERNEL (a copy kernel of at
  * most max_blocks workgroups reading the IPC-mapped peer slot over xGMI). */
+/* What a device loss pointer (`loss_dev` of publish / factor / average) points at: a float64
+ * (DPWA_F64, the default) or a float32 (DPWA_F32: e.g. a training loss tensor passed as is,
+ * widened exactly on the device as Python's float() widens it). */
+int dpwa_learner_set_loss_dtype(dpwa_learner *l, int32_t dtype);
+
 #define DPWA_PULL_COPY_ENGINE 0
 #define DPWA_PULL_KERNEL 1
 int dpwa_learner_set_pull(dpwa_learner *l, int mode, int max_blocks);

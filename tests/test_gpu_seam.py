@@ -73,3 +73,32 @@ def test_device_factor_behaves_like_the_float():
     assert torch.equal(d * t + (1 - d) * p, f * t + (1 - f) * p)
     assert float(d) == f
     assert float(1 - d) == 1 - f and float(d / 2) == f / 2 and float(-d) == -f
+
+
+def test_loss_given_as_float32_float64_tensor_or_number(tmp_path):
+    """update_send/update_wait accept the loss as a Python number, a float64 or a float32
+    device tensor (read in place by the kernels, widened exactly as float() does): the
+    factors and clocks of a loss-interpolated run match the oracle whatever the mix."""
+    from oracle.policy import factor_and_clock
+    cfg = tmp_path / "loss.yaml"
+    write_cfg(cfg, ["a", "b"], 1.0, "loss", 0.5, None)
+    group = LocalGroup()
+    conns = [DpwaConnection(nm, str(cfg), seed=i, group=group) for i, nm in enumerate("ab")]
+    flats = [torch.zeros(1024, device=DEV), torch.ones(1024, device=DEV)]
+    kinds = [lambda x: x, lambda x: torch.tensor(x, dtype=torch.float64, device=DEV),
+             lambda x: torch.tensor(x, dtype=torch.float32, device=DEV)]
+    clocks = [0.0, 0.0]
+    for r in range(9):
+        send = [float(np.float32(0.9 ** r + 0.1 * g)) for g in range(2)]
+        wait = [float(np.float32(0.8 ** r + 0.05 * g)) for g in range(2)]
+        for g, c in enumerate(conns):
+            c.update_send(flats[g], kinds[(r + g) % 3](send[g]))
+        pub = [clocks[g] + 1.0 for g in range(2)]
+        for g, c in enumerate(conns):
+            payload, factor = c.update_wait(kinds[(r + 2 * g + 1) % 3](wait[g]))
+            c.average(flats[g])
+            f, clocks[g] = factor_and_clock("loss", None, 0.5, pub[g], pub[1 - g], wait[g], send[1 - g])
+            assert float(factor) == f, (r, g)
+            assert c.clock == clocks[g], (r, g)
+    for c in conns:
+        c.close()
