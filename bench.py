@@ -86,8 +86,9 @@ def parse():
                     help="per-learner synthetic training step (bf16 GEMM loop) for the 'overlap' field; 0 = skip")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the parity leg (a short gossip through every transport, checked against the oracle)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01f.json"),
-                    help="PMC traffic summary (rocprofv3 FETCH_SIZE/WRITE_SIZE passes) to report")
+    ap.add_argument("--traffic", default=None,
+                    help="PMC traffic summary (tools/pmc_traffic.py over rocprofv3 FETCH_SIZE/WRITE_SIZE passes of "
+                         "tools/cold_sweep.py) to report; default profiles/traffic_r02_<publish form>.json")
     args = ap.parse_args()
     if args.no_write_through:
         args.publish, args.no_secondary = "full", True
@@ -722,13 +723,14 @@ def main():
         variant = "write-through" if wt_main else "full"
         traffic = None
         traffic_src = None
-        if os.path.exists(args.traffic):
-            with open(args.traffic) as f:
+        tpath = args.traffic or os.path.join(ROOT, "profiles", "traffic_r02_%s.json" % variant)
+        if os.path.exists(tpath):
+            with open(tpath) as f:
                 tr = json.load(f)
             if (tr.get("numel") == args.numel and tr.get("dtype") == args.dtype and
                     tr.get("publish", "full") == variant and tr.get("basis", "in-loop") == ("cold" if cold else "in-loop")):
                 traffic = tr.get("hbm_bytes_per_launch")
-                traffic_src = os.path.relpath(args.traffic, ROOT)
+                traffic_src = os.path.relpath(tpath, ROOT)
         out = {
             "metric": "pairwise-average GB/s (% HBM peak) + gossip rounds/s",
             "value": round(value, 2),

@@ -29,7 +29,7 @@ for b in 8 128; do
       > gpurun_out/resnet18_b$b.json 2> gpurun_out/resnet18_b$b.err || { echo "resnet b$b failed"; tail gpurun_out/resnet18_b$b.err; exit 1; }
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/overlap_$TAG -o ov_%pid% -- \
-    python3 tools/overlap_trace.py --out gpurun_out/overlap_runs > gpurun_out/overlap_$TAG.json 2> gpurun_out/overlap_$TAG.err \
+    python3 tools/overlap_trace.py --batch 128 --steps 30 > gpurun_out/overlap_$TAG.json 2> gpurun_out/overlap_$TAG.err \
     || { echo "overlap trace failed"; tail -30 gpurun_out/overlap_$TAG.err; exit 1; }
 python3 tools/overlap_trace.py --analyze gpurun_out/overlap_$TAG > gpurun_out/overlap_${TAG}_analysis.json || exit 1
 cat gpurun_out/overlap_${TAG}_analysis.json
