@@ -428,7 +428,8 @@ def main():
         g = torch.Generator(device=device).manual_seed(seed)
         flat = torch.randn(args.numel, device=device, generator=g, dtype=torch.float32).to(dtype)
         # under a DistGroup the relay buffers are allocated up front so every transport can be tried
-        conn = DpwaConnection(name, cfg, seed=1000 + seed, group=group, pull="relay" if world > 1 else None)
+        conn = DpwaConnection(name, cfg, seed=1000 + seed, group=group if world == 1 else "lockstep",
+                              pull="relay" if world > 1 else None)
         learners.append((conn, flat))
 
     stream = torch.cuda.current_stream(device)

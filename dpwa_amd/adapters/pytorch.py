@@ -31,7 +31,7 @@ class DpwaPyTorchAdapter:
     ``param.add_``, ``load_state_dict``) and that the flat buffer's own counter did not move;
     any of these forces a full publish.  In-place writes through ``param.data`` bypass version
     counters: a loop that does that between update_wait and update_send must pass
-    ``write_through=False``.  Free-running (gossip-board) rounds always publish in full."""
+    ``write_through=False``."""
 
     def __init__(self, net, name, config_file, write_through=True, transport="device", **connection_kwargs):
         """transport: "device" (peers are learners of this process or of the torch.distributed
@@ -48,9 +48,7 @@ class DpwaPyTorchAdapter:
             self._conn = DpwaConnection(name, config_file, **connection_kwargs)
         else:
             raise ValueError("transport must be 'device' or 'wire'")
-        from ..group import AsyncDistGroup
-        self._write_through = bool(write_through) and transport == "device" and \
-            not isinstance(getattr(self._conn, "_group", None), AsyncDistGroup)
+        self._write_through = bool(write_through) and transport == "device"
         self._versions = None
 
     def _param_versions(self):

@@ -267,11 +267,12 @@ int dpwa_node_publish(dpwa_node *n, const void *flat, double loss, const double 
     n->fetch_started = false;
     n->fetch_peer = -1;
     if (n->board) {   // free-running: wait out readers of the slot we rewrite, then announce
-        if (flags & DPWA_FLAG_REUSE_SNAPSHOT)
-            return set_error(DPWA_ERR_STATE, "write-through snapshots need lock-step rounds, not a board");
+        // (after a write-through average the wait already happened there and returns at once)
         const uint64_t next = learner_version(n->learner) + 1;
         int rc = dpwa_board_publish_wait(n->board, next, n->publish_timeout_ms);
-        if (!rc) rc = dpwa_learner_publish(n->learner, flat, loss, loss_dev, stream);
+        if (!rc)
+            rc = (flags & DPWA_FLAG_REUSE_SNAPSHOT) ? dpwa_learner_publish_reuse(n->learner, flat, loss, loss_dev, stream)
+                                                     : dpwa_learner_publish(n->learner, flat, loss, loss_dev, stream);
         if (!rc) rc = dpwa_board_advertise(n->board, next, stream, 0);
         return rc;
     }
@@ -346,7 +347,13 @@ int dpwa_node_update_wait_average(dpwa_node *n, void *flat, double loss, const d
     int rc = finish_fetch(n, flags, stream, peer);
     if (rc || *peer < 0) return rc;
     if (flags & DPWA_FLAG_WRITE_THROUGH) {
-        if (n->board) return set_error(DPWA_ERR_STATE, "write-through snapshots need lock-step rounds, not a board");
+        if (n->board) {
+            // the average rewrites the slot of the NEXT publish (that of publish v-1): the
+            // board's publish rule -- our publish v is visible, no live reader holds v-1 --
+            // must hold before the kernel is enqueued, not only before the next update_send
+            const int rc = dpwa_board_publish_wait(n->board, learner_version(n->learner) + 1, n->publish_timeout_ms);
+            if (rc) return rc;
+        }
         return dpwa_learner_average_through(n->learner, flat, loss, loss_dev, stream);
     }
     return dpwa_learner_average(n->learner, flat, loss, loss_dev, stream);

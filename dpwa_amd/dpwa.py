@@ -248,7 +248,8 @@ class DpwaConnection:
         elif group == "lockstep":
             from .group import DistGroup
             group = DistGroup(self.nodes, name)
-        self._group = group if group is not None else default_group(config_file, self.nodes, name)
+        self._group = group if group is not None else default_group(config_file, self.nodes, name,
+                                                                    self.config.config.get("gossip"))
         self._eager = bool(self._group.eager_fetch)
         self._flags = (_lib.FLAG_EAGER if self._group.eager_fetch else 0) | \
                       (_lib.FLAG_ZERO_COPY if self._group.zero_copy else 0)

@@ -16,6 +16,8 @@ fetch is a device-to-device pull; a group only wires the native nodes' peer tabl
                 mapped by every peer at the first publish; each round is lock-step: a
                 stream-ordered barrier after the publish, then each fetch is pulled over
                 xGMI on the learner's side stream while the training step runs.
+``AsyncDistGroup`` the same ranks and pulls in free-running rounds through the gossip board,
+                no collective per round (the default under torch.distributed).
 """
 import ctypes
 import os
@@ -226,8 +228,8 @@ class AsyncDistGroup(DistGroup):
     shared-memory block holding every rank's newest complete publish and who is reading
     which version, so a publish waits only for readers of the snapshot it would rewrite --
     the reference's RxThread Lock (conn.py:76-79, 109-110) -- and a rank that has closed or
-    died answers as a refused connection (conn.py:253-256).  The copy and kernel pulls are
-    supported; the relay and write-through snapshots need lock-step rounds."""
+    died answers as a refused connection (conn.py:253-256).  The copy and kernel pulls and
+    write-through snapshots are supported; the relay needs lock-step rounds."""
 
     def __init__(self, nodes, name, process_group=None, publish_timeout_ms=None):
         super().__init__(nodes, name, process_group)
@@ -291,11 +293,17 @@ def _single_host(dist, process_group=None):
     return len(set(ids)) == 1
 
 
-def default_group(config_file, nodes, name):
-    """LocalGroup when this process holds every node; DistGroup when torch.distributed runs
-    one rank per node of the config on ONE host.  A multi-host job cannot map peers' HBM:
-    it must use the reference's TCP protocol (transport='wire', dpwa_amd/bridge.py)."""
+def default_group(config_file, nodes, name, gossip=None):
+    """LocalGroup when this process holds every node; under torch.distributed with one rank
+    per node of the config on one host, free-running rounds (AsyncDistGroup: the reference's
+    learners never wait for each other, conn.py:73-79, 98-110) unless `gossip` -- the
+    config's optional `- gossip:` key, else $DPWA_GOSSIP -- says "lockstep" (DistGroup:
+    deterministic rounds behind a barrier; needed by the relay pull).  A multi-host job
+    cannot map peers' HBM: it must use the reference's TCP protocol (transport='wire')."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() == len(nodes) > 1:
-        return DistGroup(nodes, name)
+        mode = gossip or os.environ.get("DPWA_GOSSIP") or "async"
+        if mode not in ("async", "lockstep"):
+            raise ValueError("gossip must be 'async' or 'lockstep', got %r" % (mode,))
+        return AsyncDistGroup(nodes, name) if mode == "async" else DistGroup(nodes, name)
     return LocalGroup.for_config(config_file)

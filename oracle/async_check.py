@@ -36,7 +36,11 @@ class AsyncRuns:
     names          node names, index = rank
     Only ranks present in `peers` are known; a rank that left early is absent."""
 
-    def __init__(self, names, peers, versions, interp="constant", value=0.5, thr=0.0):
+    def __init__(self, names, peers, versions, interp="constant", value=0.5, thr=0.0, published=None):
+        """published(q, v, n): the parameters rank q published as version v (1-based).  Default:
+        async_base(q, v - 1, n), the runs whose every round publishes its known base.  Runs with
+        write-through snapshots publish what their last round averaged; pass those."""
+        self.published = published or (lambda q, v, n: async_base(q, v - 1, n))
         self.names = list(names)
         self.peers = {g: [str(p) for p in v] for g, v in peers.items()}
         self.versions = {g: [int(x) for x in v] for g, v in versions.items()}
@@ -86,7 +90,7 @@ class AsyncRuns:
             if not (self.interp == "constant" and self.thr == 0.0):
                 raise ValueError("incomplete runs can only be checked under constant interpolation")
             factor = self.value
-        return lerp_f32(mine, async_base(q, v - 1, n), factor)
+        return lerp_f32(mine, self.published(q, v, n), factor)
 
     def check_rank(self, g, params, clocks, n):
         """Checks rank g's recorded params (T x n) and clocks (T) round by round; returns a list

@@ -1,7 +1,8 @@
 """Worker process for the multi-process gossip tests (spawned; one rank per process).
 
-Each rank runs one DpwaConnection on its node; the group is chosen exactly as in
-production (torch.distributed initialised, world size == number of nodes -> DistGroup).
+Each rank runs one DpwaConnection on its node under torch.distributed (world size == number
+of nodes): the lock-step DistGroup for the trajectory tests, the free-running AsyncDistGroup
+(the default) for the board tests.
 """
 import os
 import sys
@@ -43,8 +44,8 @@ def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of
     from dpwa_amd.group import DistGroup
     init, deltas, send, wait = inputs(world, n, T)
     names = ["r%d" % i for i in range(world)]
-    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank, pull=pull)
-    assert isinstance(conn._group, DistGroup)
+    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank, pull=pull, group="lockstep")
+    assert type(conn._group) is DistGroup
     flat = torch.from_numpy(init[rank]).to(dev)
     params = np.zeros((T, n), np.float32)
     clocks = np.zeros(T)
@@ -90,7 +91,7 @@ def fault_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy"):
     from dpwa_amd import DpwaConnection
     init, deltas, send, wait = inputs(world, n, T)
     names = ["r%d" % i for i in range(world)]
-    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank, pull=pull)
+    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank, pull=pull, group="lockstep")
     flat = torch.from_numpy(init[rank]).to(dev)
     params, clocks, peers, scores = np.zeros((T, n), np.float32), np.zeros(T), [], []
     for r in range(T):
@@ -163,3 +164,43 @@ def async_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy", die_ra
         time.sleep(0.01)
     conn.close()
     os._exit(0)                    # skip the process-group teardown (the dead rank never joins it)
+
+
+def async_wt_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy"):
+    """Free-running rounds with write-through snapshots: update_send publishes the parameters
+    the last average left (the averaging kernel wrote that snapshot), the "training step" then
+    sets the parameters to async_base(rank, r), and the average writes the next snapshot.
+    Records what async_worker records; the test reconstructs every published snapshot from
+    the publisher's own recorded results."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from dpwa_amd import DpwaConnection
+    names = ["r%d" % i for i in range(world)]
+    conn = DpwaConnection(names[rank], cfg_path, seed=800 + rank, pull=pull)      # the default group
+    rng = np.random.default_rng(rank + 10)
+    flat = torch.from_numpy(async_base(rank, -1, n)).to(dev)
+    bases = [torch.from_numpy(async_base(rank, r, n)).to(dev) for r in range(T)]
+    params, clocks, peers, versions = np.zeros((T, n), np.float32), np.zeros(T), [], []
+    for r in range(T):
+        conn.update_send(flat, async_loss(rank, r), reuse_snapshot=True)
+        flat.copy_(bases[r])
+        torch.cuda._sleep(int(rng.integers(0, 400_000)))
+        payload, _ = conn.update_wait_average(flat, async_loss(rank, r, wait=True), write_through=True)
+        peers.append(payload.peer if payload is not None else "")
+        versions.append(conn._info()[2] if payload is not None else 0)
+        params[r] = flat.cpu().numpy()
+        clocks[r] = conn.clock
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=params, clocks=clocks, peers=np.array(peers),
+             versions=np.array(versions, dtype=np.int64))
+    open(os.path.join(out_dir, "done%d" % rank), "w").close()
+    import time
+    while sum(os.path.exists(os.path.join(out_dir, "done%d" % q)) for q in range(world)) < world:
+        time.sleep(0.01)
+    conn.close()
+    os._exit(0)

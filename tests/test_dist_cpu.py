@@ -28,10 +28,13 @@ def control_worker(rank, world, port, cfg, out_dir, T):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from dpwa_amd import DpwaConnection, _lib
-    from dpwa_amd.group import DistGroup
+    from dpwa_amd.group import AsyncDistGroup, DistGroup
     names = ["r%d" % i for i in range(world)]
     conn = DpwaConnection(names[rank], cfg, seed=500 + rank)
-    assert isinstance(conn._group, DistGroup)
+    assert isinstance(conn._group, AsyncDistGroup)      # free-running rounds by default
+    lock = DpwaConnection(names[rank], cfg, seed=500 + rank, group="lockstep")
+    assert type(lock._group) is DistGroup
+    lock.close()
     assert conn._group.rank == rank
     assert [conn.peer_rank(k) for k in range(len(conn.peers))] == [r for r in range(world) if r != rank]
     err = None

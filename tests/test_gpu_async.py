@@ -86,3 +86,30 @@ def test_async_gossip_survives_a_rank_that_leaves(tmp_path):
         read_r2 = [int(v) for p, v in zip(run["peers"], run["versions"]) if str(p) == "r2"]
         assert all(v <= die for v in read_r2), read_r2
         assert run["scores"][-1][1] < 1000, run["scores"][-1]      # r2 is the second peer of r0 and r1
+
+
+@pytest.mark.parametrize("world,pull,interp", [(2, "copy", "constant"), (3, "kernel:64", "clock")])
+def test_async_write_through_snapshots(tmp_path, world, pull, interp):
+    """Write-through under the board: the averaging kernel writes the next snapshot (and, for
+    constant/clock interpolation, its header), the publish moves no bytes, and the publish
+    rule still holds -- no reader ever averages a snapshot other than exactly what the
+    publisher had at that publish (reconstructed from the publisher's own recorded results)."""
+    n, T = 500_003, 30
+    names = ["r%d" % i for i in range(world)]
+    cfg = str(tmp_path / "async_wt.yaml")
+    dist_worker.write_cfg(cfg, names, 1.0, interp, 0.0)
+    mp.spawn(dist_worker.async_wt_worker, args=(world, free_port(), cfg, str(tmp_path), n, T, pull), nprocs=world,
+             join=True)
+    runs = {g: np.load(tmp_path / ("rank%d.npz" % g)) for g in range(world)}
+
+    def published(q, v, n_):
+        from oracle.async_check import async_base
+        return async_base(q, -1, n_) if v == 1 else runs[q]["params"][v - 2]
+
+    check = AsyncRuns(names, {g: runs[g]["peers"] for g in range(world)},
+                      {g: runs[g]["versions"] for g in range(world)}, interp, 0.5, 0.0, published=published)
+    for g in range(world):
+        bad = check.check_rank(g, runs[g]["params"], runs[g]["clocks"], n)
+        assert not bad, (g, bad[:5])
+        prefix, k = empty_rounds_form_a_prefix(runs[g])
+        assert prefix and k < T
