@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--publish", choices=["write-through", "full"], default="write-through",
                     help="how update_send publishes in the timed loop: write-through (the adapter's default: "
                          "the averaging kernel also writes the next snapshot, the publish moves the header only) "
-                         "or full (a 2*N*s snapshot copy every round); free-running rounds always publish in full")
+                         "or full (a 2*N*s snapshot copy every round); at N>1 free-running trials try both")
     ap.add_argument("--no-secondary", action="store_true", help="skip the run of the other publish form")
     ap.add_argument("--no-write-through", action="store_true", help="same as --publish full --no-secondary")
     ap.add_argument("--sample-every", type=int, default=8,
@@ -617,12 +617,14 @@ def main():
             run(2, 2, False, 1000)
             for mode in [m for m in modes if not m.startswith("relay")]:
                 set_pull(mode)
-                el, av, _, _ = run(trial_steps, 2, False, 1000)
-                pull_trials["async/" + mode] = round(av * 3 * args.numel * esize / el / 1e9, 2)
+                for wt in ((False, True) if wt_lockstep else (False,)):
+                    el, av, _, _ = run(trial_steps, 2, wt, 1000)
+                    pull_trials["async/" + mode + ("+wt" if wt else "")] = \
+                        round(av * 3 * args.numel * esize / el / 1e9, 2)
         pull = max(pull_trials, key=pull_trials.get)
         if pull.startswith("async/"):
             learners[:] = async_learners
-            set_pull(pull[len("async/"):])
+            set_pull(pull[len("async/"):].replace("+wt", ""))
         else:
             learners[:] = lockstep_learners
             for conn, _ in async_learners:   # free their streams and slots (fewer HW queues in use)
@@ -631,10 +633,13 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
             set_pull(pull)
-    wt_main = wt_lockstep and not pull.startswith("async/")
+    # trial key: "<mode>" (lock-step, publish per --publish) or "async/<mode>[+wt]"
+    sel_async = pull.startswith("async/")
+    sel_mode = pull.split("/")[-1].replace("+wt", "")
+    wt_main = pull.endswith("+wt") if sel_async else wt_lockstep
     elapsed, averaged, rounds, (lerp_ms, bracket_ms) = run(args.steps, args.warmup, wt_main, args.sample_every)
     pull_us = []
-    if world > 1 and not pull.split("/")[-1].startswith("relay"):
+    if world > 1 and not sel_mode.startswith("relay"):
         # the pull alone (side-stream events around each copying fetch), in a short extra run
         p_steps = max(20, args.steps // 4)
         for conn, _ in learners:
@@ -651,20 +656,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         pull_us = [float(t.item()) / world]
     secondary = None
-    if not args.no_secondary and (not wt_main or world == 1 or args.gossip != "async"):
-        # the other publish form, for comparison (write-through snapshots need lock-step rounds)
-        chosen = list(learners)
-        if not wt_main:
-            learners[:] = lockstep_learners
+    if not args.no_secondary:      # the other publish form, same learners and transport, for comparison
         secondary = (not wt_main, run(args.steps, args.warmup, not wt_main, args.sample_every))
-        learners[:] = chosen
     overlap = None
     if args.compute_us > 0:
         compute, k_gemm, gemm_us = make_compute(args.compute_us)
         o_steps = max(20, args.steps // 4)
         t_compute = run_overlap(o_steps, 3, compute, gossip=False)
         o_trials = {}
-        o_mode = pull.split("/")[-1]
+        o_mode = sel_mode
         if world > 1 and o_mode != "copy" and args.pull == "auto":
             # the copy engine leaves every CU to the training step: try it beside the
             # pure-loop winner and keep the cheaper overlap
@@ -673,7 +673,7 @@ def main():
                 o_trials[m] = run_overlap(o_steps, 3, compute, gossip=True)
             o_mode = min(o_trials, key=o_trials.get)
             t_both = o_trials[o_mode]
-            set_pull(pull.split("/")[-1])
+            set_pull(sel_mode)
         else:
             t_both = run_overlap(o_steps, 3, compute, gossip=True)
         overlap = {
@@ -751,14 +751,14 @@ def main():
                              % ("configs[1]: " if args.numel == RESNET18_NUMEL else "", args.numel, args.dtype,
                                 " (ResNet-18 size)" if args.numel == RESNET18_NUMEL else "", args.interpolation,
                                 args.fetch_probability, args.divergence_threshold, args.loss_schedule,
-                                "free-running" if pull.startswith("async/") else "lock-step", variant)),
+                                "free-running" if sel_async else "lock-step", variant)),
                 "learners": int(rounds / args.steps),
                 "learners_per_gpu": len(learners),
                 "numel": args.numel,
                 "publish": variant,
                 "transport": "in-place HBM read (co-resident peer)" if world == 1 else
                              "hipIpc-mapped slot pulled over xGMI on a side stream (%s, %s rounds)"
-                             % (pull.split("/")[-1], "free-running" if pull.startswith("async/") else "lock-step"),
+                             % (sel_mode, "free-running" if sel_async else "lock-step"),
                 "parallelism": "gossip x%d" % int(rounds / args.steps),
                 "streams": args.streams,
             },
