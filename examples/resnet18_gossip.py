@@ -63,7 +63,7 @@ def main():
     ap.add_argument("--batch-size", type=int, default=8)      # prepare.py:31
     ap.add_argument("--lr", type=float, default=0.01)         # prepare.py:31
     ap.add_argument("--interpolation", default="constant")
-    ap.add_argument("--gossip", default="lockstep", choices=["lockstep", "async"],
+    ap.add_argument("--gossip", default="async", choices=["lockstep", "async"],
                     help="under torchrun: lock-step rounds (DistGroup) or free-running ones (gossip board)")
     args = ap.parse_args()
 
