@@ -384,19 +384,16 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
     const int k = (int)(l->version % 2);   // slot of publish number version+1
     char *slot = l->slots + (size_t)k * l->slot_stride;
     const bool header_only = reuse && l->wt_valid && l->wt_flat == flat;
-    hipStream_t produced_on = s;
     if (header_only && l->wt_header) {
         // payload, header and clock of this publish were written by the last average: nothing
-        // moves (IPC-exported slots still get their system-scope write-back)
-        if (l->exported) {
-            if (l->wt_stream != s) {
-                HIP_TRY(hipEventRecord(l->ev_wt, l->wt_stream));
-                HIP_TRY(hipStreamWaitEvent(s, l->ev_wt, 0));
-            }
-            HIP_TRY(launch_release_system(s));
-        } else {
-            produced_on = l->wt_stream;
+        // moves (IPC-exported slots still get their system-scope write-back).  Work on `s`
+        // after this publish (the next factor reads the clock the average wrote) is ordered
+        // after the average.
+        if (l->wt_stream != s) {
+            HIP_TRY(hipEventRecord(l->ev_wt, l->wt_stream));
+            HIP_TRY(hipStreamWaitEvent(s, l->ev_wt, 0));
         }
+        if (l->exported) HIP_TRY(launch_release_system(s));
         l->cur = (l->cur + 1) & 3;
     } else if (header_only) {
         // the payload was written by the last average (readers of slot k were waited for then)
@@ -415,7 +412,7 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
     l->wt_valid = false;
     l->wt_header = false;
     std::lock_guard<std::mutex> g(l->pub_mu);
-    l->publish_stream[k] = produced_on;
+    l->publish_stream[k] = s;
     l->published[k] = true;
     l->version++;
     return DPWA_OK;
@@ -1056,6 +1053,7 @@ int dpwa_learner_write_clock(dpwa_learner *l, double clock)
     DeviceGuard dg(l->device);
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(&l->ctl->clock[l->cur], &clock, sizeof(double), hipMemcpyHostToDevice));
+    l->wt_header = false;   // the next header was written from the old clock: publish it anew
     return DPWA_OK;
 }
 
