@@ -237,22 +237,28 @@ def parity_lockstep_expected(names, n=PARITY_N, T=PARITY_T):
                 for r in range(T)] for g in range(G)}
 
 
-def parity_async(names, rank, cfg, pull, device, n=PARITY_N, T=PARITY_ASYNC_T):
-    """Free-running rounds over the gossip board (AsyncDistGroup): each round publishes the
-    checker's known parameters for (rank, round), runs an uneven synthetic step and averages
-    with whatever version the board hands out.  Returns (conn, params, clocks, peers, versions)."""
+def parity_async(names, rank, cfg, pull, device, n=PARITY_N, T=PARITY_ASYNC_T, write_through=False):
+    """Free-running rounds over the gossip board (AsyncDistGroup): each round publishes, runs
+    an uneven synthetic step that sets the parameters to the checker's known values for
+    (rank, round) and averages with whatever version the board hands out.  Without
+    write-through the publish comes after that step (it publishes the known values); with it,
+    before (it publishes what the last average wrote through).  Returns (conn, params,
+    clocks, peers, versions)."""
     from dpwa_amd import DpwaConnection
     from oracle.async_check import async_base, async_loss
     conn = DpwaConnection(names[rank], cfg, seed=700 + rank, group="async", pull=pull)
     rng = np.random.default_rng(rank)
-    flat = torch.empty(n, device=device, dtype=torch.float32)
+    flat = torch.from_numpy(async_base(rank, -1, n)).to(device)
     bases = [torch.from_numpy(async_base(rank, r, n)).to(device) for r in range(T)]
     params, clocks, peers, versions = np.zeros((T, n), np.float32), np.zeros(T), [], []
     for r in range(T):
-        flat.copy_(bases[r])
-        conn.update_send(flat, async_loss(rank, r))
+        if not write_through:
+            flat.copy_(bases[r])
+        conn.update_send(flat, async_loss(rank, r), reuse_snapshot=write_through)
+        if write_through:
+            flat.copy_(bases[r])
         torch.cuda._sleep(int(rng.integers(0, 200_000)))       # uneven "training steps"
-        payload, _ = conn.update_wait_average(flat, async_loss(rank, r, wait=True))
+        payload, _ = conn.update_wait_average(flat, async_loss(rank, r, wait=True), write_through=write_through)
         peers.append(payload.peer if payload is not None else "")
         versions.append(conn._info()[2] if payload is not None else 0)
         params[r] = flat.cpu().numpy()
@@ -285,14 +291,26 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             result[t] = bool(ok.item())
         else:                                  # async: free-running over the gossip board
-            from oracle.async_check import AsyncRuns
-            conn, params, clocks, peers, versions = parity_async(names, rank, cfg, pull, device)
+            from oracle.async_check import AsyncRuns, async_base
+            wt = pull.endswith("+wt")
+            conn, params, clocks, peers, versions = parity_async(names, rank, cfg, pull.replace("+wt", ""), device,
+                                                                 write_through=wt)
             conns = [conn]
             got = [None] * world
             dist.all_gather_object(got, (peers, versions))
             check = AsyncRuns(names, {g: got[g][0] for g in range(world)}, {g: got[g][1] for g in range(world)},
                               "clock", None, 0.0)
-            bad = check.check_rank(rank, params, clocks, PARITY_N)
+            if wt:   # each rank vouches for the averages of its own published versions (digests)
+                mine = check.served(rank, lambda v: async_base(rank, -1, PARITY_N) if v == 1 else params[v - 2],
+                                    PARITY_N)
+                served = [None] * world
+                dist.all_gather_object(served, mine)
+                expected = {}
+                for d in served:
+                    expected.update(d)
+                bad = check.check_rank_digests(rank, params, clocks, PARITY_N, expected)
+            else:
+                bad = check.check_rank(rank, params, clocks, PARITY_N)
             if bad:
                 print("parity %s rank %d: %s" % (t, rank, bad[:3]), file=sys.stderr, flush=True)
             ok = torch.tensor([0 if bad else 1], dtype=torch.int32,
@@ -702,7 +720,7 @@ def main():
             if args.gossip != "async":
                 transports += ["lockstep/copy", "lockstep/kernel:256", "lockstep/relay:32"]
             if args.gossip != "lockstep":
-                transports += ["async/copy", "async/kernel:256"]
+                transports += ["async/copy", "async/kernel:256", "async/copy+wt", "async/kernel:256+wt"]
         parity = parity_leg(world, rank, local_rank, device, tmp, transports, args.dist_backend)
         parity["workload"] = ("%d-element fp32 vector per learner, %d lock-step rounds (clock interpolation, "
                               "fetch_probability %g, seeded training-step deltas, write-through and split rounds "

@@ -10,6 +10,8 @@ with q's base of round v-1 under the factor of dpwa.py:143-147, and the clocks m
 dpwa.py:112 and 150-155 through exactly the versions that were read.  A torn or overwritten
 snapshot, a version handed out before its bytes landed or a stale clock cannot pass.
 """
+import hashlib
+
 import numpy as np
 
 from .lerp import lerp_f32
@@ -26,6 +28,11 @@ def async_loss(rank, r, wait=False):
     decaying, so a divergence threshold is crossed mid-run."""
     x = 2.0 * float(np.exp(-r / 8.0)) + 0.1 * rank + 0.05
     return 0.9 * x if wait else x
+
+
+def digest(a):
+    """sha1 of an array's bytes (bit-exact comparison without moving the array)."""
+    return hashlib.sha1(np.ascontiguousarray(a).view(np.uint8).tobytes()).hexdigest()
 
 
 class AsyncRuns:
@@ -109,6 +116,43 @@ class AsyncRuns:
             want = self.expected_params(g, r, n)
             if not np.array_equal(np.asarray(params[r]).view(np.uint32), want.view(np.uint32)):
                 bad.append("round %d: parameters differ from the oracle (peer %s)" % (r, self.peers[g][r] or "-"))
+            if self.complete() and float(clocks[r]) != self.clock_after(g, r):
+                bad.append("round %d: clock %r != %r" % (r, float(clocks[r]), self.clock_after(g, r)))
+        return bad
+
+    # -- distributed form: no rank needs another rank's parameters ------------------------
+    def served(self, q, published_by_q, n):
+        """Digests of what every average that read a version published by rank q must equal:
+        {(reader g, round r): digest}.  Run on rank q, which holds its own published
+        snapshots (published_by_q(v) -> array), e.g. write-through runs that publish what
+        their last round averaged."""
+        out = {}
+        for g in self.peers:
+            for r in range(len(self.peers[g])):
+                got = self.read(g, r)
+                if got is None or got[0] != q:
+                    continue
+                factor = self.policy(g, r)[0] if self.complete() else self.value
+                out[(g, r)] = digest(lerp_f32(async_base(g, r, n), published_by_q(got[1]), factor))
+        return out
+
+    def check_rank_digests(self, g, params, clocks, n, expected):
+        """check_rank with the averages compared against `expected` (the union of every
+        publisher's served()); rounds with no data must leave async_base(g, r)."""
+        bad = []
+        last = {}
+        for r in range(len(self.peers[g])):
+            got = self.read(g, r)
+            if got is None:
+                if digest(params[r]) != digest(async_base(g, r, n)):
+                    bad.append("round %d: parameters changed without an average" % r)
+            else:
+                q, v = got
+                if v < 1 or v < last.get(q, 0):
+                    bad.append("round %d: version %d of %s out of order" % (r, v, self.names[q]))
+                last[q] = v
+                if digest(params[r]) != expected.get((g, r)):
+                    bad.append("round %d: average differs from %s's published version %d" % (r, self.names[q], v))
             if self.complete() and float(clocks[r]) != self.clock_after(g, r):
                 bad.append("round %d: clock %r != %r" % (r, float(clocks[r]), self.clock_after(g, r)))
         return bad

@@ -177,3 +177,35 @@ def test_async_checker_accepts_a_consistent_run_and_rejects_a_torn_one():
                 stale = clocks.copy()
                 stale[6] += 1.0
                 assert any("round 6: clock" in b for b in check.check_rank(g, params, stale, n))
+
+
+def test_async_checker_distributed_digests():
+    """AsyncRuns.served / check_rank_digests (bench.py's write-through parity leg): the
+    publisher vouches for the averages of its own versions; a consistent CPU-made run passes
+    and a torn average fails."""
+    from oracle.async_check import AsyncRuns, async_base
+    names = ["r0", "r1"]
+    n, T = 131, 7
+    peers = {0: ["", "r1", "r1", "", "r1", "r1", "r1"], 1: ["r0", "r0", "", "r0", "r0", "r0", "r0"]}
+    versions = {0: [0, 1, 2, 0, 4, 4, 6], 1: [1, 2, 0, 3, 4, 5, 6]}
+    check = AsyncRuns(names, peers, versions, "clock", None, 0.0)
+    # write-through runs: version v of rank q is q's parameters after its round v-2 (v=1: initial)
+    params = {q: np.zeros((T, n), np.float32) for q in (0, 1)}
+    order = sorted((r, q) for q in (0, 1) for r in range(T))
+
+    def pub(q, v):
+        return async_base(q, -1, n) if v == 1 else params[q][v - 2]
+
+    for r, q in order:       # versions read never exceed the publisher's progress (v - 2 < r)
+        got = check.read(q, r)
+        params[q][r] = async_base(q, r, n) if got is None else \
+            olerp.lerp_f32(async_base(q, r, n), pub(got[0], got[1]), check.policy(q, r)[0])
+    expected = {}
+    for q in (0, 1):
+        expected.update(check.served(q, lambda v, q=q: pub(q, v), n))
+    clocks = {q: np.array([check.clock_after(q, r) for r in range(T)]) for q in (0, 1)}
+    for g in (0, 1):
+        assert check.check_rank_digests(g, params[g], clocks[g], n, expected) == []
+    torn = params[0].copy()
+    torn[4, 7] += 1.0
+    assert any("round 4" in b for b in check.check_rank_digests(0, torn, clocks[0], n, expected))
