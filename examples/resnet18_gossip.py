@@ -55,7 +55,7 @@ def resnet18(num_classes=10):
     return nn.Sequential(*layers)
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--learners", type=int, default=2, help="co-resident learners (single process)")
     ap.add_argument("--steps", type=int, default=50)
@@ -65,7 +65,7 @@ def main():
     ap.add_argument("--interpolation", default="constant")
     ap.add_argument("--gossip", default="async", choices=["lockstep", "async"],
                     help="under torchrun: lock-step rounds (DistGroup) or free-running ones (gossip board)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

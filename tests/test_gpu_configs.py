@@ -216,3 +216,17 @@ def test_gpu_key_moves_the_model_onto_its_device(tmp_path):
     assert olerp.bits_equal(got[0], olerp.lerp_f32(want[0], want[1], 0.5))
     for a in adapters:
         a.connection.close()
+
+
+def test_resnet18_example_runs(capsys):
+    """f1: examples/resnet18_gossip.py (the reference trainer's loop, main.py:122-158) runs end
+    to end with gossip every step; the clock advanced every round (fetch_probability 1)."""
+    import json
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples"))
+    import resnet18_gossip
+    resnet18_gossip.main(["--learners", "2", "--steps", "4", "--warmup", "2", "--batch-size", "8"])
+    out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert out["learners"] == 2 and out["final_clock"] == 6.0
+    assert out["train_steps_per_s_per_learner_gossip"] > 0
