@@ -38,5 +38,5 @@ timeout -k 10 600 python3 bench.py --traffic gpurun_out/traffic_${TAG}_write-thr
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
     python3 bench.py --no-cpu-baseline --traffic gpurun_out/traffic_${TAG}_write-through.json \
     > gpurun_out/bench_rocprof_$TAG.json 2> gpurun_out/bench_rocprof_$TAG.err || { echo "rocprof bench failed"; exit 1; }
-python3 tools/trace_stats.py gpurun_out/prof_$TAG/run_kernel_trace.csv > gpurun_out/prof_${TAG}_per_size.csv || exit 1
+python3 tools/trace_stats.py gpurun_out/prof_$TAG/run_kernel_trace.csv > gpurun_out/prof_${TAG}_per_size.csv && python3 tools/trace_stats.py --runs gpurun_out/prof_$TAG/run_kernel_trace.csv > gpurun_out/prof_${TAG}_runs.csv || exit 1
 echo done
