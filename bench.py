@@ -60,7 +60,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
-    ap.add_argument("--no-sweep", action="store_true", help="skip the cold kernel sweep over the north_star sizes")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip the sweeps over the north_star sizes (cold kernel, and whole rounds at N=1)")
     ap.add_argument("--publish", choices=["write-through", "full"], default="write-through",
                     help="how update_send publishes in the timed loop: write-through (the adapter's default: "
                          "the averaging kernel also writes the next snapshot, the publish moves the header only) "
@@ -384,6 +385,51 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64):
     return {"avg_launch_us": float(us.mean()), "median_launch_us": float(np.median(us)),
             "min_launch_us": float(us.min()), "max_launch_us": float(us.max()), "launches": launches,
             "rotating_buffer_pairs": pairs, "batch_bracket_us": float(batch_us)}
+
+
+def round_sweep(device, cfg_dir, steps=20, warmup=3):
+    """Whole gossip rounds (two co-resident learners, write-through publish, constant 0.5,
+    fetch_probability 1) at every north_star size in its config's dtype: the averaged GB/s
+    and rounds/s the north star asks for at 11M/100M/1B/7B on one GPU."""
+    from dpwa_amd import DpwaConnection
+    from dpwa_amd.group import LocalGroup
+    rows = []
+    cfg = os.path.join(cfg_dir, "sweep.yaml")
+    write_config(cfg, ["w1", "w2"], "constant")
+    for numel, dt in SWEEP:
+        dtype = torch.float32 if dt == "f32" else torch.bfloat16
+        esize = 4 if dt == "f32" else 2
+        flats = []
+        for g in range(2):
+            t = torch.empty(numel, dtype=dtype, device=device)
+            t.normal_(generator=torch.Generator(device=device).manual_seed(g))
+            flats.append(t)
+        group = LocalGroup()
+        conns = [DpwaConnection(nm, cfg, seed=1000 + g, group=group) for g, nm in enumerate(("w1", "w2"))]
+
+        def step():
+            for c, f in zip(conns, flats):
+                c.update_send(f, 1.0, reuse_snapshot=True)
+            n = 0
+            for c, f in zip(conns, flats):
+                n += c.update_wait_average(f, 1.0, write_through=True)[0] is not None
+            return n
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        averaged = sum(step() for _ in range(steps))
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        rows.append({"numel": numel, "dtype": dt, "value": round(averaged * 3 * numel * esize / el / 1e9, 1),
+                     "ms_per_step": round(1e3 * el / steps, 4), "gossip_rounds_per_s": round(2 * steps / el, 1),
+                     "steps": steps})
+        for c in conns:
+            c.close()
+        del flats, conns
+        torch.cuda.empty_cache()
+    return rows
 
 
 def size_sweep(device):
@@ -856,6 +902,7 @@ def main():
             out["overlap"] = overlap
         if world == 1 and not args.no_sweep:
             out["roofline"]["size_sweep"] = size_sweep(device)
+            out["round_sweep"] = round_sweep(device, tmp)
         out["cpu_baseline"] = cpu
         if parity is not None:
             out["parity"] = parity

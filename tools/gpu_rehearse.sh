@@ -17,6 +17,7 @@ GPU_MAX_HW_QUEUES=2 timeout -k 10 300 python -m torch.distributed.run --nnodes=1
     > gpurun_out/rehearse_n6.json 2> gpurun_out/rehearse_n6.err || { echo "rehearsal n=6 failed"; tail -20 gpurun_out/rehearse_n6.err; exit 1; }
 cat gpurun_out/rehearse_n6.json
 V="--no-cpu-baseline --no-sweep --no-cold --compute-us 0 --steps 50 --warmup 10"
+timeout -k 10 200 python bench.py $V --numel 100000000 --interpolation clock > gpurun_out/bench_100m_clock.json 2> gpurun_out/variants.err || { echo "variant failed"; tail gpurun_out/variants.err; exit 1; }
 timeout -k 10 200 python bench.py $V --numel 1000000000 --dtype bf16 --interpolation loss --divergence-threshold 0.5 \
     --loss-schedule decay > gpurun_out/bench_1b_bf16_loss_decay.json 2> gpurun_out/variants.err &&
 timeout -k 10 300 python bench.py $V --numel 7000000000 --dtype bf16 --fetch-probability 0.7 \
