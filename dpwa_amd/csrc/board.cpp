@@ -334,9 +334,14 @@ int dpwa_board_publish_wait(dpwa_board *b, uint64_t next, int timeout_ms)
         return timeout_ms >= 0 &&
                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms);
     };
-    int spins = 0;
+    // What is waited for is GPU progress (our advertise, peers' read releases), typically tens
+    // of microseconds: spin on the CPU for the first 200 us (a sleep costs the kernel's ~50 us
+    // timer slack), then back off to short sleeps.
     auto pause = [&]() {
-        if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
+            __builtin_ia32_pause();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
     };
     while (load(&b->nodes[b->rank].version) + 1 < next) {
         if (expired())
