@@ -236,7 +236,10 @@ __device__ __forceinline__ void span_store(__amdgpu_buffer_rsrc_t r, int lane_of
 // policy; the result is stored `sc1`, with bit 2 `sc0 sc1`, with bit 4 `nt sc1`.
 template <int POLICY> struct LerpPolicy {
     static constexpr int param_load = (POLICY & 1) ? 0 : kAuxStream;
-    static constexpr int store = kAuxStore | ((POLICY & 2) ? 1 : 0) | ((POLICY & 4) ? kAuxStream : 0);
+    static constexpr int snap_store = kAuxStore | ((POLICY & 2) ? 1 : 0) | ((POLICY & 4) ? kAuxStream : 0);
+    // bit 8: the parameters (re-read only two averages later, past the Infinity Cache's
+    // reach) are stored `nt`, leaving the cache to the snapshot the peer reads next
+    static constexpr int store = snap_store | ((POLICY & 8) ? kAuxStream : 0);
 };
 
 // One 16-byte item per lane; items beyond n/PER (the ragged tail) go to block 0.
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ pa
         __syncthreads();
         if (!s_ok) {          // no-op round; a write-through snapshot still gets the parameters
             if (DUAL)
-                span_store<V, LerpPolicy<POLICY>::store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, p);
+                span_store<V, LerpPolicy<POLICY>::snap_store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, p);
             if (DUAL && blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
                 const int64_t j = nv * Ops::PER + threadIdx.x;
                 reinterpret_cast<typename Ops::S *>(args.snap)[j] = reinterpret_cast<typename Ops::S *>(param)[j];
@@ -294,7 +297,7 @@ __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ pa
     {
         const V r = Ops::lerp(a, b, q, p);
         span_store<V, LerpPolicy<POLICY>::store>(rp, lane_off, r);
-        if (DUAL) span_store<V, LerpPolicy<POLICY>::store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, r);
+        if (DUAL) span_store<V, LerpPolicy<POLICY>::snap_store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, r);
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
         typename Ops::S *ps = reinterpret_cast<typename Ops::S *>(param);
@@ -378,7 +381,7 @@ static int lerp_policy()
     static const int forced = [] {
         const char *e = getenv("DPWA_LERP_POLICY");
         const int p = e ? atoi(e) : 0;
-        return (p >= 0 && p <= 7) ? p : 0;
+        return (p >= 0 && p <= 15) ? p : 0;
     }();
     return forced;
 }
@@ -396,6 +399,8 @@ static hipError_t launch_mode(void *param, const void *peer, int64_t n, const Le
             case 3: return launch_blocks<Ops, MODE, DUAL, 64, 3>(param, peer, n, args, s, timing);
             case 4: return launch_blocks<Ops, MODE, DUAL, 64, 4>(param, peer, n, args, s, timing);
             case 5: return launch_blocks<Ops, MODE, DUAL, 64, 5>(param, peer, n, args, s, timing);
+            case 8: return launch_blocks<Ops, MODE, DUAL, 64, 8>(param, peer, n, args, s, timing);
+            case 9: return launch_blocks<Ops, MODE, DUAL, 64, 9>(param, peer, n, args, s, timing);
             default: return launch_blocks<Ops, MODE, DUAL, 64>(param, peer, n, args, s, timing);
             }
         case 128: return launch_blocks<Ops, MODE, DUAL, 128>(param, peer, n, args, s, timing);
