@@ -306,10 +306,10 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
                                     PARITY_N)
                 served = [None] * world
                 dist.all_gather_object(served, mine)
-                expected = {}
+                vouched = {}
                 for d in served:
-                    expected.update(d)
-                bad = check.check_rank_digests(rank, params, clocks, PARITY_N, expected)
+                    vouched.update(d)
+                bad = check.check_rank_digests(rank, params, clocks, PARITY_N, vouched)
             else:
                 bad = check.check_rank(rank, params, clocks, PARITY_N)
             if bad:
