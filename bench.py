@@ -11,8 +11,11 @@ fetch_probability 1.
   * ``--gpus 1``: two learners co-resident on cuda:0 (the minimal non-degenerate gossip:
     each averages with the other's snapshot, read in place from HBM).
   * ``--gpus N`` (torchrun): one learner per GPU; peers' snapshots are mapped with
-    hipIpcOpenMemHandle and pulled over xGMI on each learner's side stream; every round is
-    lock-step behind an RCCL barrier.  Per-GPU work is fixed -> "scaling": "weak".
+    hipIpcOpenMemHandle and pulled over xGMI on each learner's side stream.  Short trials of
+    lock-step rounds (RCCL barrier; copy / kernel / relay pulls) and free-running rounds
+    (gossip board) pick the transport of the timed run.  Per-GPU work is fixed -> "scaling":
+    "weak".  Every rank logs its phases to stderr (``[bench rN +s]``), so a multi-GPU run that
+    stops names the phase it stopped in.
 
 ``value`` = algorithmic averaged bytes (3 * numel * sizeof(dtype) per completed
 averaging) summed over all learners / the max-over-ranks wall time of the
@@ -43,6 +46,15 @@ RESNET18_NUMEL = 11_173_962    # examples/pytorch-cifar/models/resnet.py ResNet1
 REF_SAMPLE_MAX = 32_000_000    # cap on the reference-round CPU sample (elements)
 # BASELINE.json north_star sizes, each in its config's dtype (configs[1..4])
 SWEEP = ((RESNET18_NUMEL, "f32"), (100_000_000, "f32"), (1_000_000_000, "bf16"), (7_000_000_000, "bf16"))
+
+
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """One stderr line per phase and rank (stdout keeps the single JSON line)."""
+    print("[bench r%s +%.1fs] %s" % (os.environ.get("RANK", "0"), time.perf_counter() - _T0, msg),
+          file=sys.stderr, flush=True)
 
 
 def parse():
@@ -278,6 +290,7 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
     result = {}
     expected = parity_lockstep_expected(names) if rank == 0 else None
     for t in transports:
+        progress("parity %s" % t)
         kind, _, pull = t.partition("/")
         if kind == "local":                   # one GPU: both learners in this process
             from dpwa_amd.group import LocalGroup
@@ -454,12 +467,18 @@ def size_sweep(device):
 
 def main():
     args = parse()
+    # a rank stopped from outside (the launcher after another rank failed, a time limit) prints
+    # where every thread was before it goes
+    import faulthandler
+    import signal
+    faulthandler.register(signal.SIGTERM, all_threads=True, chain=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d (launch N>1 with torch.distributed.run)" % (args.gpus, world))
     # the CPU baseline first, before anything touches the GPU (its learners are child processes)
+    progress("start: world %d, numel %d %s" % (world, args.numel, args.dtype))
     cpu = cpu_baseline(args.numel, args.cpu_seconds) if world == 1 and not args.no_cpu_baseline else None
     # one GPU per rank; the modulo only matters for rehearsals with more ranks than GPUs
     device = torch.device("cuda", local_rank % torch.cuda.device_count())
@@ -662,6 +681,7 @@ def main():
     lockstep_learners = list(learners)
     async_learners = []
     if world > 1:
+        progress("binding %d lock-step learner(s)" % len(learners))
         run(2, 2, False, 1000)   # binds the learners (IPC exchange) before the transport is chosen
         modes = [args.pull] if args.pull != "auto" else ["copy", "kernel:256", "kernel:1024", "relay:32",
                                                          "relay:128", "relay:512"]
@@ -671,6 +691,7 @@ def main():
                 set_pull(mode)
                 el, av, _, _ = run(trial_steps, 2, wt_lockstep, 1000)
                 pull_trials[mode] = round(av * 3 * args.numel * esize / el / 1e9, 2)
+                progress("trial %s: %.1f GB/s" % (mode, pull_trials[mode]))
         if args.gossip != "lockstep":
             # free-running rounds over the gossip board, same learners' parameters (a second
             # set of nodes: a connection's group is fixed at construction)
@@ -678,6 +699,7 @@ def main():
                 conn = DpwaConnection(name, cfg, seed=1000 + seed, group="async", pull="copy")
                 async_learners.append((conn, flat))
             learners[:] = async_learners
+            progress("binding free-running learner(s)")
             run(2, 2, False, 1000)
             for mode in [m for m in modes if not m.startswith("relay")]:
                 set_pull(mode)
@@ -685,6 +707,8 @@ def main():
                     el, av, _, _ = run(trial_steps, 2, wt, 1000)
                     pull_trials["async/" + mode + ("+wt" if wt else "")] = \
                         round(av * 3 * args.numel * esize / el / 1e9, 2)
+                    progress("trial async/%s%s: %.1f GB/s" % (mode, "+wt" if wt else "",
+                                                              pull_trials["async/" + mode + ("+wt" if wt else "")]))
         pull = max(pull_trials, key=pull_trials.get)
         if pull.startswith("async/"):
             learners[:] = async_learners
@@ -701,7 +725,9 @@ def main():
     sel_async = pull.startswith("async/")
     sel_mode = pull.split("/")[-1].replace("+wt", "")
     wt_main = pull.endswith("+wt") if sel_async else wt_lockstep
+    progress("timed run: %s, %s publish" % (pull, "write-through" if wt_main else "full"))
     elapsed, averaged, rounds, (lerp_ms, bracket_ms) = run(args.steps, args.warmup, wt_main, args.sample_every)
+    progress("timed run: %.4f ms/step" % (1e3 * elapsed / args.steps))
     pull_us = []
     if world > 1 and not sel_mode.startswith("relay"):
         # the pull alone (side-stream events around each copying fetch), in a short extra run
@@ -721,11 +747,13 @@ def main():
         pull_us = [float(t.item()) / world]
     secondary = None
     if not args.no_secondary:      # the other publish form, same learners and transport, for comparison
+        progress("secondary publish form")
         secondary = (not wt_main, run(args.steps, args.warmup, not wt_main, args.sample_every))
     overlap = None
     if args.compute_us > 0:
         compute, k_gemm, gemm_us = make_compute(args.compute_us)
         o_steps = max(20, args.steps // 4)
+        progress("overlap: %d GEMMs per step" % k_gemm)
         t_compute = run_overlap(o_steps, 3, compute, gossip=False)
         o_trials = {}
         o_mode = sel_mode
@@ -778,6 +806,7 @@ def main():
     unit_bytes = 3 * args.numel * esize
     kbytes = (4 if wt_main else 3) * args.numel * esize     # the timed loop's averaging kernel, per launch
     # the same kernel alone, cold (rotating buffers, per-launch dispatch events): the roofline's basis
+    progress("cold kernel")
     cold = cold_kernel(args.numel, dtype, device, wt_main) if not args.no_cold else None
     if rank == 0:
         value = averaged * unit_bytes / elapsed / 1e9
@@ -901,12 +930,15 @@ def main():
         if overlap is not None:
             out["overlap"] = overlap
         if world == 1 and not args.no_sweep:
+            progress("size sweep")
             out["roofline"]["size_sweep"] = size_sweep(device)
+            progress("round sweep")
             out["round_sweep"] = round_sweep(device, tmp)
         out["cpu_baseline"] = cpu
         if parity is not None:
             out["parity"] = parity
         print(json.dumps(out), flush=True)
+    progress("done")
     for conn, _ in lockstep_learners + async_learners:
         conn.close()
     if world > 1:
