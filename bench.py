@@ -53,8 +53,8 @@ _T0 = time.perf_counter()
 
 def progress(msg):
     """One stderr line per phase and rank (stdout keeps the single JSON line)."""
-    print("[bench r%s +%.1fs] %s" % (os.environ.get("RANK", "0"), time.perf_counter() - _T0, msg),
-          file=sys.stderr, flush=True)
+    sys.stderr.write("[bench r%s +%.1fs] %s\n" % (os.environ.get("RANK", "0"), time.perf_counter() - _T0, msg))
+    sys.stderr.flush()      # one write per line: ranks share the stream
 
 
 def parse():

@@ -532,10 +532,11 @@ hipError_t launch_pull(void *dst, const void *src, int64_t nbytes, int max_block
 // ---------------------------------------------------------------- relay (multi-link pull)
 // Lock-step round of G ranks where rank i averages with rank picks[i] (-1: none).  Each
 // snapshot payload is cut into G stripes.  Phase 1 on rank r pulls stripe r of every
-// snapshot some OTHER rank needs into its relay buffer (R_r[j] = stripe r of rank j);
-// after a barrier, phase 2 on rank r gathers stripe s of its peer j's snapshot from rank s's
-// relay buffer (from j itself for s == j, and directly for s == r).  Every pair's xGMI link
-// then carries one stripe per phase instead of one link carrying the whole snapshot.
+// snapshot some rank needs (its own peer's included) into its relay buffer (R_r[j] = stripe
+// r of rank j); after a barrier, phase 2 on rank r gathers stripe s of its peer j's snapshot
+// from rank s's relay buffer, from its own relay buffer for s == r (local HBM) and from j
+// itself for s == j.  Every pair's xGMI link then carries at most one stripe per phase
+// instead of one link carrying the whole snapshot.
 // blockIdx.y selects the source (phase 1) or the stripe (phase 2); blockIdx.x strides it.
 __global__ void k_release_system();
 
@@ -564,8 +565,8 @@ __global__ __launch_bounds__(kBlock) void k_relay_phase1(RelayArgs a)
 {
     const int j = blockIdx.y;
     if (j == a.rank) return;
-    bool active = false;                                   // does any rank other than me need j?
-    for (int i = 0; i < a.world; ++i) active |= (i != a.rank && a.picks[i] == j);
+    bool active = false;                                   // does any rank (me included) need j?
+    for (int i = 0; i < a.world; ++i) active |= (a.picks[i] == j);
     if (!active) return;
     const int64_t len = stripe_len(a.rank, a.stripe, a.payload);
     const char *src = a.slots[j] + a.slot_off + 256 + (int64_t)a.rank * a.stripe;
@@ -582,8 +583,9 @@ __global__ __launch_bounds__(kBlock) void k_relay_phase2(RelayArgs a)
         reinterpret_cast<u32x4 *>(a.staging)[threadIdx.x] =
             reinterpret_cast<const u32x4 *>(a.slots[j] + a.slot_off)[threadIdx.x];
     const int64_t len = stripe_len(s, a.stripe, a.payload);
-    const char *src = (s == j || s == a.rank) ? a.slots[j] + a.slot_off + 256 + (int64_t)s * a.stripe
-                                              : a.relays[s] + (int64_t)j * a.stripe;
+    const char *src = s == j        ? a.slots[j] + a.slot_off + 256 + (int64_t)s * a.stripe
+                      : s == a.rank ? a.relay_mine + (int64_t)j * a.stripe
+                                    : a.relays[s] + (int64_t)j * a.stripe;
     copy16((u32x4 *)(a.staging + 256 + (int64_t)s * a.stripe), (const u32x4 *)src, len >> 4);
 }
 
