@@ -29,7 +29,6 @@ from .sched import Scheduler, seed_key
 LOGGER = logging.getLogger(__name__)
 
 
-
 class Struct:
     def __init__(self, **entries):
         self.__dict__.update(entries)
@@ -130,11 +129,15 @@ class DeviceFactor:
         self._round = learner.version
         self._t = None
 
+    def _check(self):
+        learner = self._learner
+        if learner._h is None or learner.version != self._round:
+            raise RuntimeError("stale factor: a later update_send has started a new round")
+        return learner
+
     def tensor(self):
         if self._t is None:
-            learner = self._learner
-            if learner._h is None or learner.version != self._round:
-                raise RuntimeError("stale factor: a later update_send has started a new round")
+            learner = self._check()
             t = torch.empty((), dtype=torch.float64, device=learner.device)
             _lib.call("dpwa_learner_copy_factor", learner.handle, ctypes.c_void_p(t.data_ptr()),
                       ctypes.c_void_p(torch.cuda.current_stream(learner.device).cuda_stream))
@@ -144,7 +147,7 @@ class DeviceFactor:
     def __float__(self):
         if self._t is not None:
             return float(self._t.item())
-        return float(self._learner.read_coef().factor)
+        return float(self._check().read_coef().factor)
 
     def __mul__(self, other):
         return self.tensor() * other
@@ -174,7 +177,7 @@ class DeviceFactor:
         return -self.tensor()
 
     def coefficients(self):
-        c = self._learner.read_coef()
+        c = self._check().read_coef()
         return {"factor": c.factor, "new_clock": c.new_clock, "a": c.a, "b": c.b, "status": c.status}
 
     def __repr__(self):
