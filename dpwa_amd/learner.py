@@ -55,7 +55,7 @@ class Learner:
         self.version = 0                 # publishes so far (mirrors dpwa_learner_version)
         self._keep = None
         self._loss_dtype = _lib.F64      # what device loss pointers point at (native side)
-        self._checked = None             # (id, data_ptr) of the last validated flat tensor
+        self._checked = None             # (id, data_ptr, numel, dtype) of the last validated tensor
         self._f_publish = lib.dpwa_learner_publish
         self._f_fetch = lib.dpwa_learner_fetch
         self._f_average = lib.dpwa_learner_average
@@ -95,9 +95,13 @@ class Learner:
             pass
 
     def _ptr(self, t):
-        key = (id(t), t.data_ptr())
+        if not isinstance(t, torch.Tensor):
+            raise ValueError("expected a %s tensor on %s, got %s" % (self.dtype, self.device, type(t).__name__))
+        # id and address alone can repeat for a new tensor (a freed one's id, the caching
+        # allocator's block): size and dtype are part of the key, so such a tensor is checked
+        key = (id(t), t.data_ptr(), t.numel(), t.dtype)
         if key != self._checked:
-            if not isinstance(t, torch.Tensor) or t.device != self.device or t.dtype != self.dtype:
+            if t.device != self.device or t.dtype != self.dtype:
                 raise ValueError("expected a %s tensor on %s" % (self.dtype, self.device))
             if not t.is_contiguous() or t.numel() != self.numel:
                 raise ValueError("expected a contiguous tensor of %d elements, got %s" % (self.numel, tuple(t.shape)))
