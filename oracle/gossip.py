@@ -10,12 +10,21 @@ any fetch of round r is served, which is the schedule the GPU gossip group runs.
 """
 import numpy as np
 
-from .lerp import lerp_f32
+from .lerp import bf16_to_f32, f32_to_bf16, lerp_f32
 from .policy import OracleLearner
 
 
+def add_bf16(param_u16, delta_u16):
+    """torch's bf16 ``param.add_(delta)``: both widened to fp32, one fp32 add, rounded to
+    bf16 (RNE); arrays hold raw bf16 bits."""
+    with np.errstate(all="ignore"):
+        return f32_to_bf16(bf16_to_f32(param_u16) + bf16_to_f32(delta_u16))
+
+
 def simulate(names, init, deltas, send_loss, wait_loss, method, value, threshold, fetch_probability,
-             seeds, lerp=lerp_f32):
+             seeds, lerp=lerp_f32, add=None):
+    """init (G, n) and deltas (T, G, n): fp32 arrays, or raw bf16 bits (uint16) with
+    lerp=lerp_bf16, add=add_bf16."""
     G, n = init.shape
     T = deltas.shape[0]
     learners = [OracleLearner(names[g], [x for x in names if x != names[g]], fetch_probability,
@@ -33,7 +42,8 @@ def simulate(names, init, deltas, send_loss, wait_loss, method, value, threshold
             snaps.append(params[g].copy())
             fetching[r, g] = learners[g].fetching
         for g in range(G):
-            params[g] = np.add(params[g], deltas[r, g], dtype=params.dtype)
+            params[g] = (np.add(params[g], deltas[r, g], dtype=params.dtype) if add is None
+                         else add(params[g], deltas[r, g]))
         for g in range(G):
             L = learners[g]
             state, payload, attempts = None, None, []

@@ -14,13 +14,33 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-def inputs(world, n, T, seed=0):
+def inputs(world, n, T, seed=0, dtype="f32"):
+    """Initial parameters, per-round training deltas and losses; bf16 as raw bits (uint16)."""
     rng = np.random.default_rng(seed)
     init = rng.standard_normal((world, n)).astype(np.float32)
     deltas = (0.01 * rng.standard_normal((T, world, n))).astype(np.float32)
     send = [[float(2 * np.exp(-r / 4) + 0.05 * rng.random()) for _ in range(world)] for r in range(T)]
     wait = [[float(2 * np.exp(-(r + .5) / 4) + 0.05 * rng.random()) for _ in range(world)] for r in range(T)]
+    if dtype == "bf16":
+        from oracle.lerp import f32_to_bf16
+        init, deltas = f32_to_bf16(init), f32_to_bf16(deltas)
     return init, deltas, send, wait
+
+
+def to_device(a, dev):
+    """An fp32 array, or raw bf16 bits (uint16), as a device tensor of that dtype."""
+    import torch
+    if a.dtype == np.uint16:
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).to(dev).view(torch.bfloat16)
+    return torch.from_numpy(a).to(dev)
+
+
+def to_host(t):
+    """Inverse of to_device."""
+    import torch
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).cpu().numpy().view(np.uint16)
+    return t.cpu().numpy()
 
 
 def write_cfg(path, names, fp, interp, thr):
@@ -32,7 +52,7 @@ def write_cfg(path, names, fp, interp, thr):
         f.write("\n".join(lines) + "\n")
 
 
-def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of_rank, pull="copy"):
+def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of_rank, pull="copy", dtype="f32"):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -42,17 +62,17 @@ def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of
     torch.cuda.set_device(dev)
     from dpwa_amd import DpwaConnection
     from dpwa_amd.group import DistGroup
-    init, deltas, send, wait = inputs(world, n, T)
+    init, deltas, send, wait = inputs(world, n, T, dtype=dtype)
     names = ["r%d" % i for i in range(world)]
     conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank, pull=pull, group="lockstep")
     assert type(conn._group) is DistGroup
-    flat = torch.from_numpy(init[rank]).to(dev)
-    params = np.zeros((T, n), np.float32)
+    flat = to_device(init[rank], dev)
+    params = np.zeros((T, n), init.dtype)
     clocks = np.zeros(T)
     peers = []
     for r in range(T):
         conn.update_send(flat, send[r][rank])
-        flat.add_(torch.from_numpy(deltas[r, rank]).to(dev))
+        flat.add_(to_device(deltas[r, rank], dev))
         if r % 2:
             payload, factor = conn.update_wait(wait[r][rank])      # split: factor kernel, then lerp
             if payload is not None:
@@ -63,7 +83,7 @@ def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of
             peers.append(payload.peer)
         else:
             peers.append(None)
-        params[r] = flat.cpu().numpy()
+        params[r] = to_host(flat)
         clocks[r] = conn.clock
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=params, clocks=clocks,
              peers=np.array([p or "" for p in peers]))

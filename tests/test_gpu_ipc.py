@@ -32,21 +32,34 @@ def free_port():
                                                        (2, "clock", 1.0, 0.0, "relay:8"),
                                                        (3, "loss", 0.7, 0.5, "relay"),
                                                        (4, "clock", 0.6, 0.0, "relay:16")])
-def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100_003):
+def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100_003, dtype="f32"):
     T = 12
     names = ["r%d" % i for i in range(world)]
     cfg = str(tmp_path / "dist.yaml")
     dist_worker.write_cfg(cfg, names, fp, interp, thr)
-    mp.spawn(dist_worker.gossip_worker, args=(world, free_port(), cfg, str(tmp_path), n, T, "gloo", 0, pull),
+    mp.spawn(dist_worker.gossip_worker, args=(world, free_port(), cfg, str(tmp_path), n, T, "gloo", 0, pull, dtype),
              nprocs=world, join=True)
-    init, deltas, send, wait = dist_worker.inputs(world, n, T)
-    exp = ogossip.simulate(names, init, deltas, send, wait, interp, 0.5, thr, fp, [500 + r for r in range(world)])
+    init, deltas, send, wait = dist_worker.inputs(world, n, T, dtype=dtype)
+    kw = dict(lerp=olerp.lerp_bf16, add=ogossip.add_bf16) if dtype == "bf16" else {}
+    exp = ogossip.simulate(names, init, deltas, send, wait, interp, 0.5, thr, fp, [500 + r for r in range(world)],
+                           **kw)
     for r in range(world):
         got = np.load(tmp_path / ("rank%d.npz" % r))
         want_peers = [p[0] if p else "" for p in (exp["picks"][t][r] for t in range(T))]
         assert list(got["peers"]) == want_peers, r
         assert np.array_equal(got["clocks"], exp["clocks"][:, r]), r
         assert olerp.bits_equal(got["params"], exp["params"][:, r]), r
+
+
+@pytest.mark.parametrize("world,interp,fp,thr,pull", [(2, "clock", 1.0, 0.0, "copy"),
+                                                       (3, "loss", 0.7, 0.5, "kernel:64"),
+                                                       (3, "clock", 0.8, 0.0, "relay:8")])
+def test_ipc_gossip_bf16_matches_oracle(tmp_path, world, interp, fp, thr, pull):
+    """bf16 through every pull (BASELINE configs[3-4] dtype) with an odd element count: the
+    payload (2n bytes) is not a multiple of the 16-byte vector, so the copy engine, the pull
+    kernel and the relay's stripes all handle a ragged tail; bit-exact against the oracle's
+    torch-eager bf16 lerp and bf16 training-step add."""
+    test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100_003, dtype="bf16")
 
 
 @pytest.mark.parametrize("pull", ["relay:8", "kernel"])

@@ -209,3 +209,14 @@ def test_async_checker_distributed_digests():
     torn = params[0].copy()
     torn[4, 7] += 1.0
     assert any("round 4" in b for b in check.check_rank_digests(0, torn, clocks[0], n, expected))
+
+
+def test_bf16_training_add_matches_torch():
+    """oracle.gossip.add_bf16 (the bf16 multi-process tests' training step) is torch's bf16
+    add_ (no reference bf16 path exists; pinned to torch-eager like the bf16 lerp)."""
+    from tests import dist_worker
+    init, deltas, _, _ = dist_worker.inputs(2, 50_001, 3, dtype="bf16")
+    for g in range(2):
+        p = dist_worker.to_device(init[g].copy(), "cpu")     # from_numpy shares the array
+        p.add_(dist_worker.to_device(deltas[1, g], "cpu"))
+        assert np.array_equal(dist_worker.to_host(p), ogossip.add_bf16(init[g], deltas[1, g]))
