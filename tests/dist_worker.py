@@ -4,6 +4,7 @@ Each rank runs one DpwaConnection on its node under torch.distributed (world siz
 of nodes): the lock-step DistGroup for the trajectory tests, the free-running AsyncDistGroup
 (the default) for the board tests.
 """
+import hashlib
 import os
 import sys
 
@@ -17,8 +18,9 @@ if ROOT not in sys.path:
 def inputs(world, n, T, seed=0, dtype="f32"):
     """Initial parameters, per-round training deltas and losses; bf16 as raw bits (uint16)."""
     rng = np.random.default_rng(seed)
-    init = rng.standard_normal((world, n)).astype(np.float32)
-    deltas = (0.01 * rng.standard_normal((T, world, n))).astype(np.float32)
+    init = rng.standard_normal((world, n), dtype=np.float32)
+    deltas = rng.standard_normal((T, world, n), dtype=np.float32)
+    deltas *= np.float32(0.01)
     send = [[float(2 * np.exp(-r / 4) + 0.05 * rng.random()) for _ in range(world)] for r in range(T)]
     wait = [[float(2 * np.exp(-(r + .5) / 4) + 0.05 * rng.random()) for _ in range(world)] for r in range(T)]
     if dtype == "bf16":
@@ -52,7 +54,10 @@ def write_cfg(path, names, fp, interp, thr):
         f.write("\n".join(lines) + "\n")
 
 
-def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of_rank, pull="copy", dtype="f32"):
+def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of_rank, pull="copy", dtype="f32",
+                  digest=False):
+    """Lock-step rounds through DistGroup; saves every round's parameters (or, with
+    `digest`, their sha1 -- for full-size vectors), clock and peer."""
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -67,7 +72,7 @@ def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of
     conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank, pull=pull, group="lockstep")
     assert type(conn._group) is DistGroup
     flat = to_device(init[rank], dev)
-    params = np.zeros((T, n), init.dtype)
+    params = [] if digest else np.zeros((T, n), init.dtype)
     clocks = np.zeros(T)
     peers = []
     for r in range(T):
@@ -83,7 +88,10 @@ def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of
             peers.append(payload.peer)
         else:
             peers.append(None)
-        params[r] = to_host(flat)
+        if digest:
+            params.append(hashlib.sha1(to_host(flat).tobytes()).hexdigest())
+        else:
+            params[r] = to_host(flat)
         clocks[r] = conn.clock
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=params, clocks=clocks,
              peers=np.array([p or "" for p in peers]))

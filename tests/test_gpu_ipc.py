@@ -62,6 +62,29 @@ def test_ipc_gossip_bf16_matches_oracle(tmp_path, world, interp, fp, thr, pull):
     test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100_003, dtype="bf16")
 
 
+@pytest.mark.parametrize("pull", ["copy", "relay:64"])
+def test_ipc_gossip_configs2_full_size(tmp_path, pull):
+    """BASELINE configs[2] at its own size and interpolation through the multi-process path:
+    100,000,000 fp32 per rank, clock interpolation, lock-step rounds over IPC-mapped slots
+    (here two ranks share the one GPU); every round's parameters compared with the oracle by
+    sha1 of the whole vector, clocks and peers exactly."""
+    import hashlib
+    world, n, T = 2, 100_000_000, 3
+    names = ["r%d" % i for i in range(world)]
+    cfg = str(tmp_path / "c2.yaml")
+    dist_worker.write_cfg(cfg, names, 1.0, "clock", 0.0)
+    mp.spawn(dist_worker.gossip_worker,
+             args=(world, free_port(), cfg, str(tmp_path), n, T, "gloo", 0, pull, "f32", True), nprocs=world, join=True)
+    init, deltas, send, wait = dist_worker.inputs(world, n, T)
+    exp = ogossip.simulate(names, init, deltas, send, wait, "clock", 0.5, 0.0, 1.0, [500 + r for r in range(world)])
+    for r in range(world):
+        got = np.load(tmp_path / ("rank%d.npz" % r))
+        assert list(got["peers"]) == [p[0] if p else "" for p in (exp["picks"][t][r] for t in range(T))], r
+        assert np.array_equal(got["clocks"], exp["clocks"][:, r]), r
+        want = [hashlib.sha1(exp["params"][t, r].tobytes()).hexdigest() for t in range(T)]
+        assert list(got["params"]) == want, r
+
+
 @pytest.mark.parametrize("pull", ["relay:8", "kernel"])
 def test_ipc_gossip_six_ranks(tmp_path, monkeypatch, pull):
     """Six ranks (the relay's stripes over more than four peers).  Six processes on one card
