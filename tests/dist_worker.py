@@ -232,3 +232,85 @@ def async_wt_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy"):
         time.sleep(0.01)
     conn.close()
     os._exit(0)
+
+
+# -- full-size multi-process runs (BASELINE configs[3-4]: 1B / 7B bf16) -------------------------
+# Parameters and training deltas are closed-form functions of the element index, computed the
+# same way on the device (chunked, int64 torch ops) and in numpy for a few sampled windows, so
+# the oracle replays the windows without materialising 7B elements on the host.  Values are
+# k / 2^23 - 1/2 with an integer k < 2^23 (exact in fp32), deltas the same times 2^-7.
+_CHUNK = 1 << 27
+
+
+def synth_f32(idx, g, r):
+    """fp32 values at int64 indices `idx` for rank g; r = -1: initial parameters, r >= 0: the
+    training delta of round r.  Works on numpy arrays and on torch tensors alike."""
+    m = (1 << 23) - 1        # the low and high index bits hashed apart: no int64 overflow
+    k = ((idx & m) * 5039617 + (idx >> 23) * 3141597 + (g * 40503 + (r + 1) * 977)) & m
+    if isinstance(k, np.ndarray):
+        v = k.astype(np.float32) * np.float32(2.0 ** -23) - np.float32(0.5)
+        return v * np.float32(2.0 ** -7) if r >= 0 else v
+    import torch
+    v = k.to(torch.float32) * (2.0 ** -23) - 0.5
+    return v * (2.0 ** -7) if r >= 0 else v
+
+
+def synth_windows(n):
+    """Sampled [begin, end) windows: head, middle, a ragged tail."""
+    return [(0, 4096), (n // 2 - 2048, n // 2 + 2048), (n - 4099, n)]
+
+
+def synth_losses(world, T):
+    """Losses crossing a 0.5 divergence threshold within T rounds (configs[3])."""
+    send = [[1.2 * 0.55 ** r + 0.01 * g for g in range(world)] for r in range(T)]
+    wait = [[1.1 * 0.55 ** r + 0.02 * g for g in range(world)] for r in range(T)]
+    return send, wait
+
+
+def _synth_fill(flat, g, r, add):
+    import torch
+    n = flat.numel()
+    for b in range(0, n, _CHUNK):
+        e = min(n, b + _CHUNK)
+        v = synth_f32(torch.arange(b, e, device=flat.device, dtype=torch.int64), g, r).to(flat.dtype)
+        if add:
+            flat[b:e].add_(v)
+        else:
+            flat[b:e].copy_(v)
+
+
+def big_worker(rank, world, port, cfg_path, out_dir, n, T, pull, dtype):
+    """Lock-step rounds at full size (DistGroup over IPC, gloo barrier on one GPU); records the
+    sampled windows of the parameters after every round, the clocks and the peers."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from dpwa_amd import DpwaConnection
+    names = ["r%d" % i for i in range(world)]
+    conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank, pull=pull, group="lockstep")
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    flat = torch.empty(n, dtype=tdt, device=dev)
+    _synth_fill(flat, rank, -1, add=False)
+    send, wait = synth_losses(world, T)
+    wins, clocks, peers = [], np.zeros(T), []
+    for r in range(T):
+        conn.update_send(flat, send[r][rank], reuse_snapshot=r >= 2)
+        _synth_fill(flat, rank, r, add=True)
+        if r == 0:
+            payload, _ = conn.update_wait(wait[r][rank])
+            if payload is not None:
+                conn.average(flat)
+        else:                           # the adapter's default: fused, write-through
+            payload, _ = conn.update_wait_average(flat, wait[r][rank], write_through=True)
+        peers.append(payload.peer if payload is not None else "")
+        wins.append(np.concatenate([to_host(flat[b:e]) for b, e in synth_windows(n)]))
+        clocks[r] = conn.clock
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=np.stack(wins), clocks=clocks, peers=np.array(peers))
+    torch.cuda.synchronize()
+    dist.barrier()
+    conn.close()
+    dist.destroy_process_group()

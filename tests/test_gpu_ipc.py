@@ -85,6 +85,35 @@ def test_ipc_gossip_configs2_full_size(tmp_path, pull):
         assert list(got["params"]) == want, r
 
 
+@pytest.mark.parametrize("n,interp,fp,thr,pull", [(1_000_000_000, "loss", 1.0, 0.5, "relay:128"),
+                                                  (7_000_000_000, "constant", 0.7, 0.0, "copy"),
+                                                  (7_000_000_000, "constant", 0.7, 0.0, "kernel:512")])
+def test_ipc_gossip_configs3_4_full_size(tmp_path, n, interp, fp, thr, pull):
+    """BASELINE configs[3] (1B bf16, loss interpolation, divergence_threshold 0.5 crossed by a
+    decaying loss) and configs[4] (7B bf16, fetch_probability 0.7) at full size through the
+    multi-process path: two ranks over IPC-mapped slots (byte offsets beyond 2^32), split and
+    fused write-through rounds; sampled windows of every round's parameters (head, middle,
+    ragged tail) bit-exact against the oracle replaying those windows, clocks and peers exact."""
+    world, T = 2, 4
+    names = ["r%d" % i for i in range(world)]
+    cfg = str(tmp_path / "big.yaml")
+    dist_worker.write_cfg(cfg, names, fp, interp, thr)
+    mp.spawn(dist_worker.big_worker, args=(world, free_port(), cfg, str(tmp_path), n, T, pull, "bf16"),
+             nprocs=world, join=True)
+    idx = np.concatenate([np.arange(b, e, dtype=np.int64) for b, e in dist_worker.synth_windows(n)])
+    init = np.stack([olerp.f32_to_bf16(dist_worker.synth_f32(idx, g, -1)) for g in range(world)])
+    deltas = np.stack([np.stack([olerp.f32_to_bf16(dist_worker.synth_f32(idx, g, r)) for g in range(world)])
+                       for r in range(T)])
+    send, wait = dist_worker.synth_losses(world, T)
+    exp = ogossip.simulate(names, init, deltas, send, wait, interp, 0.5, thr, fp, [500 + r for r in range(world)],
+                           lerp=olerp.lerp_bf16, add=ogossip.add_bf16)
+    for r in range(world):
+        got = np.load(tmp_path / ("rank%d.npz" % r))
+        assert list(got["peers"]) == [p[0] if p else "" for p in (exp["picks"][t][r] for t in range(T))], r
+        assert np.array_equal(got["clocks"], exp["clocks"][:, r]), r
+        assert olerp.bits_equal(got["params"], exp["params"][:, r]), r
+
+
 @pytest.mark.parametrize("pull", ["relay:8", "kernel"])
 def test_ipc_gossip_six_ranks(tmp_path, monkeypatch, pull):
     """Six ranks (the relay's stripes over more than four peers).  Six processes on one card
