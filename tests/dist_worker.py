@@ -282,6 +282,12 @@ def _synth_fill(flat, g, r, add):
 def big_worker(rank, world, port, cfg_path, out_dir, n, T, pull, dtype):
     """Lock-step rounds at full size (DistGroup over IPC, gloo barrier on one GPU); records the
     sampled windows of the parameters after every round, the clocks and the peers."""
+    import time
+    t0 = time.perf_counter()
+
+    def log(msg):
+        sys.stderr.write("[big_worker r%d +%.1fs] %s\n" % (rank, time.perf_counter() - t0, msg))
+        sys.stderr.flush()
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -289,12 +295,15 @@ def big_worker(rank, world, port, cfg_path, out_dir, n, T, pull, dtype):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    log("process group up")
     from dpwa_amd import DpwaConnection
     names = ["r%d" % i for i in range(world)]
     conn = DpwaConnection(names[rank], cfg_path, seed=500 + rank, pull=pull, group="lockstep")
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     flat = torch.empty(n, dtype=tdt, device=dev)
     _synth_fill(flat, rank, -1, add=False)
+    torch.cuda.synchronize()
+    log("%d parameters filled" % n)
     send, wait = synth_losses(world, T)
     wins, clocks, peers = [], np.zeros(T), []
     for r in range(T):
@@ -309,6 +318,7 @@ def big_worker(rank, world, port, cfg_path, out_dir, n, T, pull, dtype):
         peers.append(payload.peer if payload is not None else "")
         wins.append(np.concatenate([to_host(flat[b:e]) for b, e in synth_windows(n)]))
         clocks[r] = conn.clock
+        log("round %d done (peer %s)" % (r, peers[-1] or "-"))
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=np.stack(wins), clocks=clocks, peers=np.array(peers))
     torch.cuda.synchronize()
     dist.barrier()
