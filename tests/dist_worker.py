@@ -306,15 +306,25 @@ def big_worker(rank, world, port, cfg_path, out_dir, n, T, pull, dtype):
     log("%d parameters filled" % n)
     send, wait = synth_losses(world, T)
     wins, clocks, peers = [], np.zeros(T), []
+    trace = os.environ.get("DPWA_TEST_TRACE") == "1"
+
+    def step(msg):
+        if trace:
+            torch.cuda.synchronize()
+            log(msg)
     for r in range(T):
         conn.update_send(flat, send[r][rank], reuse_snapshot=r >= 2)
+        step("round %d: update_send" % r)
         _synth_fill(flat, rank, r, add=True)
+        step("round %d: training step" % r)
         if r == 0:
             payload, _ = conn.update_wait(wait[r][rank])
+            step("round %d: update_wait" % r)
             if payload is not None:
                 conn.average(flat)
         else:                           # the adapter's default: fused, write-through
             payload, _ = conn.update_wait_average(flat, wait[r][rank], write_through=True)
+        step("round %d: averaged" % r)
         peers.append(payload.peer if payload is not None else "")
         wins.append(np.concatenate([to_host(flat[b:e]) for b, e in synth_windows(n)]))
         clocks[r] = conn.clock
