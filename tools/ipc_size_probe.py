@@ -18,7 +18,12 @@ def hip():
         paths = sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})
     lib = ctypes.CDLL(paths[0])
     lib.hipGetErrorString.restype = ctypes.c_char_p
+    lib.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), Handle, ctypes.c_uint]
     return lib
+
+
+class Handle(ctypes.Structure):           # hipIpcMemHandle_t, passed by value
+    _fields_ = [("reserved", ctypes.c_char * 64)]
 
 
 def worker(rank, port, sizes):
@@ -46,7 +51,7 @@ def worker(rank, port, sizes):
         blob = [handle.raw if rank == 0 else None]
         dist.broadcast_object_list(blob, src=0)
         if rank == 1:
-            h = ctypes.create_string_buffer(blob[0], 64)
+            h = Handle.from_buffer_copy(blob[0])
             opened = ctypes.c_void_p()
             log("%.2f GiB hipIpcOpenMemHandle ..." % gib)
             rc = lib.hipIpcOpenMemHandle(ctypes.byref(opened), h, ctypes.c_uint(1))
