@@ -1,15 +1,16 @@
 // Diagnostic: share a multi-GiB device buffer between two processes with HIP's virtual memory
 // API instead of hipIpcOpenMemHandle (which hangs above ~2 GiB on this image).  The buffer
 // is hipMemCreate'd in chunks, mapped contiguously in the exporter; each chunk is exported as
-// a POSIX fd, the importer fetches the fds with pidfd_getfd, maps them contiguously and reads
-// both sides of every chunk boundary.  fork() happens before any HIP call.
+// a POSIX fd and passed over a Unix socket (SCM_RIGHTS; pidfd_getfd is not permitted between
+// sibling processes here); the importer maps them contiguously and reads both sides of every
+// chunk boundary.  fork() happens before any HIP call.
 //   hipcc -O2 tools/vmm_probe.cpp -o tools/vmm_probe && tools/vmm_probe 6 1
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <sys/syscall.h>
+#include <sys/socket.h>
 #include <sys/wait.h>
 #include <unistd.h>
 #include <vector>
@@ -40,12 +41,12 @@ int main(int argc, char **argv)
 {
     const double gib = argc > 1 ? std::atof(argv[1]) : 6.0;
     const double chunk_gib = argc > 2 ? std::atof(argv[2]) : 1.0;
-    int pipefd[2];
-    if (pipe(pipefd) != 0) return 3;
+    int sv[2];
+    if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) return 3;
     const pid_t child = fork();
     if (child != 0) {   // ------------------------------------------------ exporter
         who = "exporter";
-        close(pipefd[0]);
+        close(sv[0]);
         hipMemAllocationProp prop = prop_for(0);
         size_t gran = 0;
         CK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
@@ -75,8 +76,23 @@ int main(int argc, char **argv)
         std::printf("[exporter] %d chunks of %zu bytes (granularity %zu), total %zu\n", k, chunk, gran, total);
         std::fflush(stdout);
         long msg[3] = {(long)getpid(), (long)k, (long)chunk};
-        if (write(pipefd[1], msg, sizeof(msg)) != sizeof(msg)) return 4;
-        if (write(pipefd[1], fds.data(), sizeof(int) * k) != (ssize_t)(sizeof(int) * k)) return 4;
+        for (int i = 0; i < k; ++i) {   // one message per chunk: the header words + its fd
+            struct iovec io = {msg, sizeof(msg)};
+            char cbuf[CMSG_SPACE(sizeof(int))];
+            std::memset(cbuf, 0, sizeof(cbuf));
+            struct msghdr mh;
+            std::memset(&mh, 0, sizeof(mh));
+            mh.msg_iov = &io;
+            mh.msg_iovlen = 1;
+            mh.msg_control = cbuf;
+            mh.msg_controllen = sizeof(cbuf);
+            struct cmsghdr *c = CMSG_FIRSTHDR(&mh);
+            c->cmsg_level = SOL_SOCKET;
+            c->cmsg_type = SCM_RIGHTS;
+            c->cmsg_len = CMSG_LEN(sizeof(int));
+            std::memcpy(CMSG_DATA(c), &fds[i], sizeof(int));
+            if (sendmsg(sv[1], &mh, 0) != (ssize_t)sizeof(msg)) return 4;
+        }
         int status = 0;
         waitpid(child, &status, 0);
         CK(hipMemUnmap(base, total));
@@ -87,29 +103,33 @@ int main(int argc, char **argv)
     }
     // ---------------------------------------------------------------- importer
     who = "importer";
-    close(pipefd[1]);
+    close(sv[1]);
     long msg[3];
-    if (read(pipefd[0], msg, sizeof(msg)) != sizeof(msg)) return 6;
-    const pid_t owner = (pid_t)msg[0];
+    std::vector<int> rfds;
+    do {
+        struct iovec io = {msg, sizeof(msg)};
+        char cbuf[CMSG_SPACE(sizeof(int))];
+        struct msghdr mh;
+        std::memset(&mh, 0, sizeof(mh));
+        mh.msg_iov = &io;
+        mh.msg_iovlen = 1;
+        mh.msg_control = cbuf;
+        mh.msg_controllen = sizeof(cbuf);
+        if (recvmsg(sv[0], &mh, MSG_WAITALL) != (ssize_t)sizeof(msg)) return 6;
+        struct cmsghdr *c = CMSG_FIRSTHDR(&mh);
+        if (!c || c->cmsg_type != SCM_RIGHTS) return 7;
+        int fd;
+        std::memcpy(&fd, CMSG_DATA(c), sizeof(int));
+        rfds.push_back(fd);
+    } while ((long)rfds.size() < msg[1]);
     const int k = (int)msg[1];
     const size_t chunk = (size_t)msg[2];
-    std::vector<int> rfds((size_t)k);
-    if (read(pipefd[0], rfds.data(), sizeof(int) * k) != (ssize_t)(sizeof(int) * k)) return 6;
-    const int pidfd = (int)syscall(SYS_pidfd_open, owner, 0);
-    if (pidfd < 0) {
-        std::perror("pidfd_open");
-        return 7;
-    }
     const size_t total = chunk * (size_t)k;
     void *base = nullptr;
     CK(hipMemAddressReserve(&base, total, 0, nullptr, 0));
     std::vector<hipMemGenericAllocationHandle_t> h((size_t)k);
     for (int i = 0; i < k; ++i) {
-        const int fd = (int)syscall(SYS_pidfd_getfd, pidfd, rfds[i], 0);
-        if (fd < 0) {
-            std::perror("pidfd_getfd");
-            return 8;
-        }
+        const int fd = rfds[i];
         CK(hipMemImportFromShareableHandle(&h[i], (void *)(intptr_t)fd, hipMemHandleTypePosixFileDescriptor));
         CK(hipMemMap((char *)base + (size_t)i * chunk, chunk, 0, h[i], 0));
         close(fd);
