@@ -87,6 +87,8 @@ SIGNATURES = {
     "dpwa_learner_attach_local": [_vp, _int, _vp],
     "dpwa_learner_ipc_handle": [_vp, _vp, _i64],
     "dpwa_learner_attach_ipc": [_vp, _int, _vp, _i64],
+    "dpwa_learner_export_fds": [_vp, _int, _pint, _int, _pint, ctypes.POINTER(_i64)],
+    "dpwa_learner_attach_fds": [_vp, _int, _vp, _i64, _pint, _int, _i64],
     "dpwa_learner_fetch": [_vp, _int, _u64, _int, _vp],
     "dpwa_learner_average": [_vp, _vp, _dbl, _vp, _vp],
     "dpwa_learner_average_through": [_vp, _vp, _dbl, _vp, _vp],
@@ -101,6 +103,7 @@ SIGNATURES = {
     "dpwa_learner_relay_enable": [_vp, _int, _int],
     "dpwa_learner_relay_handle": [_vp, _vp, _i64],
     "dpwa_learner_relay_attach": [_vp, _int, _int, _vp, _i64],
+    "dpwa_learner_relay_attach_fds": [_vp, _int, _int, _vp, _i64, _pint, _int, _i64],
     "dpwa_learner_relay_wait": [_vp, _vp],
     "dpwa_learner_relay_phase1": [_vp, _vp, _u64, _int, _vp],
     "dpwa_learner_relay_phase2": [_vp, _vp, _int, _u64, _int],

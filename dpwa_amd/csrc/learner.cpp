@@ -64,9 +64,173 @@ struct IpcBlob {
     int32_t dtype;
     int32_t device;
     int32_t pid;
-    int32_t reserved;
+    int32_t vmm;                // 1: the allocation is shared as fds (dpwa_learner_export_fds)
 };
 static_assert(sizeof(IpcBlob) <= DPWA_IPC_HANDLE_BYTES, "IPC blob too large");
+
+// An exportable device allocation (snapshot slots, relay buffer).  Ordinary allocations come
+// from hipMalloc and are shared with hipIpcGetMemHandle / hipIpcOpenMemHandle.  On this ROCm
+// stack hipIpcOpenMemHandle never returns for allocations above ~2 GiB (tools/ipc_size_probe.py),
+// so allocations from kVmmMinBytes up (or any size with DPWA_VMM=1) are built from hipMemCreate
+// chunks mapped contiguously, and shared as one POSIX fd per chunk (hipMemExportToShareableHandle)
+// that the peer maps contiguously again (tools/vmm_probe.cpp; streaming rates equal hipMalloc's,
+// tools/vmm_perf.hip).
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+constexpr size_t kVmmMinBytes = (size_t)3 << 29;     // 1.5 GiB
+constexpr size_t kVmmChunk = (size_t)1 << 30;        // 1 GiB per exported chunk
+constexpr size_t kVmmAlign = (size_t)2 << 20;
+
+struct DevMem {
+    char *ptr = nullptr;
+    size_t bytes = 0;                                   // mapped bytes (VMM: chunk multiple)
+    size_t chunk = 0;
+    std::vector<hipMemGenericAllocationHandle_t> handles;   // VMM chunks; empty: hipMalloc
+    bool vmm() const { return !handles.empty(); }
+};
+
+hipMemAllocationProp vmm_prop(int device)
+{
+    hipMemAllocationProp p;
+    memset(&p, 0, sizeof(p));
+    p.type = hipMemAllocationTypePinned;
+    p.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
+    p.location.type = hipMemLocationTypeDevice;
+    p.location.id = device;
+    return p;
+}
+
+hipError_t vmm_grant(const DevMem &m, int device)
+{
+    hipMemAccessDesc a;
+    memset(&a, 0, sizeof(a));
+    a.location.type = hipMemLocationTypeDevice;
+    a.location.id = device;
+    a.flags = hipMemAccessFlagsProtReadWrite;
+    return hipMemSetAccess(m.ptr, m.bytes, &a, 1);
+}
+
+void devmem_free(DevMem &m)
+{
+    if (!m.ptr) return;
+    if (m.vmm()) {
+        (void)hipMemUnmap(m.ptr, m.bytes);
+        for (auto h : m.handles) (void)hipMemRelease(h);
+        (void)hipMemAddressFree(m.ptr, m.bytes);
+    } else {
+        (void)hipFree(m.ptr);
+    }
+    m = DevMem();
+}
+
+// Maps `n` chunks (VMM handles in h[]) contiguously into a fresh reservation, readable and
+// writable from `device`; releases the handles on failure.
+hipError_t vmm_map(DevMem &m, std::vector<hipMemGenericAllocationHandle_t> &h, size_t chunk, int device)
+{
+    m = DevMem();
+    const size_t total = chunk * h.size();
+    void *va = nullptr;
+    hipError_t e = hipMemAddressReserve(&va, total, kVmmAlign, nullptr, 0);
+    size_t mapped = 0;
+    if (e == hipSuccess) {
+        for (; mapped < h.size(); ++mapped)
+            if ((e = hipMemMap((char *)va + mapped * chunk, chunk, 0, h[mapped], 0)) != hipSuccess) break;
+    }
+    m.ptr = (char *)va;
+    m.bytes = total;
+    m.chunk = chunk;
+    if (e == hipSuccess) {
+        m.handles = h;
+        if ((e = vmm_grant(m, device)) == hipSuccess) return hipSuccess;
+    }
+    if (va) {
+        if (mapped) (void)hipMemUnmap(va, mapped * chunk);
+        (void)hipMemAddressFree(va, total);
+    }
+    for (auto x : h) (void)hipMemRelease(x);
+    h.clear();
+    m = DevMem();
+    return e;
+}
+
+bool use_vmm(size_t bytes)
+{
+    const char *e = getenv("DPWA_VMM");
+    if (e && e[0] == '1') return true;
+    if (e && e[0] == '0') return false;
+    return bytes >= kVmmMinBytes;
+}
+
+hipError_t devmem_alloc(DevMem &m, size_t bytes, int device)
+{
+    m = DevMem();
+    if (!use_vmm(bytes)) {
+        hipError_t e = hipMalloc(&m.ptr, bytes);
+        if (e == hipSuccess) m.bytes = bytes;
+        return e;
+    }
+    const hipMemAllocationProp prop = vmm_prop(device);
+    size_t gran = 0;
+    hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+    if (e != hipSuccess) return e;
+    const size_t unit = std::max(gran, kVmmAlign);
+    size_t chunk = std::min(kVmmChunk, round_up(bytes, unit));
+    chunk = round_up(chunk, unit);
+    const size_t n = (bytes + chunk - 1) / chunk;
+    std::vector<hipMemGenericAllocationHandle_t> h;
+    for (size_t i = 0; i < n; ++i) {
+        hipMemGenericAllocationHandle_t x;
+        if ((e = hipMemCreate(&x, chunk, &prop, 0)) != hipSuccess) {
+            for (auto y : h) (void)hipMemRelease(y);
+            return e;
+        }
+        h.push_back(x);
+    }
+    return vmm_map(m, h, chunk, device);
+}
+
+// One POSIX fd per chunk of a VMM allocation (the caller closes them).
+int devmem_export(const DevMem &m, int *fds, int max_fds, int *n_fds, int64_t *chunk_bytes)
+{
+    *n_fds = 0;
+    if (chunk_bytes) *chunk_bytes = (int64_t)m.chunk;
+    if (!m.vmm()) return DPWA_OK;
+    if ((int)m.handles.size() > max_fds)
+        return set_error(DPWA_ERR_ARG, "export: %zu chunks, room for %d fds", m.handles.size(), max_fds);
+    for (size_t i = 0; i < m.handles.size(); ++i) {
+        int fd = -1;
+        hipError_t e = hipMemExportToShareableHandle(&fd, m.handles[i], hipMemHandleTypePosixFileDescriptor, 0);
+        if (e != hipSuccess) {
+            for (int j = 0; j < (int)i; ++j) close(fds[j]);
+            return set_error(DPWA_ERR_HIP, "hipMemExportToShareableHandle: %s", hipGetErrorString(e));
+        }
+        fds[i] = fd;
+    }
+    *n_fds = (int)m.handles.size();
+    return DPWA_OK;
+}
+
+// Maps a peer's exported chunks (fds from devmem_export, received over a Unix socket) into
+// this process, readable and writable from `device`.  The fds stay the caller's.
+int devmem_import(DevMem &m, const int *fds, int n_fds, int64_t chunk, size_t need_bytes, int device)
+{
+    if (n_fds < 1 || chunk <= 0 || (size_t)chunk * (size_t)n_fds < need_bytes)
+        return set_error(DPWA_ERR_ARG, "import: %d chunks of %lld bytes for %zu bytes", n_fds, (long long)chunk,
+                         need_bytes);
+    std::vector<hipMemGenericAllocationHandle_t> h;
+    for (int i = 0; i < n_fds; ++i) {
+        hipMemGenericAllocationHandle_t x;
+        hipError_t e = hipMemImportFromShareableHandle(&x, (void *)(intptr_t)fds[i], hipMemHandleTypePosixFileDescriptor);
+        if (e != hipSuccess) {
+            for (auto y : h) (void)hipMemRelease(y);
+            return set_error(DPWA_ERR_HIP, "hipMemImportFromShareableHandle: %s", hipGetErrorString(e));
+        }
+        h.push_back(x);
+    }
+    hipError_t e = vmm_map(m, h, (size_t)chunk, device);
+    if (e != hipSuccess) return set_error(DPWA_ERR_HIP, "import: mapping the peer's chunks: %s", hipGetErrorString(e));
+    return DPWA_OK;
+}
 
 struct Ctl {            // device control block
     double clock[4];    // a ring: a factor reads clock[cur] and writes clock[cur+1]; a
@@ -75,7 +239,6 @@ struct Ctl {            // device control block
     dpwa_coef coef;
 };
 
-size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // Registry of live learners, so a learner never dereferences a destroyed local peer.
 std::mutex g_reg_mu;
@@ -108,7 +271,18 @@ struct Endpoint {
     int64_t slot_stride = 0;
     int64_t n = 0;
     int32_t dtype = 0;
+    DevMem imported;                 // kind 2 through fds (VMM); empty: hipIpc-opened `base`
 };
+
+static void close_endpoint(Endpoint &ep)
+{
+    if (ep.kind != 2 || !ep.base) return;
+    if (ep.imported.vmm())
+        devmem_free(ep.imported);
+    else
+        (void)hipIpcCloseMemHandle(ep.base);
+    ep.base = nullptr;
+}
 
 struct dpwa_learner {
     int device = 0;
@@ -117,7 +291,8 @@ struct dpwa_learner {
     dpwa_interp cfg{};
     size_t payload_bytes = 0;
     size_t slot_stride = 0;
-    char *slots = nullptr;          // 2 slots
+    char *slots = nullptr;          // 2 slots (= slot_mem.ptr)
+    DevMem slot_mem;
     char *staging = nullptr;        // 1 slot
     Ctl *ctl = nullptr;
     uint64_t version = 0;
@@ -158,10 +333,12 @@ struct dpwa_learner {
     bool relay_on = false;
     int relay_world = 0, relay_rank = 0;
     int64_t relay_stripe = 0;
-    char *relay_buf = nullptr;               // world x stripe, IPC-exported
+    char *relay_buf = nullptr;               // world x stripe, IPC-exported (= relay_mem.ptr)
+    DevMem relay_mem;
     std::vector<const char *> relay_slots;   // per rank: slot 0 base (own or IPC-mapped)
     std::vector<const char *> relay_bufs;    // per rank: relay buffer (own or IPC-mapped)
     std::vector<char *> relay_opened;        // IPC mappings to close
+    std::vector<DevMem> relay_imported;      // fd-imported relay buffers to unmap
     hipEvent_t ev_relay = nullptr;           // all relay work of the last round
     bool relay_pending = false;
     // host readers of published slots (wire bridge) run on other threads
@@ -280,7 +457,8 @@ int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype
     l->slot_stride = kHeader + round_up(l->payload_bytes, 256);
     hipError_t e = hipSuccess;
     do {
-        if ((e = hipMalloc(&l->slots, 2 * l->slot_stride)) != hipSuccess) break;
+        if ((e = devmem_alloc(l->slot_mem, 2 * l->slot_stride, device)) != hipSuccess) break;
+        l->slots = l->slot_mem.ptr;
         if ((e = hipMalloc(&l->staging, l->slot_stride)) != hipSuccess) break;
         if ((e = hipMalloc(&l->ctl, sizeof(Ctl))) != hipSuccess) break;
         if ((e = hipMemset(l->slots, 0, kHeader)) != hipSuccess) break;
@@ -329,8 +507,7 @@ int dpwa_learner_destroy(dpwa_learner *l)
     }
     DeviceGuard dg(l->device);
     (void)hipDeviceSynchronize();
-    for (auto &kv : l->peers)
-        if (kv.second.kind == 2 && kv.second.base) (void)hipIpcCloseMemHandle(kv.second.base);
+    for (auto &kv : l->peers) close_endpoint(kv.second);
     if (l->side) (void)hipStreamDestroy(l->side);
     for (auto ev : l->ev_published)
         if (ev) (void)hipEventDestroy(ev);
@@ -350,10 +527,11 @@ int dpwa_learner_destroy(dpwa_learner *l)
         (void)hipEventDestroy(t.stop);
     }
     for (char *p : l->relay_opened) (void)hipIpcCloseMemHandle(p);
-    if (l->relay_buf) (void)hipFree(l->relay_buf);
+    for (auto &m : l->relay_imported) devmem_free(m);
+    devmem_free(l->relay_mem);
     if (l->read_stream) (void)hipStreamDestroy(l->read_stream);
     if (l->host_status) (void)hipHostFree(l->host_status);
-    if (l->slots) (void)hipFree(l->slots);
+    devmem_free(l->slot_mem);
     if (l->staging) (void)hipFree(l->staging);
     if (l->ctl) (void)hipFree(l->ctl);
     delete l;
@@ -457,6 +635,7 @@ int dpwa_learner_attach_local(dpwa_learner *l, int peer_id, dpwa_learner *peer)
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
             return set_error(DPWA_ERR_HIP, "hipDeviceEnablePeerAccess: %s", hipGetErrorString(e));
         (void)hipGetLastError();
+        if (peer->slot_mem.vmm()) HIP_TRY(vmm_grant(peer->slot_mem, l->device));   // VMM: per-device access
         peer->exported = true;   // read by another GPU: its publishes release at system scope
     }
     Endpoint ep;
@@ -471,48 +650,96 @@ int dpwa_learner_attach_local(dpwa_learner *l, int peer_id, dpwa_learner *peer)
     return DPWA_OK;
 }
 
+static IpcBlob make_blob(const dpwa_learner *l, const DevMem &m, int64_t stride)
+{
+    IpcBlob b;
+    memset(&b, 0, sizeof(b));
+    b.magic = kIpcMagic;
+    b.slot_stride = stride;
+    b.n = l->n;
+    b.dtype = l->dtype;
+    b.device = l->device;
+    b.pid = (int32_t)getpid();
+    b.vmm = m.vmm() ? 1 : 0;
+    return b;
+}
+
 int dpwa_learner_ipc_handle(dpwa_learner *l, void *handle_out, int64_t handle_len)
 {
     if (!l || !handle_out || handle_len < (int64_t)sizeof(IpcBlob))
         return set_error(DPWA_ERR_ARG, "dpwa_learner_ipc_handle: need %zu bytes", sizeof(IpcBlob));
     DeviceGuard dg(l->device);
-    IpcBlob b;
-    memset(&b, 0, sizeof(b));
-    HIP_TRY(hipIpcGetMemHandle(&b.handle, l->slots));
-    b.magic = kIpcMagic;
-    b.slot_stride = (int64_t)l->slot_stride;
-    b.n = l->n;
-    b.dtype = l->dtype;
-    b.device = l->device;
-    b.pid = (int32_t)getpid();
+    IpcBlob b = make_blob(l, l->slot_mem, (int64_t)l->slot_stride);
+    if (!b.vmm) HIP_TRY(hipIpcGetMemHandle(&b.handle, l->slots));   // else: fds, dpwa_learner_export_fds
     memset(handle_out, 0, (size_t)handle_len);
     memcpy(handle_out, &b, sizeof(b));
     l->exported = true;   // from now on publishes release at system scope
     return DPWA_OK;
 }
 
-int dpwa_learner_attach_ipc(dpwa_learner *l, int peer_id, const void *handle, int64_t handle_len)
+int dpwa_learner_export_fds(dpwa_learner *l, int which, int *fds, int max_fds, int *n_fds, int64_t *chunk_bytes)
 {
-    if (!l || !handle || handle_len < (int64_t)sizeof(IpcBlob)) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_ipc: bad handle");
-    IpcBlob b;
-    memcpy(&b, handle, sizeof(b));
-    if (b.magic != kIpcMagic) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_ipc: not a dpwa handle");
-    if (b.n != l->n || b.dtype != l->dtype)
-        return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_ipc: peer holds %lld elements of dtype %d, this learner %lld of %d",
-                         (long long)b.n, b.dtype, (long long)l->n, l->dtype);
+    if (!l || (which != 0 && which != 1) || !n_fds || (max_fds > 0 && !fds) || (which == 1 && !l->relay_on))
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_export_fds: bad arguments");
     DeviceGuard dg(l->device);
-    void *ptr = nullptr;
-    HIP_TRY(hipIpcOpenMemHandle(&ptr, b.handle, hipIpcMemLazyEnablePeerAccess));
+    const int rc = devmem_export(which == 0 ? l->slot_mem : l->relay_mem, fds, max_fds, n_fds, chunk_bytes);
+    if (rc == DPWA_OK) l->exported = true;
+    return rc;
+}
+
+static int check_blob(const dpwa_learner *l, const void *handle, int64_t handle_len, IpcBlob &b, const char *fn)
+{
+    if (!handle || handle_len < (int64_t)sizeof(IpcBlob)) return set_error(DPWA_ERR_ARG, "%s: bad handle", fn);
+    memcpy(&b, handle, sizeof(b));
+    if (b.magic != kIpcMagic) return set_error(DPWA_ERR_ARG, "%s: not a dpwa handle", fn);
+    if (b.n != l->n || b.dtype != l->dtype)
+        return set_error(DPWA_ERR_ARG, "%s: peer holds %lld elements of dtype %d, this learner %lld of %d", fn,
+                         (long long)b.n, b.dtype, (long long)l->n, l->dtype);
+    return DPWA_OK;
+}
+
+static void set_remote(dpwa_learner *l, int peer_id, const IpcBlob &b, char *base, DevMem &&imported)
+{
     auto it = l->peers.find(peer_id);
-    if (it != l->peers.end() && it->second.kind == 2 && it->second.base) (void)hipIpcCloseMemHandle(it->second.base);
+    if (it != l->peers.end()) close_endpoint(it->second);
     Endpoint ep;
     ep.kind = 2;
-    ep.base = (char *)ptr;
+    ep.base = base;
     ep.device = b.device;
     ep.slot_stride = b.slot_stride;
     ep.n = b.n;
     ep.dtype = b.dtype;
-    l->peers[peer_id] = ep;
+    ep.imported = std::move(imported);
+    l->peers[peer_id] = std::move(ep);
+}
+
+int dpwa_learner_attach_ipc(dpwa_learner *l, int peer_id, const void *handle, int64_t handle_len)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_ipc: NULL learner");
+    IpcBlob b;
+    int rc = check_blob(l, handle, handle_len, b, "dpwa_learner_attach_ipc");
+    if (rc) return rc;
+    if (b.vmm) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_ipc: the peer shares its slots as fds (dpwa_learner_attach_fds)");
+    DeviceGuard dg(l->device);
+    void *ptr = nullptr;
+    HIP_TRY(hipIpcOpenMemHandle(&ptr, b.handle, hipIpcMemLazyEnablePeerAccess));
+    set_remote(l, peer_id, b, (char *)ptr, DevMem());
+    return DPWA_OK;
+}
+
+int dpwa_learner_attach_fds(dpwa_learner *l, int peer_id, const void *handle, int64_t handle_len, const int *fds,
+                            int n_fds, int64_t chunk_bytes)
+{
+    if (!l || !fds) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_fds: bad arguments");
+    IpcBlob b;
+    int rc = check_blob(l, handle, handle_len, b, "dpwa_learner_attach_fds");
+    if (rc) return rc;
+    if (!b.vmm) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_fds: the peer shares a hipIpc handle (dpwa_learner_attach_ipc)");
+    DeviceGuard dg(l->device);
+    DevMem m;
+    if ((rc = devmem_import(m, fds, n_fds, chunk_bytes, 2 * (size_t)b.slot_stride, l->device))) return rc;
+    char *base = m.ptr;
+    set_remote(l, peer_id, b, base, std::move(m));
     return DPWA_OK;
 }
 
@@ -750,7 +977,8 @@ int dpwa_learner_relay_enable(dpwa_learner *l, int world, int rank)
     DeviceGuard dg(l->device);
     const int64_t payload16 = (int64_t)round_up(l->payload_bytes, 16);
     l->relay_stripe = (int64_t)round_up((size_t)((payload16 + world - 1) / world), 256);
-    HIP_TRY(hipMalloc(&l->relay_buf, (size_t)l->relay_stripe * world));
+    HIP_TRY(devmem_alloc(l->relay_mem, (size_t)l->relay_stripe * world, l->device));
+    l->relay_buf = l->relay_mem.ptr;
     HIP_TRY(hipEventCreateWithFlags(&l->ev_relay, hipEventDisableTiming));
     l->relay_world = world;
     l->relay_rank = rank;
@@ -767,39 +995,60 @@ int dpwa_learner_relay_handle(dpwa_learner *l, void *handle_out, int64_t handle_
     if (!l || !l->relay_on || !handle_out || handle_len < (int64_t)sizeof(IpcBlob))
         return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_handle: relay not enabled or short buffer");
     DeviceGuard dg(l->device);
-    IpcBlob b;
-    memset(&b, 0, sizeof(b));
-    HIP_TRY(hipIpcGetMemHandle(&b.handle, l->relay_buf));
-    b.magic = kIpcMagic;
-    b.slot_stride = l->relay_stripe;
-    b.n = l->n;
-    b.dtype = l->dtype;
-    b.device = l->device;
-    b.pid = (int32_t)getpid();
+    IpcBlob b = make_blob(l, l->relay_mem, l->relay_stripe);
+    if (!b.vmm) HIP_TRY(hipIpcGetMemHandle(&b.handle, l->relay_buf));
     memset(handle_out, 0, (size_t)handle_len);
     memcpy(handle_out, &b, sizeof(b));
     l->exported = true;
     return DPWA_OK;
 }
 
-int dpwa_learner_relay_attach(dpwa_learner *l, int rank, int peer_id, const void *relay_handle, int64_t handle_len)
+static int relay_check(dpwa_learner *l, int rank, int peer_id, const void *relay_handle, int64_t handle_len,
+                       IpcBlob &b, Endpoint *&slots_ep, const char *fn)
 {
     if (!l || !l->relay_on || rank < 0 || rank >= l->relay_world || rank == l->relay_rank || !relay_handle ||
         handle_len < (int64_t)sizeof(IpcBlob))
-        return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_attach: bad arguments");
+        return set_error(DPWA_ERR_ARG, "%s: bad arguments", fn);
     auto it = l->peers.find(peer_id);
     if (it == l->peers.end() || it->second.kind != 2)
-        return set_error(DPWA_ERR_STATE, "dpwa_learner_relay_attach: peer %d's slots are not IPC-attached", peer_id);
-    IpcBlob b;
+        return set_error(DPWA_ERR_STATE, "%s: peer %d's slots are not IPC-attached", fn, peer_id);
     memcpy(&b, relay_handle, sizeof(b));
     if (b.magic != kIpcMagic || b.slot_stride != l->relay_stripe || b.n != l->n || b.dtype != l->dtype)
-        return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_attach: relay buffer of rank %d does not match", rank);
+        return set_error(DPWA_ERR_ARG, "%s: relay buffer of rank %d does not match", fn, rank);
+    slots_ep = &it->second;
+    return DPWA_OK;
+}
+
+int dpwa_learner_relay_attach(dpwa_learner *l, int rank, int peer_id, const void *relay_handle, int64_t handle_len)
+{
+    IpcBlob b;
+    Endpoint *ep = nullptr;
+    int rc = relay_check(l, rank, peer_id, relay_handle, handle_len, b, ep, "dpwa_learner_relay_attach");
+    if (rc) return rc;
+    if (b.vmm) return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_attach: rank %d shares its relay buffer as fds", rank);
     DeviceGuard dg(l->device);
     void *ptr = nullptr;
     HIP_TRY(hipIpcOpenMemHandle(&ptr, b.handle, hipIpcMemLazyEnablePeerAccess));
     l->relay_opened.push_back((char *)ptr);
-    l->relay_slots[rank] = it->second.base;
+    l->relay_slots[rank] = ep->base;
     l->relay_bufs[rank] = (const char *)ptr;
+    return DPWA_OK;
+}
+
+int dpwa_learner_relay_attach_fds(dpwa_learner *l, int rank, int peer_id, const void *relay_handle,
+                                  int64_t handle_len, const int *fds, int n_fds, int64_t chunk_bytes)
+{
+    IpcBlob b;
+    Endpoint *ep = nullptr;
+    int rc = relay_check(l, rank, peer_id, relay_handle, handle_len, b, ep, "dpwa_learner_relay_attach_fds");
+    if (rc) return rc;
+    if (!b.vmm || !fds) return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_attach_fds: rank %d shares a hipIpc handle", rank);
+    DeviceGuard dg(l->device);
+    DevMem m;
+    if ((rc = devmem_import(m, fds, n_fds, chunk_bytes, (size_t)l->relay_stripe * l->relay_world, l->device))) return rc;
+    l->relay_slots[rank] = ep->base;
+    l->relay_bufs[rank] = m.ptr;
+    l->relay_imported.push_back(std::move(m));
     return DPWA_OK;
 }
 

@@ -12,8 +12,10 @@ fetch is a device-to-device pull; a group only wires the native nodes' peer tabl
                 update_wait, after every learner of the round has published (lock-step
                 order); a same-device peer's slot is read in place (no copy).
 ``DistGroup``   one node per torch.distributed rank, rank == node index in the YAML, one
-                GPU per rank.  Snapshot slots are exported with hipIpcGetMemHandle and
-                mapped by every peer at the first publish; each round is lock-step: a
+                GPU per rank.  Snapshot slots are exported (a hipIpcGetMemHandle, or for
+                allocations of 1.5 GiB and more one fd per 1 GiB chunk handed over a Unix
+                socket: hipIpcOpenMemHandle does not return above ~2 GiB on this ROCm stack)
+                and mapped by every peer at the first publish; each round is lock-step: a
                 stream-ordered barrier after the publish, then each fetch is pulled over
                 xGMI on the learner's side stream while the training step runs.
 ``AsyncDistGroup`` the same ranks and pulls in free-running rounds through the gossip board,
@@ -21,6 +23,7 @@ fetch is a device-to-device pull; a group only wires the native nodes' peer tabl
 """
 import ctypes
 import os
+import socket
 import threading
 import weakref
 
@@ -104,6 +107,53 @@ class LocalGroup:
                 _lib.call("dpwa_node_start_fetch", m._node, m._flags, m._raw_stream(m._learner.device.index))
 
 
+class _FdServer:
+    """Hands this rank's exported chunk fds (SCM_RIGHTS over an abstract Unix socket on this
+    host) to each of `expected` peers, then closes them."""
+    TIMEOUT_S = 600
+
+    def __init__(self, fds, expected):
+        self.fds, self.error = list(fds), None
+        self.sock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        self.address = "\0dpwa-fds-%d-%s" % (os.getpid(), os.urandom(8).hex())
+        self.sock.bind(self.address)
+        self.sock.listen(max(1, expected))
+        self.sock.settimeout(self.TIMEOUT_S)
+        self.thread = threading.Thread(target=self._serve, args=(expected,), daemon=True)
+        self.thread.start()
+
+    def _serve(self, expected):
+        try:
+            for _ in range(expected):
+                c, _ = self.sock.accept()
+                with c:
+                    socket.send_fds(c, [b"dpwa"], self.fds)
+        except Exception as e:      # reported by finish()
+            self.error = e
+
+    def finish(self):
+        self.thread.join(self.TIMEOUT_S)
+        self.sock.close()
+        for fd in self.fds:
+            os.close(fd)
+        self.fds = []
+        if self.thread.is_alive() or self.error is not None:
+            raise RuntimeError("handing the snapshot allocation's fds to the peers failed: %r" % (self.error,))
+
+
+def _fetch_fds(address, n):
+    """The `n` fds a peer's _FdServer at `address` hands out."""
+    with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as s:
+        s.settimeout(_FdServer.TIMEOUT_S)
+        s.connect(address)
+        _, fds, _, _ = socket.recv_fds(s, 16, n)
+    if len(fds) != n:
+        for fd in fds:
+            os.close(fd)
+        raise RuntimeError("expected %d fds from the peer, got %d" % (n, len(fds)))
+    return fds
+
+
 class DistGroup:
     """One learner per rank; see the module docstring."""
     eager_fetch = True
@@ -148,15 +198,38 @@ class DistGroup:
             buf = ctypes.create_string_buffer(_lib.IPC_HANDLE_BYTES)
             _lib.call("dpwa_learner_relay_handle", learner._h, buf, _lib.IPC_HANDLE_BYTES)
             relay = buf.raw
-        handles = [None] * self.world
-        self.dist.all_gather_object(handles, (handle, relay), group=self.pg)
-        for k in range(len(conn.peers)):
-            r = conn.peer_rank(k)
-            learner.attach_ipc(k, handles[r][0])
-            if self.relay_blocks:
-                blob = ctypes.create_string_buffer(bytes(handles[r][1]), _lib.IPC_HANDLE_BYTES)
-                _lib.call("dpwa_learner_relay_attach", learner._h, r, k, blob, _lib.IPC_HANDLE_BYTES)
-            conn._set_peer(k, _lib.NODE_PEER_REMOTE, None)
+        slot_fds, slot_chunk = learner.export_fds(0)
+        relay_fds, relay_chunk = learner.export_fds(1) if self.relay_blocks else ([], 0)
+        server = _FdServer(slot_fds + relay_fds, self.world - 1) if (slot_fds or relay_fds) else None
+        mine = (handle, relay, server.address if server else None, len(slot_fds), slot_chunk, len(relay_fds),
+                relay_chunk)
+        infos = [None] * self.world
+        try:
+            self.dist.all_gather_object(infos, mine, group=self.pg)
+            for k in range(len(conn.peers)):
+                r = conn.peer_rank(k)
+                h, rh, address, ns, cs, nr, cr = infos[r]
+                fds = _fetch_fds(address, ns + nr) if address else []
+                try:
+                    if ns:
+                        learner.attach_fds(k, h, fds[:ns], cs)
+                    else:
+                        learner.attach_ipc(k, h)
+                    if self.relay_blocks:
+                        blob = ctypes.create_string_buffer(bytes(rh), _lib.IPC_HANDLE_BYTES)
+                        if nr:
+                            arr = (ctypes.c_int * nr)(*fds[ns:])
+                            _lib.call("dpwa_learner_relay_attach_fds", learner._h, r, k, blob, _lib.IPC_HANDLE_BYTES,
+                                      arr, nr, cr)
+                        else:
+                            _lib.call("dpwa_learner_relay_attach", learner._h, r, k, blob, _lib.IPC_HANDLE_BYTES)
+                finally:
+                    for fd in fds:
+                        os.close(fd)
+                conn._set_peer(k, _lib.NODE_PEER_REMOTE, None)
+        finally:
+            if server is not None:
+                server.finish()
         if self.relay_blocks:
             dev = learner.device
             self._pick = torch.full((1,), -1, dtype=torch.int32, device=dev)

@@ -14,6 +14,7 @@ from . import _lib
 DTYPES = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}
 
 _c_void_p = ctypes.c_void_p
+MAX_FDS = 240          # chunks (1 GiB each) one exported allocation may have; < SCM_MAX_FD (253)
 
 
 def loss_args(loss, device):
@@ -136,6 +137,21 @@ class Learner:
     def attach_ipc(self, peer_id, handle):
         buf = ctypes.create_string_buffer(bytes(handle), _lib.IPC_HANDLE_BYTES)
         _lib.call("dpwa_learner_attach_ipc", self._h, peer_id, buf, _lib.IPC_HANDLE_BYTES)
+
+    def export_fds(self, which=0):
+        """(fds, chunk bytes) sharing this learner's snapshot slots (which=0) or relay buffer
+        (which=1) when that allocation is VMM-backed (>= 1.5 GiB, or DPWA_VMM=1); ([], 0)
+        for an ordinary allocation, shared by ipc_handle's hipIpc handle.  The caller closes
+        the fds once the peers hold theirs."""
+        arr = (ctypes.c_int * MAX_FDS)()
+        n, chunk = ctypes.c_int(), ctypes.c_int64()
+        _lib.call("dpwa_learner_export_fds", self._h, which, arr, MAX_FDS, ctypes.byref(n), ctypes.byref(chunk))
+        return list(arr[:n.value]), chunk.value
+
+    def attach_fds(self, peer_id, handle, fds, chunk):
+        buf = ctypes.create_string_buffer(bytes(handle), _lib.IPC_HANDLE_BYTES)
+        arr = (ctypes.c_int * max(1, len(fds)))(*fds)
+        _lib.call("dpwa_learner_attach_fds", self._h, peer_id, buf, _lib.IPC_HANDLE_BYTES, arr, len(fds), chunk)
 
     def fetch(self, peer_id, peer_version, zero_copy, stream):
         rc = self._f_fetch(self._h, peer_id, peer_version, 1 if zero_copy else 0, stream.cuda_stream)

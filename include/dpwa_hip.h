@@ -140,12 +140,22 @@ int dpwa_learner_version(const dpwa_learner *l, uint64_t *version);
 
 /* Peers.  `peer_id` is the caller's index of that peer (e.g. its node index).
  * attach_local: the peer learner lives in this process (any device).
- * ipc_handle / attach_ipc: the peer lives in another process; its snapshot allocation is
- * exported with hipIpcGetMemHandle (handle_len = DPWA_IPC_HANDLE_BYTES). */
+ * ipc_handle / attach_ipc: the peer lives in another process; ipc_handle describes the
+ * snapshot allocation (handle_len = DPWA_IPC_HANDLE_BYTES) and, for an ordinary allocation,
+ * carries its hipIpcGetMemHandle.  Allocations of 1.5 GiB and more (or any size with
+ * DPWA_VMM=1) are hipMemCreate chunks instead -- hipIpcOpenMemHandle does not return for
+ * allocations above ~2 GiB on this ROCm stack -- and are shared as POSIX fds:
+ * export_fds (which = 0: snapshot slots, 1: relay buffer) yields one fd per chunk, *n_fds = 0
+ * for an ordinary allocation; the caller passes them to the peer process (e.g. SCM_RIGHTS over
+ * a Unix socket) and closes its copies; the peer maps them with attach_fds (the fds stay the
+ * caller's). */
 #define DPWA_IPC_HANDLE_BYTES 128
 int dpwa_learner_attach_local(dpwa_learner *l, int peer_id, dpwa_learner *peer);
 int dpwa_learner_ipc_handle(dpwa_learner *l, void *handle_out, int64_t handle_len);
 int dpwa_learner_attach_ipc(dpwa_learner *l, int peer_id, const void *handle, int64_t handle_len);
+int dpwa_learner_export_fds(dpwa_learner *l, int which, int *fds, int max_fds, int *n_fds, int64_t *chunk_bytes);
+int dpwa_learner_attach_fds(dpwa_learner *l, int peer_id, const void *handle, int64_t handle_len, const int *fds,
+                            int n_fds, int64_t chunk_bytes);
 
 /* The fetch (TxThread request -> reply, conn.py:297-298): pull peer `peer_id`'s snapshot of
  * publish number `peer_version` (1-based) into this learner's staging buffer on the
@@ -190,7 +200,7 @@ int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *pay
 /* Relay transport: a lock-step round's pulls spread over every xGMI link.  Each snapshot is
  * cut into `world` stripes; phase 1 (after the caller's collective that shares every rank's
  * pick, so that all publishes of the round are complete) pulls stripe `rank` of every
- * snapshot another rank needs into this rank's relay buffer; phase 2 (after a second
+ * snapshot some rank needs into this rank's relay buffer; phase 2 (after a second
  * barrier) gathers this rank's peer's stripes from all ranks into staging and makes it the
  * fetch in flight (my_pick = rank averaged with, -1 none).  Both phases run on the learner's
  * side stream; picks_dev holds `world` int32 on this learner's device.
@@ -200,6 +210,8 @@ int dpwa_learner_relay_enable(dpwa_learner *l, int world, int rank);
 int dpwa_learner_relay_handle(dpwa_learner *l, void *handle_out, int64_t handle_len);
 int dpwa_learner_relay_attach(dpwa_learner *l, int rank, int peer_id, const void *relay_handle,
                               int64_t handle_len);
+int dpwa_learner_relay_attach_fds(dpwa_learner *l, int rank, int peer_id, const void *relay_handle,
+                                  int64_t handle_len, const int *fds, int n_fds, int64_t chunk_bytes);
 int dpwa_learner_relay_wait(dpwa_learner *l, dpwa_stream_t stream);
 int dpwa_learner_relay_phase1(dpwa_learner *l, const int32_t *picks_dev, uint64_t version, int blocks,
                               dpwa_stream_t stream);

@@ -113,3 +113,9 @@ def test_async_write_through_snapshots(tmp_path, world, pull, interp):
         assert not bad, (g, bad[:5])
         prefix, k = empty_rounds_form_a_prefix(runs[g])
         assert prefix and k < T
+
+
+def test_async_write_through_vmm_shared_slots(tmp_path, monkeypatch):
+    """The free-running board over fd-shared (hipMemCreate) snapshot slots, DPWA_VMM=1."""
+    monkeypatch.setenv("DPWA_VMM", "1")
+    test_async_write_through_snapshots(tmp_path, 3, "copy", "clock")

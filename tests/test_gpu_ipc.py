@@ -173,3 +173,13 @@ def test_ipc_gossip_with_injected_faults(tmp_path, pull):
             assert olerp.bits_equal(got["params"][r], params[g]), (g, r)
             want_scores = [-1 if s is None else s for s in learners[g].scores([x for x in names if x != names[g]])]
             assert list(got["scores"][r]) == want_scores, (g, r)
+
+
+@pytest.mark.parametrize("world,interp,fp,thr,pull", [(2, "clock", 1.0, 0.0, "copy"), (3, "loss", 0.7, 0.5, "kernel:64"),
+                                                       (3, "clock", 0.8, 0.0, "relay:8")])
+def test_ipc_gossip_vmm_shared_slots(tmp_path, monkeypatch, world, interp, fp, thr, pull):
+    """DPWA_VMM=1: the snapshot slots (and relay buffers) are hipMemCreate chunks shared as fds
+    over a Unix socket -- the form every allocation of 1.5 GiB and more takes, since
+    hipIpcOpenMemHandle does not return above ~2 GiB -- at a small size, against the oracle."""
+    monkeypatch.setenv("DPWA_VMM", "1")
+    test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100_003)
