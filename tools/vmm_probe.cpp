@@ -41,6 +41,9 @@ int main(int argc, char **argv)
 {
     const double gib = argc > 1 ? std::atof(argv[1]) : 6.0;
     const double chunk_gib = argc > 2 ? std::atof(argv[2]) : 1.0;
+    const bool by_ptr = argc > 3 && std::strcmp(argv[3], "ptr") == 0;
+    int rt = 0;
+    (void)hipRuntimeGetVersion;   // printed by the exporter below
     int sv[2];
     if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) return 3;
     const pid_t child = fork();
@@ -73,7 +76,9 @@ int main(int argc, char **argv)
             CK(hipMemsetD32((hipDeviceptr_t)((char *)base + (size_t)i * chunk), 0x11111111u * (unsigned)(i + 1),
                             chunk / 4));
         CK(hipDeviceSynchronize());
-        std::printf("[exporter] %d chunks of %zu bytes (granularity %zu), total %zu\n", k, chunk, gran, total);
+        CK(hipRuntimeGetVersion(&rt));
+        std::printf("[exporter] HIP runtime %d; %d chunks of %zu bytes (granularity %zu), total %zu\n", rt, k, chunk,
+                    gran, total);
         std::fflush(stdout);
         long msg[3] = {(long)getpid(), (long)k, (long)chunk};
         for (int i = 0; i < k; ++i) {   // one message per chunk: the header words + its fd
@@ -130,7 +135,9 @@ int main(int argc, char **argv)
     std::vector<hipMemGenericAllocationHandle_t> h((size_t)k);
     for (int i = 0; i < k; ++i) {
         const int fd = rfds[i];
-        CK(hipMemImportFromShareableHandle(&h[i], (void *)(intptr_t)fd, hipMemHandleTypePosixFileDescriptor));
+        int fd_copy = fd;   // "ptr" mode: pass the fd's address (older runtimes read *osHandle)
+        CK(hipMemImportFromShareableHandle(&h[i], by_ptr ? (void *)&fd_copy : (void *)(intptr_t)fd,
+                                           hipMemHandleTypePosixFileDescriptor));
         CK(hipMemMap((char *)base + (size_t)i * chunk, chunk, 0, h[i], 0));
         close(fd);
         std::printf("[importer] chunk %d mapped\n", i);
