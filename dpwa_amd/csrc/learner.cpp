@@ -217,10 +217,21 @@ int devmem_import(DevMem &m, const int *fds, int n_fds, int64_t chunk, size_t ne
     if (n_fds < 1 || chunk <= 0 || (size_t)chunk * (size_t)n_fds < need_bytes)
         return set_error(DPWA_ERR_ARG, "import: %d chunks of %lld bytes for %zu bytes", n_fds, (long long)chunk,
                          need_bytes);
+    // How the fd is handed over depends on the runtime in the process (a torch process runs the
+    // HIP runtime torch bundles): 7.0 reads the fd through the pointer (and faults on an fd
+    // passed as the pointer value), 7.2 takes the fd as the pointer value (and rejects an
+    // address as an invalid fd) -- tools/vmm_torch_probe.py, tools/vmm_probe.cpp.
+    int rt = 0;
+    (void)hipRuntimeGetVersion(&rt);
+    const bool fd_by_value = rt >= 70200000;
     std::vector<hipMemGenericAllocationHandle_t> h;
     for (int i = 0; i < n_fds; ++i) {
         hipMemGenericAllocationHandle_t x;
-        hipError_t e = hipMemImportFromShareableHandle(&x, (void *)(intptr_t)fds[i], hipMemHandleTypePosixFileDescriptor);
+        int fd = fds[i];
+        hipError_t e = hipMemImportFromShareableHandle(&x, fd_by_value ? (void *)(intptr_t)fd : (void *)&fd,
+                                                       hipMemHandleTypePosixFileDescriptor);
+        if (e == hipErrorInvalidValue && fd_by_value)   // a runtime of the older convention
+            e = hipMemImportFromShareableHandle(&x, (void *)&fd, hipMemHandleTypePosixFileDescriptor);
         if (e != hipSuccess) {
             for (auto y : h) (void)hipMemRelease(y);
             return set_error(DPWA_ERR_HIP, "hipMemImportFromShareableHandle: %s", hipGetErrorString(e));
