@@ -850,7 +850,8 @@ def main():
                 "numel": args.numel,
                 "publish": variant,
                 "transport": "in-place HBM read (co-resident peer)" if world == 1 else
-                             "hipIpc-mapped slot pulled over xGMI on a side stream (%s, %s rounds)"
+                             "peer slot mapped into this process (hipIpc handle, or fds of hipMemCreate chunks from "
+                             "1.5 GiB up) pulled over xGMI on a side stream (%s, %s rounds)"
                              % (sel_mode, "free-running" if sel_async else "lock-step"),
                 "parallelism": "gossip x%d" % int(rounds / args.steps),
                 "streams": args.streams,
