@@ -10,8 +10,9 @@ vector (ResNet-18 size) per learner, N(0,1) data, constant interpolation 0.5,
 fetch_probability 1.
   * ``--gpus 1``: two learners co-resident on cuda:0 (the minimal non-degenerate gossip:
     each averages with the other's snapshot, read in place from HBM).
-  * ``--gpus N`` (torchrun): one learner per GPU; peers' snapshots are mapped with
-    hipIpcOpenMemHandle and pulled over xGMI on each learner's side stream.  Short trials of
+  * ``--gpus N`` (torchrun): one learner per GPU; peers' snapshot slots are mapped into each
+    process (hipIpc handles; fds of hipMemCreate chunks from 1.5 GiB up) and pulled over xGMI
+    on each learner's side stream.  Short trials of
     lock-step rounds (RCCL barrier; copy / kernel / relay pulls) and free-running rounds
     (gossip board) pick the transport of the timed run.  Per-GPU work is fixed -> "scaling":
     "weak".  Every rank logs its phases to stderr (``[bench rN +s]``), so a multi-GPU run that
