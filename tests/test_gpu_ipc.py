@@ -3,7 +3,6 @@ share the one GPU, map each other's snapshot slots with hipIpcOpenMemHandle and 
 on their side streams, lock-step, checked against the oracle simulation.  (RCCL refuses
 two ranks on one device, so the barrier runs over gloo here; the data path -- IPC-mapped
 slots, side-stream pulls, device factor, fused lerp -- is the production one.)"""
-import functools
 import socket
 
 import numpy as np
