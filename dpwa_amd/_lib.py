@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("DPWA_HIP_LIB", os.path.join(_HERE, "libdpwa_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dpwa_hip.h")
 
 # Constants mirrored from include/dpwa_hip.h
-ABI_VERSION = 1
+ABI_VERSION = 2
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_NOMEM = 0, -1, -2, -3, -4
 F32, BF16, F64 = 0, 1, 2
 INTERP_CONSTANT, INTERP_CLOCK, INTERP_LOSS = 0, 1, 2

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DPWA_ABI_VERSION 1
+#define DPWA_ABI_VERSION 2
 
 #define DPWA_OK 0
 #define DPWA_ERR_ARG (-1)     /* bad argument (API misuse)                          */
