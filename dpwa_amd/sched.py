@@ -10,6 +10,12 @@ import ctypes
 
 from . import _lib
 
+# conn.py:178-181 (the native scheduler's bounds, dpwa_amd/csrc/sched.cpp)
+FLOW_CONTROL_MIN_SCORE = 10
+FLOW_CONTROL_MAX_SCORE = 1000
+FLOW_CONTROL_INC_SCORE = 10
+FLOW_CONTROL_DEC_SCORE = 100
+
 OUTCOMES = {
     "connect_ok": _lib.CONNECT_OK, "refused": _lib.CONNECT_REFUSED, "connect_error": _lib.CONNECT_ERROR,
     "payload": _lib.REPLY_PAYLOAD, "empty": _lib.REPLY_EMPTY, "timeout": _lib.REPLY_TIMEOUT,
@@ -32,7 +38,7 @@ class Scheduler:
         self._owned = handle is None
         self._h = ctypes.c_void_p() if handle is None else ctypes.c_void_p(handle)
         if handle is not None:
-            pass
+            pass                  # the node's scheduler, borrowed (dpwa_node_handles)
         elif seed is None:
             _lib.call("dpwa_sched_create", ctypes.byref(self._h), n_peers, None, -1, float(fetch_probability))
         else:

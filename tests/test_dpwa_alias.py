@@ -37,3 +37,26 @@ def test_messaging_names_frame_like_the_reference():
         d = rec["decoded"]
         assert got[0] == d["type"] and got[1] == d["message"]
         assert (got[2].hex() if got[2] is not None else None) == d["payload_hex"]
+
+
+def test_conn_constants_and_scheduler_bounds():
+    """dpwa.conn's constants (conn.py:34, 40, 178-181), and the native scheduler honours the
+    flow-control ones: a refused peer drops by DEC to no lower than MIN, a reply lifts it by
+    INC up to MAX."""
+    from dpwa.conn import (FLOW_CONTROL_DEC_SCORE, FLOW_CONTROL_INC_SCORE, FLOW_CONTROL_MAX_SCORE,
+                           FLOW_CONTROL_MIN_SCORE, MESSAGE_TYPE_FETCH_PARAMETERS, TCP_SOCKET_BUFFER_SIZE)
+    from dpwa_amd.sched import Scheduler
+    assert (MESSAGE_TYPE_FETCH_PARAMETERS, TCP_SOCKET_BUFFER_SIZE) == (1, 8 * 1024 * 1024)
+    s = Scheduler(1, seed=3)
+    assert s.score(0) == FLOW_CONTROL_MAX_SCORE
+    want = FLOW_CONTROL_MAX_SCORE
+    for _ in range(12):
+        peer, connected = s.pick()
+        assert peer == 0 and not connected
+        s.report(0, "refused")
+        want = max(want - FLOW_CONTROL_DEC_SCORE, FLOW_CONTROL_MIN_SCORE)
+        assert s.score(0) == want
+    peer, connected = s.pick()
+    s.report(0, "connect_ok")
+    s.report(0, "payload")
+    assert s.score(0) == min(want + FLOW_CONTROL_INC_SCORE, FLOW_CONTROL_MAX_SCORE)
