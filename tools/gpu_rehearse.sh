@@ -16,6 +16,12 @@ GPU_MAX_HW_QUEUES=2 timeout -k 10 300 python -m torch.distributed.run --nnodes=1
     --master-port 29506 bench.py --gpus 6 --dist-backend gloo --steps 40 --warmup 5 --compute-us 300 \
     > gpurun_out/rehearse_n6.json 2> gpurun_out/rehearse_n6.err || { echo "rehearsal n=6 failed"; tail -20 gpurun_out/rehearse_n6.err; exit 1; }
 cat gpurun_out/rehearse_n6.json
+# configs[3]'s size across two processes: 4 GB of slots per rank, shared as hipMemCreate fds
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29512 bench.py --gpus 2 --dist-backend gloo --numel 1000000000 --dtype bf16 --interpolation loss \
+    --divergence-threshold 0.5 --loss-schedule decay --steps 20 --warmup 3 --compute-us 0 \
+    > gpurun_out/rehearse_n2_1b.json 2> gpurun_out/rehearse_n2_1b.err || { echo "rehearsal 1B failed"; tail -20 gpurun_out/rehearse_n2_1b.err; exit 1; }
+tail -1 gpurun_out/rehearse_n2_1b.json
 V="--no-cpu-baseline --no-sweep --no-cold --compute-us 0 --steps 50 --warmup 10"
 timeout -k 10 200 python bench.py $V --numel 100000000 --interpolation clock > gpurun_out/bench_100m_clock.json 2> gpurun_out/variants.err || { echo "variant failed"; tail gpurun_out/variants.err; exit 1; }
 timeout -k 10 200 python bench.py $V --numel 1000000000 --dtype bf16 --interpolation loss --divergence-threshold 0.5 \
