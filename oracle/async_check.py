@@ -14,13 +14,18 @@ import hashlib
 
 import numpy as np
 
-from .lerp import lerp_f32
+from .lerp import bits_equal, f32_to_bf16, lerp_f32
 from .policy import factor_and_clock
 
 
 def async_base(rank, r, n):
     """The parameters rank `rank` publishes at its round r (publish number r + 1)."""
     return (np.arange(n, dtype=np.float32) * np.float32(1e-3) + np.float32(rank * 1000 + r)).astype(np.float32)
+
+
+def async_base_bf16(rank, r, n):
+    """async_base rounded to bf16 (raw bits), for the bf16 runs."""
+    return f32_to_bf16(async_base(rank, r, n))
 
 
 def async_loss(rank, r, wait=False):
@@ -43,11 +48,14 @@ class AsyncRuns:
     names          node names, index = rank
     Only ranks present in `peers` are known; a rank that left early is absent."""
 
-    def __init__(self, names, peers, versions, interp="constant", value=0.5, thr=0.0, published=None):
+    def __init__(self, names, peers, versions, interp="constant", value=0.5, thr=0.0, published=None,
+                 base=async_base, lerp=lerp_f32):
         """published(q, v, n): the parameters rank q published as version v (1-based).  Default:
-        async_base(q, v - 1, n), the runs whose every round publishes its known base.  Runs with
-        write-through snapshots publish what their last round averaged; pass those."""
-        self.published = published or (lambda q, v, n: async_base(q, v - 1, n))
+        base(q, v - 1, n), the runs whose every round publishes its known base.  Runs with
+        write-through snapshots publish what their last round averaged; pass those.  base and
+        lerp give the dtype: async_base / lerp_f32, or their bf16 forms (raw bits)."""
+        self.base, self.lerp = base, lerp
+        self.published = published or (lambda q, v, n: self.base(q, v - 1, n))
         self.names = list(names)
         self.peers = {g: [str(p) for p in v] for g, v in peers.items()}
         self.versions = {g: [int(x) for x in v] for g, v in versions.items()}
@@ -86,7 +94,7 @@ class AsyncRuns:
 
     def expected_params(self, g, r, n):
         """What rank g's parameters must be after round r."""
-        mine = async_base(g, r, n)
+        mine = self.base(g, r, n)
         got = self.read(g, r)
         if got is None:
             return mine
@@ -97,7 +105,7 @@ class AsyncRuns:
             if not (self.interp == "constant" and self.thr == 0.0):
                 raise ValueError("incomplete runs can only be checked under constant interpolation")
             factor = self.value
-        return lerp_f32(mine, self.published(q, v, n), factor)
+        return self.lerp(mine, self.published(q, v, n), factor)
 
     def check_rank(self, g, params, clocks, n):
         """Checks rank g's recorded params (T x n) and clocks (T) round by round; returns a list
@@ -114,7 +122,7 @@ class AsyncRuns:
                     bad.append("round %d: versions of %s went backwards" % (r, self.names[q]))
                 last[q] = v
             want = self.expected_params(g, r, n)
-            if not np.array_equal(np.asarray(params[r]).view(np.uint32), want.view(np.uint32)):
+            if not bits_equal(np.asarray(params[r]), want):
                 bad.append("round %d: parameters differ from the oracle (peer %s)" % (r, self.peers[g][r] or "-"))
             if self.complete() and float(clocks[r]) != self.clock_after(g, r):
                 bad.append("round %d: clock %r != %r" % (r, float(clocks[r]), self.clock_after(g, r)))
@@ -133,7 +141,7 @@ class AsyncRuns:
                 if got is None or got[0] != q:
                     continue
                 factor = self.policy(g, r)[0] if self.complete() else self.value
-                out[(g, r)] = digest(lerp_f32(async_base(g, r, n), published_by_q(got[1]), factor))
+                out[(g, r)] = digest(self.lerp(self.base(g, r, n), published_by_q(got[1]), factor))
         return out
 
     def check_rank_digests(self, g, params, clocks, n, expected):
@@ -144,7 +152,7 @@ class AsyncRuns:
         for r in range(len(self.peers[g])):
             got = self.read(g, r)
             if got is None:
-                if digest(params[r]) != digest(async_base(g, r, n)):
+                if digest(params[r]) != digest(self.base(g, r, n)):
                     bad.append("round %d: parameters changed without an average" % r)
             else:
                 q, v = got

@@ -140,7 +140,7 @@ def fault_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy"):
     dist.destroy_process_group()
 
 
-from oracle.async_check import async_base, async_loss  # noqa: E402  (checker's published values)
+from oracle.async_check import async_base, async_base_bf16, async_loss  # noqa: E402  (checker's published values)
 
 
 def async_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy", die_rank=-1, die_round=-1):
@@ -194,7 +194,7 @@ def async_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy", die_ra
     os._exit(0)                    # skip the process-group teardown (the dead rank never joins it)
 
 
-def async_wt_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy"):
+def async_wt_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy", dtype="f32"):
     """Free-running rounds with write-through snapshots: update_send publishes the parameters
     the last average left (the averaging kernel wrote that snapshot), the "training step" then
     sets the parameters to async_base(rank, r), and the average writes the next snapshot.
@@ -211,9 +211,10 @@ def async_wt_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy"):
     names = ["r%d" % i for i in range(world)]
     conn = DpwaConnection(names[rank], cfg_path, seed=800 + rank, pull=pull)      # the default group
     rng = np.random.default_rng(rank + 10)
-    flat = torch.from_numpy(async_base(rank, -1, n)).to(dev)
-    bases = [torch.from_numpy(async_base(rank, r, n)).to(dev) for r in range(T)]
-    params, clocks, peers, versions = np.zeros((T, n), np.float32), np.zeros(T), [], []
+    base = async_base if dtype == "f32" else async_base_bf16
+    flat = to_device(base(rank, -1, n), dev)
+    bases = [to_device(base(rank, r, n), dev) for r in range(T)]
+    params, clocks, peers, versions = np.zeros((T, n), base(rank, 0, 1).dtype), np.zeros(T), [], []
     for r in range(T):
         conn.update_send(flat, async_loss(rank, r), reuse_snapshot=True)
         flat.copy_(bases[r])
@@ -221,7 +222,7 @@ def async_wt_worker(rank, world, port, cfg_path, out_dir, n, T, pull="copy"):
         payload, _ = conn.update_wait_average(flat, async_loss(rank, r, wait=True), write_through=True)
         peers.append(payload.peer if payload is not None else "")
         versions.append(conn._info()[2] if payload is not None else 0)
-        params[r] = flat.cpu().numpy()
+        params[r] = to_host(flat)
         clocks[r] = conn.clock
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=params, clocks=clocks, peers=np.array(peers),

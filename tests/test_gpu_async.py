@@ -115,6 +115,31 @@ def test_async_write_through_snapshots(tmp_path, world, pull, interp):
         assert prefix and k < T
 
 
+def test_async_write_through_bf16(tmp_path):
+    """bf16 (BASELINE configs[3-4]'s dtype) through the free-running board with write-through
+    snapshots: every average against the oracle's torch-eager bf16 lerp of the exact snapshot
+    version read, clocks exact."""
+    from oracle.async_check import async_base_bf16
+    from oracle.lerp import lerp_bf16
+    world, n, T, interp = 3, 300_007, 24, "clock"
+    names = ["r%d" % i for i in range(world)]
+    cfg = str(tmp_path / "async_bf16.yaml")
+    dist_worker.write_cfg(cfg, names, 1.0, interp, 0.0)
+    mp.spawn(dist_worker.async_wt_worker, args=(world, free_port(), cfg, str(tmp_path), n, T, "kernel:64", "bf16"),
+             nprocs=world, join=True)
+    runs = {g: np.load(tmp_path / ("rank%d.npz" % g)) for g in range(world)}
+
+    def published(q, v, n_):
+        return async_base_bf16(q, -1, n_) if v == 1 else runs[q]["params"][v - 2]
+
+    check = AsyncRuns(names, {g: runs[g]["peers"] for g in range(world)},
+                      {g: runs[g]["versions"] for g in range(world)}, interp, 0.5, 0.0, published=published,
+                      base=async_base_bf16, lerp=lerp_bf16)
+    for g in range(world):
+        bad = check.check_rank(g, runs[g]["params"], runs[g]["clocks"], n)
+        assert not bad, (g, bad[:5])
+
+
 def test_async_write_through_vmm_shared_slots(tmp_path, monkeypatch):
     """The free-running board over fd-shared (hipMemCreate) snapshot slots, DPWA_VMM=1."""
     monkeypatch.setenv("DPWA_VMM", "1")
