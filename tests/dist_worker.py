@@ -335,3 +335,70 @@ def big_worker(rank, world, port, cfg_path, out_dir, n, T, pull, dtype):
     dist.barrier()
     conn.close()
     dist.destroy_process_group()
+
+
+def resnet_worker(rank, world, port, cfg_path, out_dir, T, group):
+    """The reference's training loop (examples/pytorch-cifar/main.py:122-158) on one rank:
+    CIFAR ResNet-18, synthetic batches, SGD, the adapter's parameters gossiped every step over
+    the multi-process group.  update_wait goes through the connection seam (payload, factor),
+    so the fetched snapshot can be recorded before the reference's lerp is applied.  Records
+    per round the sha1 of the snapshot it published and of the one it fetched, the peer, the
+    clock, the losses, and whether the average equals oracle.lerp(before, fetched, factor)."""
+    import hashlib
+    import torch
+    import torch.distributed as dist
+    import torch.nn.functional as F
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    sys.path.insert(0, os.path.join(ROOT, "examples"))
+    from resnet18_gossip import resnet18
+
+    from dpwa_amd import DpwaPyTorchAdapter
+    from oracle.lerp import bits_equal, lerp_f32
+    names = ["w%d" % (i + 1) for i in range(world)]
+    torch.manual_seed(rank)
+    net = resnet18().to(dev)
+    adapter = DpwaPyTorchAdapter(net, names[rank], cfg_path, seed=100 + rank, group=group)
+    conn, flat = adapter.connection, adapter.flat.buffer
+    opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
+    gen = torch.Generator(device=dev).manual_seed(5 + rank)
+
+    def sha(t):
+        return hashlib.sha1(t.cpu().numpy().tobytes()).hexdigest()
+    rec = {k: [] for k in ("published", "fetched", "peers", "clocks", "send", "wait", "ok")}
+    send = 2.3
+    for r in range(T):
+        adapter.update_send(send)
+        rec["published"].append(sha(flat))
+        x = torch.randn(8, 3, 32, 32, device=dev, generator=gen)
+        y = torch.randint(0, 10, (8,), device=dev, generator=gen)
+        opt.zero_grad(set_to_none=True)
+        loss = F.cross_entropy(net(x), y)
+        loss.backward()
+        opt.step()
+        wait = float(loss)
+        before = flat.cpu().numpy()
+        payload, factor = conn.update_wait(wait)
+        if payload is None:
+            rec["fetched"].append("")
+            rec["peers"].append("")
+            rec["ok"].append(bits_equal(flat.cpu().numpy(), before))
+        else:
+            snap = payload.tensor()
+            rec["fetched"].append(sha(snap))
+            rec["peers"].append(payload.peer)
+            f = float(factor)
+            conn.average(flat)
+            rec["ok"].append(bits_equal(flat.cpu().numpy(), lerp_f32(before, snap.cpu().numpy(), f)))
+        rec["clocks"].append(conn.clock)
+        rec["send"].append(send)
+        rec["wait"].append(wait)
+        send = wait
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), **{k: np.array(v) for k, v in rec.items()})
+    torch.cuda.synchronize()
+    dist.barrier()
+    conn.close()
+    dist.destroy_process_group()

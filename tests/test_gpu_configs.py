@@ -230,3 +230,43 @@ def test_resnet18_example_runs(capsys):
     out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert out["learners"] == 2 and out["final_clock"] == 6.0
     assert out["train_steps_per_s_per_learner_gossip"] > 0
+
+
+@pytest.mark.parametrize("group", ["lockstep", "async"])
+def test_configs0_resnet18_training_across_processes(tmp_path, group):
+    """configs[0]'s trainer (ResNet-18, constant 0.5, threshold 0.5) with one learner per
+    process through the multi-process groups (IPC-mapped slots; two ranks share the one GPU):
+    every fetched snapshot is byte-identical to what its peer published that round, every
+    average is oracle.lerp(before, fetched, factor), and -- lock-step -- peers and clocks
+    follow the oracle replay of the recorded losses."""
+    import torch.multiprocessing as mp
+
+    from tests import dist_worker
+    from tests.test_gpu_ipc import free_port
+    G, T = 2, 5
+    names = ["w%d" % (g + 1) for g in range(G)]
+    cfg = tmp_path / "c0mp.yaml"
+    write_cfg(cfg, names, 1, "constant", 0.5, 0.5)
+    mp.spawn(dist_worker.resnet_worker, args=(G, free_port(), str(cfg), str(tmp_path), T, group), nprocs=G,
+             join=True)
+    runs = [np.load(tmp_path / ("rank%d.npz" % g)) for g in range(G)]
+    for g in range(G):
+        assert all(runs[g]["ok"]), (g, list(runs[g]["ok"]))
+        for r in range(T):
+            peer = str(runs[g]["peers"][r])
+            if peer:
+                q = names.index(peer)
+                # free-running: whichever of the peer's publishes the board handed out
+                allowed = {str(runs[q]["published"][r])} if group == "lockstep" else \
+                    {str(h) for h in runs[q]["published"]}
+                assert str(runs[g]["fetched"][r]) in allowed, (g, r)
+    if group == "lockstep":
+        L = [OracleLearner(names[g], [x for x in names if x != names[g]], 1, "constant", 0.5, 0.5, 100 + g)
+             for g in range(G)]
+        for r in range(T):
+            exp = oracle_round(L, [runs[g]["send"][r] for g in range(G)], [runs[g]["wait"][r] for g in range(G)],
+                               names)
+            for g in range(G):
+                q, _ = exp[g]
+                assert str(runs[g]["peers"][r]) == (names[q] if q is not None else ""), (r, g)
+                assert runs[g]["clocks"][r] == L[g].clock, (r, g)
