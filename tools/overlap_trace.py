@@ -10,8 +10,9 @@ LocalGroup(prefetch=True, zero_copy=False): once both have published the round, 
 stream, then the forward/backward/SGD steps are enqueued on the compute stream and
 update_wait averages.  This is the schedule of learners on different GPUs of one process
 (peer-to-peer pulls over xGMI) and of one rank per GPU (`--procs 2`: the production
-DistGroup, which on one GPU must use a gloo barrier that synchronises the host every round,
-so there the pull finishes before the host has enqueued the step).  Run it under
+free-running group by default -- no barrier, the pull starts at update_send on the side
+stream; `--gossip lockstep` uses DistGroup, whose gloo barrier on one GPU synchronises the
+host every round, so there the pull finishes before the host has enqueued the step).  Run it under
 
   rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/overlap -o ov -- python3 tools/overlap_trace.py
 
@@ -30,7 +31,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def worker(rank, world, port, cfg, steps, batch, out_dir):
+def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async"):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "examples"))
     import time
@@ -48,7 +49,7 @@ def worker(rank, world, port, cfg, steps, batch, out_dir):
     torch.cuda.set_device(dev)
     torch.manual_seed(rank)
     net = resnet18().to(dev)
-    adapter = DpwaPyTorchAdapter(net, "w%d" % rank, cfg, seed=100 + rank, group="lockstep", pull="kernel:256")
+    adapter = DpwaPyTorchAdapter(net, "w%d" % rank, cfg, seed=100 + rank, group=gossip, pull="kernel:256")
     opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
     x = torch.randn(batch, 3, 32, 32, device=dev)
     y = torch.randint(0, 10, (batch,), device=dev)
@@ -157,7 +158,7 @@ def run(args):
     port = s.getsockname()[1]
     s.close()
     os.makedirs(args.out, exist_ok=True)
-    mp.spawn(worker, args=(2, port, cfg, args.steps, args.batch, args.out), nprocs=2, join=True)
+    mp.spawn(worker, args=(2, port, cfg, args.steps, args.batch, args.out, args.gossip), nprocs=2, join=True)
     res = [json.load(open(os.path.join(args.out, "overlap_rank%d.json" % r))) for r in range(2)]
     print(json.dumps(res))
 
@@ -208,7 +209,9 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "overlap_runs"))
     ap.add_argument("--procs", type=int, default=1, choices=[1, 2],
-                    help="1: two learners in this process (prefetching LocalGroup); 2: one rank each (DistGroup)")
+                    help="1: two learners in this process (prefetching LocalGroup); 2: one rank each")
+    ap.add_argument("--gossip", default="async", choices=["async", "lockstep"],
+                    help="--procs 2: free-running rounds (the default group, no per-round barrier) or lock-step")
     ap.add_argument("--analyze", default=None, help="rocprofv3 output directory to analyse instead of running")
     args = ap.parse_args()
     if args.analyze:
