@@ -54,16 +54,23 @@ def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async"):
     x = torch.randn(batch, 3, 32, 32, device=dev)
     y = torch.randint(0, 10, (batch,), device=dev)
 
+    host = {"send": 0.0, "wait": 0.0, "n": 0}
+
     def step(gossip, loss):
         if gossip:
+            t = time.perf_counter()
             adapter.update_send(loss)
+            host["send"] += time.perf_counter() - t
         opt.zero_grad(set_to_none=True)
         out = F.cross_entropy(net(x), y)
         out.backward()
         opt.step()
         loss = out.detach()
         if gossip:
+            t = time.perf_counter()
             adapter.update_wait(loss)
+            host["wait"] += time.perf_counter() - t
+            host["n"] += 1
         return loss
 
     loss = torch.tensor(2.3, device=dev)
@@ -82,7 +89,9 @@ def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async"):
     with open(os.path.join(out_dir, "overlap_rank%d.json" % rank), "w") as f:
         json.dump({"rank": rank, "pid": os.getpid(), "steps": steps, "batch": batch,
                    "ms_per_step_plain": 1e3 * times[False] / steps, "ms_per_step_gossip": 1e3 * times[True] / steps,
-                   "final_clock": adapter.connection.clock}, f)
+                   "final_clock": adapter.connection.clock,
+                   "host_ms_in_update_send": 1e3 * host["send"] / max(1, host["n"]),
+                   "host_ms_in_update_wait": 1e3 * host["wait"] / max(1, host["n"])}, f)
     adapter.connection.close()
     dist.barrier()
     dist.destroy_process_group()
