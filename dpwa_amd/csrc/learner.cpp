@@ -322,6 +322,15 @@ struct dpwa_learner {
     hipEvent_t ev_consumed = nullptr;   // this learner finished reading its fetch source
     hipStream_t consume_stream = nullptr;
     bool consumed_once = false;
+    // Fetches of published snapshots (DPWA_FETCH_PUBLISHED: the gossip board) alternate between
+    // two staging buffers and are not ordered after the caller's stream: each waits only for
+    // the average that last read its buffer (ev_stage_done), so a pull starts at update_send
+    // instead of after the caller's queued work, and a peer's read mark is released sooner.
+    char *staging_alt = nullptr;        // second staging buffer, allocated at the first such fetch
+    hipEvent_t ev_stage_done[2] = {nullptr, nullptr};
+    bool stage_read[2] = {false, false};
+    int stage_next = 0;
+    int src_stage = -1;                 // staging buffer (0 / 1) l->src points into, -1: none
     hipEvent_t ev_factor = nullptr;     // last factor computation done
     // write-through snapshot: the last average also wrote its result into the slot of the
     // next publish (for the flat buffer `wt_flat`, on stream `wt_stream`)
@@ -483,6 +492,9 @@ int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype
         if ((e = hipEventCreateWithFlags(&l->ev_issue, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_fetched, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_consumed, hipEventDisableTiming)) != hipSuccess) break;
+        for (auto &ev : l->ev_stage_done)
+            if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) break;
+        if (e != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_factor, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_wt, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_read, hipEventDisableTiming)) != hipSuccess) break;
@@ -525,6 +537,9 @@ int dpwa_learner_destroy(dpwa_learner *l)
     if (l->ev_issue) (void)hipEventDestroy(l->ev_issue);
     if (l->ev_fetched) (void)hipEventDestroy(l->ev_fetched);
     if (l->ev_consumed) (void)hipEventDestroy(l->ev_consumed);
+    for (auto ev : l->ev_stage_done)
+        if (ev) (void)hipEventDestroy(ev);
+    if (l->staging_alt) (void)hipFree(l->staging_alt);
     if (l->ev_factor) (void)hipEventDestroy(l->ev_factor);
     if (l->ev_wt) (void)hipEventDestroy(l->ev_wt);
     if (l->ev_read) (void)hipEventDestroy(l->ev_read);
@@ -754,8 +769,9 @@ int dpwa_learner_attach_fds(dpwa_learner *l, int peer_id, const void *handle, in
     return DPWA_OK;
 }
 
-int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int zero_copy, dpwa_stream_t stream)
+int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int flags, dpwa_stream_t stream)
 {
+    const int zero_copy = flags & DPWA_FETCH_ZERO_COPY;
     if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_fetch: NULL learner");
     auto it = l->peers.find(peer_id);
     if (it == l->peers.end()) return set_error(DPWA_ERR_ARG, "dpwa_learner_fetch: peer %d not attached", peer_id);
@@ -782,7 +798,32 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
     if (zero_copy && ep.kind == 1 && ep.device == l->device) {
         l->src = peer_slot;             // read in place; stream order covers the rest
         l->src_copied = false;
+        l->src_stage = -1;
+    } else if ((flags & DPWA_FETCH_PUBLISHED) && ep.kind == 2) {
+        if (!l->staging_alt) {
+            HIP_TRY(hipMalloc(&l->staging_alt, l->slot_stride));
+            HIP_TRY(hipMemsetAsync(l->staging_alt, 0, kHeader, l->side));
+        }
+        const int b = l->stage_next;
+        l->stage_next ^= 1;
+        char *dst = b == 0 ? l->staging : l->staging_alt;
+        // WAR: the average that last read this buffer; nothing else on the caller's stream
+        if (l->stage_read[b]) HIP_TRY(hipStreamWaitEvent(l->side, l->ev_stage_done[b], 0));
+        const size_t nbytes = kHeader + round_up(l->payload_bytes, 16);
+        const LaunchTiming *ft = l->fetch_timing_used < (int)l->fetch_timing.size()
+                                     ? &l->fetch_timing[l->fetch_timing_used++] : nullptr;
+        if (ft) HIP_TRY(hipEventRecord(ft->start, l->side));
+        if (l->pull_mode == DPWA_PULL_KERNEL)
+            HIP_TRY(launch_pull(dst, peer_slot, (int64_t)nbytes, l->pull_blocks, true, l->side));
+        else
+            HIP_TRY(hipMemcpyAsync(dst, peer_slot, nbytes, hipMemcpyDefault, l->side));
+        if (ft) HIP_TRY(hipEventRecord(ft->stop, l->side));
+        HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
+        l->src = dst;
+        l->src_copied = true;
+        l->src_stage = b;
     } else {
+        if (l->stage_read[0]) HIP_TRY(hipStreamWaitEvent(l->side, l->ev_stage_done[0], 0));
         HIP_TRY(hipEventRecord(l->ev_issue, s));
         HIP_TRY(hipStreamWaitEvent(l->side, l->ev_issue, 0));
         // WAR on our own staging buffer: the previous average must have consumed it.
@@ -803,6 +844,7 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
         HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
         l->src = l->staging;
         l->src_copied = true;
+        l->src_stage = 0;
     }
     l->src_owner = ep.kind == 1 ? ep.local : nullptr;
     l->src_slot = k;
@@ -842,6 +884,14 @@ int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dp
     return DPWA_OK;
 }
 
+// The fetched snapshot in staging buffer src_stage has been read by everything enqueued on s.
+static hipError_t staging_read(dpwa_learner *l, hipStream_t s)
+{
+    if (l->src_stage < 0 || !l->src_copied) return hipSuccess;
+    l->stage_read[l->src_stage] = true;
+    return hipEventRecord(l->ev_stage_done[l->src_stage], s);
+}
+
 static void finish_fetch(dpwa_learner *l)
 {
     l->have_fetch = false;
@@ -856,6 +906,7 @@ int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream)
     DeviceGuard dg(l->device);
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(launch_lerp(l->dtype, flat, l->src + kHeader, l->n, &l->ctl->coef, 0.f, 0.f, s));
+    HIP_TRY(staging_read(l, s));
     l->wt_valid = false;
     l->consume_stream = s;
     l->consumed_once = true;
@@ -888,6 +939,7 @@ static int average_impl(dpwa_learner *l, void *flat, double loss, const double *
         timing = &l->timing[l->timing_used++];
     l->timing_armed = false;
     HIP_TRY(launch_average(l->dtype, flat, l->src + kHeader, l->n, fa, snap, s, timing));
+    HIP_TRY(staging_read(l, s));
     l->consume_stream = s;
     l->consumed_once = true;
     l->cur = (l->cur + 1) & 3;
@@ -966,6 +1018,7 @@ int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *pay
         HIP_TRY(hipEventRecord(l->ev_consumed, l->consume_stream));
         HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
     }
+    if (l->stage_read[0]) HIP_TRY(hipStreamWaitEvent(l->side, l->ev_stage_done[0], 0));
     // pageable host sources: the calls return once the host bytes have been taken
     HIP_TRY(hipMemcpyAsync(l->staging, header, kHeader, hipMemcpyHostToDevice, l->side));
     if (payload_bytes)
@@ -973,6 +1026,7 @@ int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *pay
     HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
     l->src = l->staging;
     l->src_copied = true;
+    l->src_stage = 0;
     l->src_owner = nullptr;
     l->src_slot = -1;
     l->have_fetch = true;
@@ -1125,6 +1179,7 @@ int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_
         HIP_TRY(hipEventRecord(l->ev_consumed, l->consume_stream));
         HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
     }
+    if (my_pick >= 0 && l->stage_read[0]) HIP_TRY(hipStreamWaitEvent(l->side, l->ev_stage_done[0], 0));
     HIP_TRY(launch_relay(2, a, blocks, l->side));
     HIP_TRY(hipEventRecord(l->ev_relay, l->side));
     l->relay_pending = true;
@@ -1132,6 +1187,7 @@ int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_
         HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
         l->src = l->staging;
         l->src_copied = true;
+        l->src_stage = 0;
         l->src_owner = nullptr;
         l->src_slot = -1;
         l->have_fetch = true;

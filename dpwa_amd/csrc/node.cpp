@@ -217,7 +217,8 @@ static int start_fetch(dpwa_node *n, int flags, dpwa_stream_t stream)
         n->last_attempts = attempts;
         if (peer < 0) return DPWA_OK;
         const int r = n->board_rank[peer];
-        if ((rc = dpwa_learner_fetch(n->learner, peer, version, 0, stream))) {
+        // a completed publish (the board advertised it): the pull needs no ordering after `stream`
+        if ((rc = dpwa_learner_fetch(n->learner, peer, version, DPWA_FETCH_PUBLISHED, stream))) {
             dpwa_board_release(n->board, r, nullptr, 1);
             return rc;
         }

@@ -159,11 +159,16 @@ int dpwa_learner_attach_fds(dpwa_learner *l, int peer_id, const void *handle, in
 
 /* The fetch (TxThread request -> reply, conn.py:297-298): pull peer `peer_id`'s snapshot of
  * publish number `peer_version` (1-based) into this learner's staging buffer on the
- * learner's side stream, after all work already enqueued on `stream`.  For a peer on the
- * same device with zero_copy != 0 no bytes move: the average reads the peer's slot in place.
- * Slot reuse is protected for local peers by events; for IPC peers by the caller's
- * lock-step barrier (a slot is rewritten two publishes later). */
-int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int zero_copy,
+ * learner's side stream, after all work already enqueued on `stream`.  flags:
+ * DPWA_FETCH_ZERO_COPY -- for a peer on the same device no bytes move: the average reads the
+ * peer's slot in place; DPWA_FETCH_PUBLISHED -- an IPC peer's snapshot whose publish is
+ * already complete (the gossip board advertised it): the pull is not ordered after `stream`
+ * and alternates between two staging buffers, waiting only for the average that last read
+ * the one it fills.  Slot reuse is protected for local peers by events; for IPC peers by the
+ * caller's lock-step barrier or the board's read marks. */
+#define DPWA_FETCH_ZERO_COPY 1
+#define DPWA_FETCH_PUBLISHED 2
+int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int flags,
                        dpwa_stream_t stream);
 
 /* update_wait's averaging (dpwa.py:133-155 + pytorch.py:64-68) as ONE kernel: make `stream`
