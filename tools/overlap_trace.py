@@ -31,7 +31,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async"):
+def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async", sync_loss=True):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "examples"))
     import time
@@ -65,7 +65,8 @@ def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async"):
         out = F.cross_entropy(net(x), y)
         out.backward()
         opt.step()
-        loss = out.detach()
+        # main.py:142 reads the loss on the host every step (a sync), and passes a float
+        loss = float(out) if sync_loss else out.detach()
         if gossip:
             t = time.perf_counter()
             adapter.update_wait(loss)
@@ -73,7 +74,7 @@ def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async"):
             host["n"] += 1
         return loss
 
-    loss = torch.tensor(2.3, device=dev)
+    loss = 2.3 if sync_loss else torch.tensor(2.3, device=dev)
     times = {}
     for gossip in (False, True):
         for _ in range(5):
@@ -167,7 +168,8 @@ def run(args):
     port = s.getsockname()[1]
     s.close()
     os.makedirs(args.out, exist_ok=True)
-    mp.spawn(worker, args=(2, port, cfg, args.steps, args.batch, args.out, args.gossip), nprocs=2, join=True)
+    mp.spawn(worker, args=(2, port, cfg, args.steps, args.batch, args.out, args.gossip, not args.no_sync),
+             nprocs=2, join=True)
     res = [json.load(open(os.path.join(args.out, "overlap_rank%d.json" % r))) for r in range(2)]
     print(json.dumps(res))
 
@@ -219,6 +221,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "overlap_runs"))
     ap.add_argument("--procs", type=int, default=1, choices=[1, 2],
                     help="1: two learners in this process (prefetching LocalGroup); 2: one rank each")
+    ap.add_argument("--no-sync", action="store_true",
+                    help="--procs 2: keep the loss on the device (the reference loop reads it every step)")
     ap.add_argument("--gossip", default="async", choices=["async", "lockstep"],
                     help="--procs 2: free-running rounds (the default group, no per-round barrier) or lock-step")
     ap.add_argument("--analyze", default=None, help="rocprofv3 output directory to analyse instead of running")
