@@ -54,13 +54,14 @@ def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async", sync_l
     x = torch.randn(batch, 3, 32, 32, device=dev)
     y = torch.randint(0, 10, (batch,), device=dev)
 
-    host = {"send": 0.0, "wait": 0.0, "n": 0}
+    host = {"send": 0.0, "wait": 0.0, "n": 0, "sends": [], "waits": []}
 
     def step(gossip, loss):
         if gossip:
             t = time.perf_counter()
             adapter.update_send(loss)
             host["send"] += time.perf_counter() - t
+            host["sends"].append(time.perf_counter() - t)
         opt.zero_grad(set_to_none=True)
         out = F.cross_entropy(net(x), y)
         out.backward()
@@ -71,6 +72,7 @@ def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async", sync_l
             t = time.perf_counter()
             adapter.update_wait(loss)
             host["wait"] += time.perf_counter() - t
+            host["waits"].append(time.perf_counter() - t)
             host["n"] += 1
         return loss
 
@@ -92,7 +94,10 @@ def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async", sync_l
                    "ms_per_step_plain": 1e3 * times[False] / steps, "ms_per_step_gossip": 1e3 * times[True] / steps,
                    "final_clock": adapter.connection.clock,
                    "host_ms_in_update_send": 1e3 * host["send"] / max(1, host["n"]),
-                   "host_ms_in_update_wait": 1e3 * host["wait"] / max(1, host["n"])}, f)
+                   "host_ms_in_update_wait": 1e3 * host["wait"] / max(1, host["n"]),
+                   "host_ms_update_send_median_max": [round(1e3 * sorted(host["sends"])[len(host["sends"]) // 2], 3),
+                                                      round(1e3 * max(host["sends"]), 3)] if host["sends"] else None},
+                  f)
     adapter.connection.close()
     dist.barrier()
     dist.destroy_process_group()
