@@ -167,7 +167,8 @@ def run(args):
     sys.path.insert(0, ROOT)
     from dpwa_amd.launch import write_config
     tmp = tempfile.mkdtemp(prefix="dpwa_overlap_")
-    cfg = write_config(os.path.join(tmp, "dpwa.yaml"), ["w0", "w1"], interpolation="constant")
+    cfg = write_config(os.path.join(tmp, "dpwa.yaml"), ["w0", "w1"], interpolation="constant",
+                       fetch_probability=args.fetch_probability)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -226,6 +227,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "overlap_runs"))
     ap.add_argument("--procs", type=int, default=1, choices=[1, 2],
                     help="1: two learners in this process (prefetching LocalGroup); 2: one rank each")
+    ap.add_argument("--fetch-probability", type=float, default=1.0, help="--procs 2: the config's fetch_probability")
     ap.add_argument("--no-sync", action="store_true",
                     help="--procs 2: keep the loss on the device (the reference loop reads it every step)")
     ap.add_argument("--gossip", default="async", choices=["async", "lockstep"],
