@@ -78,7 +78,8 @@ def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async", sync_l
 
     loss = 2.3 if sync_loss else torch.tensor(2.3, device=dev)
     times = {}
-    for gossip in (False, True):
+    sequence = []
+    for gossip in (False, True, False, True):      # interleaved: order effects (clocks) show up
         for _ in range(5):
             loss = step(gossip, loss)
         torch.cuda.synchronize()
@@ -88,11 +89,12 @@ def worker(rank, world, port, cfg, steps, batch, out_dir, gossip="async", sync_l
             loss = step(gossip, loss)
         torch.cuda.synchronize()
         times[gossip] = time.perf_counter() - t0
+        sequence.append(("gossip" if gossip else "plain", round(1e3 * times[gossip] / steps, 3)))
         dist.barrier()
     with open(os.path.join(out_dir, "overlap_rank%d.json" % rank), "w") as f:
         json.dump({"rank": rank, "pid": os.getpid(), "steps": steps, "batch": batch,
                    "ms_per_step_plain": 1e3 * times[False] / steps, "ms_per_step_gossip": 1e3 * times[True] / steps,
-                   "final_clock": adapter.connection.clock,
+                   "final_clock": adapter.connection.clock, "sequence_ms_per_step": sequence,
                    "host_ms_in_update_send": 1e3 * host["send"] / max(1, host["n"]),
                    "host_ms_in_update_wait": 1e3 * host["wait"] / max(1, host["n"]),
                    "host_ms_update_send_median_max": [round(1e3 * sorted(host["sends"])[len(host["sends"]) // 2], 3),
