@@ -50,7 +50,7 @@ def worker(rank, port, mode):
         h = H()
         assert lib.hipIpcGetMemHandle(ctypes.byref(h), ctypes.c_void_p(buf.data_ptr())) == 0
         hs = [None, None]
-        dist.all_gather_object(hs, bytes(h.r))
+        dist.all_gather_object(hs, ctypes.string_at(ctypes.addressof(h), 64))
         other = H.from_buffer_copy(hs[1 - rank])
         p = ctypes.c_void_p()
         assert lib.hipIpcOpenMemHandle(ctypes.byref(p), other, 1) == 0
