@@ -38,7 +38,8 @@ def worker(rank, port, mode):
     torch.cuda.set_device(dev)
     out = {"before": bench(torch, dev)}
     dist.barrier()
-    if mode == "hipipc":
+    if mode.startswith("hipipc"):
+        one_way = mode == "hipipc-oneway"          # rank 0 only exports, rank 1 only opens
         with open("/proc/self/maps") as f:
             path = sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})[0]
         lib = ctypes.CDLL(path)
@@ -53,11 +54,14 @@ def worker(rank, port, mode):
         dist.all_gather_object(hs, ctypes.string_at(ctypes.addressof(h), 64))
         other = H.from_buffer_copy(hs[1 - rank])
         p = ctypes.c_void_p()
-        assert lib.hipIpcOpenMemHandle(ctypes.byref(p), other, 1) == 0
+        opens = not one_way or rank == 1
+        if opens:
+            assert lib.hipIpcOpenMemHandle(ctypes.byref(p), other, 1) == 0
         dist.barrier()
         out["mapped"] = bench(torch, dev)
         dist.barrier()
-        lib.hipIpcCloseMemHandle(p)
+        if opens:
+            lib.hipIpcCloseMemHandle(p)
         dist.barrier()
         out["closed"] = bench(torch, dev)
     else:
