@@ -13,15 +13,19 @@ sys.path.insert(0, ROOT)
 
 
 def bench(torch, dev, reps=60):
+    """ms per iteration of a conv and a GEMM (the training step's two kernel families)."""
     x = torch.randn(128, 64, 32, 32, device=dev)
     conv = torch.nn.Conv2d(64, 64, 3, padding=1).to(dev)
+    a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
     with torch.no_grad():
         for _ in range(5):
             conv(x)
+            a @ a
         torch.cuda.synchronize()
         t = time.perf_counter()
         for _ in range(reps):
             conv(x)
+            a @ a
         torch.cuda.synchronize()
     return 1e3 * (time.perf_counter() - t) / reps
 
@@ -38,7 +42,13 @@ def worker(rank, port, mode):
     torch.cuda.set_device(dev)
     out = {"before": bench(torch, dev)}
     dist.barrier()
-    if mode.startswith("hipipc"):
+    if mode == "none":                 # control: same barriers and benchmarks, no mapping
+        dist.barrier()
+        out["mapped"] = bench(torch, dev)
+        dist.barrier()
+        dist.barrier()
+        out["closed"] = bench(torch, dev)
+    elif mode.startswith("hipipc"):
         one_way = mode == "hipipc-oneway"          # rank 0 only exports, rank 1 only opens
         with open("/proc/self/maps") as f:
             path = sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})[0]
