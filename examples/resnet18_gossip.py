@@ -113,12 +113,17 @@ def main(argv=None):
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
-    run(args.warmup, False)
-    t_plain = run(args.steps, False)
     group = {"group": args.gossip} if world > 1 else {}
     adapters = [DpwaPyTorchAdapter(nets[i], names[g], cfg, seed=100 + g, **group) for i, g in enumerate(mine)]
+    run(args.warmup, False)
     run(args.warmup, True, adapters)
-    t_gossip = run(args.steps, True, adapters)
+    # interleaved phases, the first pair discarded: a run's first phase executes at a higher
+    # GPU clock than the later ones (profiles/r02_overlap_2proc.json)
+    sequence = []
+    for gossip in (False, True) * 3:
+        sequence.append((gossip, run(args.steps, gossip, adapters)))
+    t_plain = sum(t for g, t in sequence[2:] if not g) / 2
+    t_gossip = sum(t for g, t in sequence[2:] if g) / 2
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([t_plain, t_gossip], device=dev)
