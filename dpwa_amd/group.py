@@ -113,6 +113,9 @@ class _FdServer:
     TIMEOUT_S = 600
 
     def __init__(self, fds, expected):
+        if len(fds) > 250:          # one SCM_RIGHTS message carries at most 253 fds
+            raise ValueError("%d chunk fds exceed one socket message; allocations this large are not supported"
+                             % len(fds))
         self.fds, self.error = list(fds), None
         self.sock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
         self.address = "\0dpwa-fds-%d-%s" % (os.getpid(), os.urandom(8).hex())
