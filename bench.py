@@ -355,14 +355,16 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64):
     nbuf = 3 if write_through else 2
     pairs = max(2, int(np.ceil(1.2e9 / (nbuf * numel * esize))))
     launches = max(2 * pairs, min(launches, int(np.ceil(64 * 134e6 / (3 * numel * esize)))))
-    hdr = 256 // esize
+    hdr = _lib.SLOT_PAYLOAD_OFFSET // esize
     params, slots, snaps = [], [], []
     for _ in range(pairs):
         params.append(torch.empty(numel, device=device, dtype=dtype).normal_())
-        slot = torch.zeros(hdr + numel, device=device, dtype=dtype)     # 256-B header (zeros) + payload
+        # a snapshot slot as the learner lays it out: header (zeros) and pad, then the payload
+        slot = torch.zeros(hdr + numel, device=device, dtype=dtype)
         slot[hdr:].normal_()
         slots.append(slot)
-        snaps.append(torch.empty(numel, device=device, dtype=dtype) if write_through else None)
+        # the write-through destination is the payload of another slot
+        snaps.append(torch.empty(hdr + numel, device=device, dtype=dtype)[hdr:] if write_through else None)
     clock = torch.zeros(2, device=device, dtype=torch.float64)
     coef = torch.zeros(4, device=device, dtype=torch.float64)           # dpwa_coef, 32 B
     cfg = _lib.Interp(_lib.INTERP_CONSTANT, 0, 0.5, 0.0)

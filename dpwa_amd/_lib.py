@@ -18,12 +18,13 @@ LIB_PATH = os.environ.get("DPWA_HIP_LIB", os.path.join(_HERE, "libdpwa_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dpwa_hip.h")
 
 # Constants mirrored from include/dpwa_hip.h
-ABI_VERSION = 2
+ABI_VERSION = 3
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_NOMEM = 0, -1, -2, -3, -4
 F32, BF16, F64 = 0, 1, 2
 INTERP_CONSTANT, INTERP_CLOCK, INTERP_LOSS = 0, 1, 2
 STATUS_OK, STATUS_ZERO_DIVISION = 0, 1
 IPC_HANDLE_BYTES = 128
+SLOT_PAYLOAD_OFFSET = 4096   # [dpwa_header | pad | payload]
 CONNECT_OK, CONNECT_REFUSED, CONNECT_ERROR = 0, 1, 2
 REPLY_PAYLOAD, REPLY_EMPTY, REPLY_TIMEOUT, REPLY_ERROR = 3, 4, 5, 6
 PEER_READY, PEER_NO_STATE, PEER_DOWN, PEER_SLOW, PEER_DEAD = 0, 1, 2, 3, 4

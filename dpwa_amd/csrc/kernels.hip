@@ -464,7 +464,7 @@ __global__ __launch_bounds__(BLOCK) void k_publish(char *__restrict__ slot, cons
                                                    const double *__restrict__ loss_d, int32_t loss_f32,
                                                    uint64_t version)
 {
-    char *payload = slot + sizeof(dpwa_header);
+    char *payload = slot + DPWA_SLOT_PAYLOAD_OFFSET;
     if (VEC) {   // one 16-B item per lane, streaming policy of the lerp (nt loads, sc1 stores)
         constexpr int SPAN = BLOCK * 16;
         const int64_t n16 = nbytes >> 4;
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void k_relay_phase1(RelayArgs a)
     for (int i = 0; i < a.world; ++i) active |= (a.picks[i] == j);
     if (!active) return;
     const int64_t len = stripe_len(a.rank, a.stripe, a.payload);
-    const char *src = a.slots[j] + a.slot_off + 256 + (int64_t)a.rank * a.stripe;
+    const char *src = a.slots[j] + a.slot_off + DPWA_SLOT_PAYLOAD_OFFSET + (int64_t)a.rank * a.stripe;
     char *dst = a.relay_mine + (int64_t)j * a.stripe;
     copy16((u32x4 *)dst, (const u32x4 *)src, len >> 4);
 }
@@ -583,10 +583,10 @@ __global__ __launch_bounds__(kBlock) void k_relay_phase2(RelayArgs a)
         reinterpret_cast<u32x4 *>(a.staging)[threadIdx.x] =
             reinterpret_cast<const u32x4 *>(a.slots[j] + a.slot_off)[threadIdx.x];
     const int64_t len = stripe_len(s, a.stripe, a.payload);
-    const char *src = s == j        ? a.slots[j] + a.slot_off + 256 + (int64_t)s * a.stripe
+    const char *src = s == j        ? a.slots[j] + a.slot_off + DPWA_SLOT_PAYLOAD_OFFSET + (int64_t)s * a.stripe
                       : s == a.rank ? a.relay_mine + (int64_t)j * a.stripe
                                     : a.relays[s] + (int64_t)j * a.stripe;
-    copy16((u32x4 *)(a.staging + 256 + (int64_t)s * a.stripe), (const u32x4 *)src, len >> 4);
+    copy16((u32x4 *)(a.staging + DPWA_SLOT_PAYLOAD_OFFSET + (int64_t)s * a.stripe), (const u32x4 *)src, len >> 4);
 }
 
 hipError_t launch_relay(int phase, const RelayArgs &a, int blocks_per_part, hipStream_t s)

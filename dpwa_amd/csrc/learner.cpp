@@ -3,7 +3,7 @@
 // The reference keeps, per node, an RxThread that serves the latest (state, payload)
 // under a lock (conn.py:51-172) and a TxThread that fetches one peer's (state, payload)
 // over TCP (conn.py:197-334).  Here a node (learner) owns, on its GPU:
-//   slots    two snapshot slots [header 256 B | payload] -- RxThread.state/payload,
+//   slots    two snapshot slots [header 256 B | pad to 4 KiB | payload] -- RxThread.state/payload,
 //            double-buffered so a publish never overwrites the slot a peer may be reading
 //   staging  one slot-sized buffer receiving a peer's snapshot -- TxThread.peer_payload
 //   ctl      the device clock and the averaging coefficients (dpwa_coef)
@@ -53,6 +53,8 @@ using namespace dpwa;
 namespace {
 
 constexpr size_t kHeader = sizeof(dpwa_header);
+constexpr size_t kPayloadOff = DPWA_SLOT_PAYLOAD_OFFSET;   // [header | pad | payload]
+static_assert(kPayloadOff >= kHeader && kPayloadOff % 1024 == 0, "payload offset");
 static_assert(sizeof(dpwa_header) == 256, "dpwa_header must be 256 bytes");
 constexpr uint64_t kIpcMagic = 0x445057414950430aULL;  // "DPWAIPC\n"
 
@@ -454,7 +456,7 @@ int dpwa_average(int32_t dtype, void *param, const void *peer_slot, int64_t n, c
     fa.loss_h = loss;
     fa.coef_out = coef_dev;
     LaunchTiming t{(hipEvent_t)start_event, (hipEvent_t)stop_event};
-    HIP_TRY(launch_average(dtype, param, (const char *)peer_slot + kHeader, n, fa, snap_payload, (hipStream_t)stream,
+    HIP_TRY(launch_average(dtype, param, (const char *)peer_slot + kPayloadOff, n, fa, snap_payload, (hipStream_t)stream,
                            start_event ? &t : nullptr));
     return DPWA_OK;
 }
@@ -474,16 +476,16 @@ int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype
     l->dtype = dtype;
     l->cfg = *cfg;
     l->payload_bytes = (size_t)n * dtype_size(dtype);
-    l->slot_stride = kHeader + round_up(l->payload_bytes, 256);
+    l->slot_stride = kPayloadOff + round_up(l->payload_bytes, kPayloadOff);
     hipError_t e = hipSuccess;
     do {
         if ((e = devmem_alloc(l->slot_mem, 2 * l->slot_stride, device)) != hipSuccess) break;
         l->slots = l->slot_mem.ptr;
         if ((e = hipMalloc(&l->staging, l->slot_stride)) != hipSuccess) break;
         if ((e = hipMalloc(&l->ctl, sizeof(Ctl))) != hipSuccess) break;
-        if ((e = hipMemset(l->slots, 0, kHeader)) != hipSuccess) break;
-        if ((e = hipMemset(l->slots + l->slot_stride, 0, kHeader)) != hipSuccess) break;
-        if ((e = hipMemset(l->staging, 0, kHeader)) != hipSuccess) break;
+        if ((e = hipMemset(l->slots, 0, kPayloadOff)) != hipSuccess) break;
+        if ((e = hipMemset(l->slots + l->slot_stride, 0, kPayloadOff)) != hipSuccess) break;
+        if ((e = hipMemset(l->staging, 0, kPayloadOff)) != hipSuccess) break;
         if ((e = hipMemset(l->ctl, 0, sizeof(Ctl))) != hipSuccess) break;
         if ((e = hipStreamCreateWithFlags(&l->side, hipStreamNonBlocking)) != hipSuccess) break;
         for (auto &ev : l->ev_published)
@@ -802,14 +804,14 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
     } else if ((flags & DPWA_FETCH_PUBLISHED) && ep.kind == 2) {
         if (!l->staging_alt) {
             HIP_TRY(hipMalloc(&l->staging_alt, l->slot_stride));
-            HIP_TRY(hipMemsetAsync(l->staging_alt, 0, kHeader, l->side));
+            HIP_TRY(hipMemsetAsync(l->staging_alt, 0, kPayloadOff, l->side));
         }
         const int b = l->stage_next;
         l->stage_next ^= 1;
         char *dst = b == 0 ? l->staging : l->staging_alt;
         // WAR: the average that last read this buffer; nothing else on the caller's stream
         if (l->stage_read[b]) HIP_TRY(hipStreamWaitEvent(l->side, l->ev_stage_done[b], 0));
-        const size_t nbytes = kHeader + round_up(l->payload_bytes, 16);
+        const size_t nbytes = kPayloadOff + round_up(l->payload_bytes, 16);
         const LaunchTiming *ft = l->fetch_timing_used < (int)l->fetch_timing.size()
                                      ? &l->fetch_timing[l->fetch_timing_used++] : nullptr;
         if (ft) HIP_TRY(hipEventRecord(ft->start, l->side));
@@ -831,7 +833,7 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
             HIP_TRY(hipEventRecord(l->ev_consumed, l->consume_stream));
             HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
         }
-        const size_t nbytes = kHeader + round_up(l->payload_bytes, 16);
+        const size_t nbytes = kPayloadOff + round_up(l->payload_bytes, 16);
         const LaunchTiming *ft = l->fetch_timing_used < (int)l->fetch_timing.size()
                                      ? &l->fetch_timing[l->fetch_timing_used++] : nullptr;
         if (ft) HIP_TRY(hipEventRecord(ft->start, l->side));
@@ -905,7 +907,7 @@ int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream)
     if (!l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_lerp: no factor computed for this fetch");
     DeviceGuard dg(l->device);
     hipStream_t s = (hipStream_t)stream;
-    HIP_TRY(launch_lerp(l->dtype, flat, l->src + kHeader, l->n, &l->ctl->coef, 0.f, 0.f, s));
+    HIP_TRY(launch_lerp(l->dtype, flat, l->src + kPayloadOff, l->n, &l->ctl->coef, 0.f, 0.f, s));
     HIP_TRY(staging_read(l, s));
     l->wt_valid = false;
     l->consume_stream = s;
@@ -924,9 +926,9 @@ static int average_impl(dpwa_learner *l, void *flat, double loss, const double *
         const int k = (int)(l->version % 2);   // slot of the next publish
         int rc = wait_slot_readers(l, k, s);
         if (rc) return rc;
-        snap = l->slots + (size_t)k * l->slot_stride + kHeader;
+        snap = l->slots + (size_t)k * l->slot_stride + kPayloadOff;
         if (l->cfg.method != DPWA_INTERP_LOSS) {   // peers never read this header's loss
-            fa.next_header = (dpwa_header *)(snap - kHeader);
+            fa.next_header = (dpwa_header *)(snap - kPayloadOff);
             fa.clock_next = &l->ctl->clock[(l->cur + 2) & 3];
             fa.next_version = l->version + 1;
             fa.n = l->n;
@@ -938,7 +940,7 @@ static int average_impl(dpwa_learner *l, void *flat, double loss, const double *
     if (l->timing_armed && l->timing_used < (int)l->timing.size() && ((uintptr_t)flat & 15) == 0)
         timing = &l->timing[l->timing_used++];
     l->timing_armed = false;
-    HIP_TRY(launch_average(l->dtype, flat, l->src + kHeader, l->n, fa, snap, s, timing));
+    HIP_TRY(launch_average(l->dtype, flat, l->src + kPayloadOff, l->n, fa, snap, s, timing));
     HIP_TRY(staging_read(l, s));
     l->consume_stream = s;
     l->consumed_once = true;
@@ -991,7 +993,7 @@ int dpwa_learner_read_snapshot(dpwa_learner *l, void *header_out, void *payload_
         const char *slot = l->slots + (size_t)k * l->slot_stride;
         HIP_TRY(hipMemcpyAsync(header_out, slot, kHeader, hipMemcpyDeviceToHost, l->read_stream));
         if (payload_bytes)
-            HIP_TRY(hipMemcpyAsync(payload_out, slot + kHeader, (size_t)payload_bytes, hipMemcpyDeviceToHost,
+            HIP_TRY(hipMemcpyAsync(payload_out, slot + kPayloadOff, (size_t)payload_bytes, hipMemcpyDeviceToHost,
                                    l->read_stream));
         HIP_TRY(hipStreamSynchronize(l->read_stream));
         // a slot is rewritten two publishes later: if that happened meanwhile, read again
@@ -1022,7 +1024,7 @@ int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *pay
     // pageable host sources: the calls return once the host bytes have been taken
     HIP_TRY(hipMemcpyAsync(l->staging, header, kHeader, hipMemcpyHostToDevice, l->side));
     if (payload_bytes)
-        HIP_TRY(hipMemcpyAsync(l->staging + kHeader, payload, (size_t)payload_bytes, hipMemcpyHostToDevice, l->side));
+        HIP_TRY(hipMemcpyAsync(l->staging + kPayloadOff, payload, (size_t)payload_bytes, hipMemcpyHostToDevice, l->side));
     HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
     l->src = l->staging;
     l->src_copied = true;
@@ -1041,7 +1043,7 @@ int dpwa_learner_relay_enable(dpwa_learner *l, int world, int rank)
     if (l->relay_on) return set_error(DPWA_ERR_STATE, "dpwa_learner_relay_enable: already enabled");
     DeviceGuard dg(l->device);
     const int64_t payload16 = (int64_t)round_up(l->payload_bytes, 16);
-    l->relay_stripe = (int64_t)round_up((size_t)((payload16 + world - 1) / world), 256);
+    l->relay_stripe = (int64_t)round_up((size_t)((payload16 + world - 1) / world), kPayloadOff);
     HIP_TRY(devmem_alloc(l->relay_mem, (size_t)l->relay_stripe * world, l->device));
     l->relay_buf = l->relay_mem.ptr;
     HIP_TRY(hipEventCreateWithFlags(&l->ev_relay, hipEventDisableTiming));
@@ -1325,7 +1327,7 @@ int dpwa_learner_copy_fetched(dpwa_learner *l, void *dst_dev, dpwa_stream_t stre
     hipStream_t s = (hipStream_t)stream;
     if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));
     if (l->payload_bytes)
-        HIP_TRY(hipMemcpyAsync(dst_dev, l->src + kHeader, l->payload_bytes, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipMemcpyAsync(dst_dev, l->src + kPayloadOff, l->payload_bytes, hipMemcpyDeviceToDevice, s));
     l->consume_stream = s;   // the staging buffer / peer slot is read on s
     l->consumed_once = true;
     return DPWA_OK;
@@ -1345,7 +1347,7 @@ int dpwa_learner_pointers(dpwa_learner *l, double **clock_dev, dpwa_coef **coef_
     if (clock_dev) *clock_dev = &l->ctl->clock[l->cur];
     if (coef_dev) *coef_dev = &l->ctl->coef;
     if (staging_header_dev) *staging_header_dev = (dpwa_header *)l->staging;
-    if (staging_payload_dev) *staging_payload_dev = l->staging + kHeader;
+    if (staging_payload_dev) *staging_payload_dev = l->staging + kPayloadOff;
     return DPWA_OK;
 }
 

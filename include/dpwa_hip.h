@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DPWA_ABI_VERSION 2
+#define DPWA_ABI_VERSION 3
 
 #define DPWA_OK 0
 #define DPWA_ERR_ARG (-1)     /* bad argument (API misuse)                          */
@@ -54,6 +54,11 @@ typedef void *dpwa_stream_t;
 /* The published `state` of one learner (dpwa.py:115 `{'clock', 'loss'}`), stored as the
  * first 256 bytes of every snapshot slot so that state and parameters travel together
  * exactly as RxThread sends them together (conn.py:110). */
+/* A snapshot slot is [dpwa_header | zero pad | payload]: the payload starts 4 KiB into the
+ * slot, so every 1-KiB wave span of the averaging kernel lies inside one aligned 1-KiB block
+ * (a payload right behind the 256-B header made each span straddle two: 0.7 % slower at
+ * 11.17M fp32 and 2 % at 100M, tools/skew_tune.hip). */
+#define DPWA_SLOT_PAYLOAD_OFFSET 4096
 typedef struct dpwa_header {
     double clock;        /* publisher's clock after `clock += 1` (dpwa.py:112)           */
     double loss;         /* loss given to update_send (dpwa.py:115)                      */
@@ -106,7 +111,7 @@ int dpwa_lerp_bf16_host(uint16_t *param, const uint16_t *peer, int64_t n, double
 
 /* The fused average of dpwa_learner_average without a learner (the product kernel over
  * caller-owned buffers): reads clock_dev[0] and the 256-B dpwa_header at `peer_slot`, lerps the
- * n elements following that header into `param` in place, writes clock_dev[1] = new clock and
+ * n elements at peer_slot + DPWA_SLOT_PAYLOAD_OFFSET into `param` in place, writes clock_dev[1] = new clock and
  * *coef_dev.  snap_payload (NULL or n elements): the write-through form, which also stores the
  * result there (dpwa_learner_average_through).  start_event/stop_event (hipEvent_t, both or neither): the kernel is launched with
  * hipExtLaunchKernelGGL so they record its own begin and end (measurement). */

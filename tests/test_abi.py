@@ -33,6 +33,7 @@ def test_header_constants_match_binding():
     consts = dict(re.findall(r"#define (DPWA_\w+) \(?(-?\d+)\)?", text))
     assert int(consts["DPWA_ABI_VERSION"]) == _lib.ABI_VERSION
     assert int(consts["DPWA_IPC_HANDLE_BYTES"]) == _lib.IPC_HANDLE_BYTES
+    assert int(consts["DPWA_SLOT_PAYLOAD_OFFSET"]) == _lib.SLOT_PAYLOAD_OFFSET
     for c, v in [("DPWA_F32", _lib.F32), ("DPWA_BF16", _lib.BF16), ("DPWA_INTERP_LOSS", _lib.INTERP_LOSS),
                  ("DPWA_STATUS_ZERO_DIVISION", _lib.STATUS_ZERO_DIVISION), ("DPWA_REPLY_ERROR", _lib.REPLY_ERROR),
                  ("DPWA_PEER_DEAD", _lib.PEER_DEAD), ("DPWA_ERR_STATE", _lib.ERR_STATE)]:
