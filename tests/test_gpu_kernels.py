@@ -211,3 +211,74 @@ def test_zero_division_status_makes_lerp_a_noop():
     dev_lerp(p, q, coef)
     torch.cuda.synchronize()
     assert torch.equal(p, before)
+
+
+def average_slot(peer_payload, peer_clock, peer_loss):
+    """A peer snapshot laid out as a learner's slot (ABI 3): dpwa_header at 0, payload at
+    DPWA_SLOT_PAYLOAD_OFFSET."""
+    off = _lib.SLOT_PAYLOAD_OFFSET
+    raw = torch.zeros(off + peer_payload.numel() * peer_payload.element_size(), dtype=torch.uint8, device=DEV)
+    raw[:256].copy_(torch.frombuffer(bytearray(header_bytes(peer_clock, peer_loss)), dtype=torch.uint8))
+    if peer_payload.numel():
+        raw[off:].copy_(peer_payload.view(torch.uint8))
+    return raw
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 5, 9, 4099, 65536 + 13, (1 << 20) + 5])
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("write_through", [False, True])
+def test_fused_average_entry_point_vs_oracle(n, dtype, write_through):
+    """dpwa_average -- the product kernel (device factor + lerp [+ the next snapshot]) over
+    caller-owned buffers -- at ragged sizes: clock interpolation (interpolation.py:22-24) and
+    the clock update of dpwa.py:150 against the oracle policy, the payload against the C oracle
+    lerp, and the write-through copy equal to the averaged parameters."""
+    rng = np.random.default_rng(1000 + n)
+    p32 = rng.standard_normal(n).astype(np.float32)
+    q32 = rng.standard_normal(n).astype(np.float32)
+    my_clock, peer_clock = 3.0, 7.0
+    f, new_clock = opolicy.factor_and_clock("clock", None, 0.0, my_clock, peer_clock, 1.0, 1.0)
+    if dtype == "f32":
+        exp = p32.copy()
+        olerp.c_lerp_f32_(exp, q32, f)
+        p, q = torch.from_numpy(p32).to(DEV), torch.from_numpy(q32).to(DEV)
+    else:
+        pu, qu = olerp.f32_to_bf16(p32), olerp.f32_to_bf16(q32)
+        exp = pu.copy()
+        olerp.c_lerp_bf16_(exp, qu, f)
+        p, q = from_u16(pu), from_u16(qu)
+    slot = average_slot(q, peer_clock, 1.0)
+    snap = torch.full_like(p, float("nan")) if write_through else None
+    clock = torch.tensor([my_clock, -1.0], dtype=torch.float64, device=DEV)
+    coef = torch.zeros(32, dtype=torch.uint8, device=DEV)
+    cfg = _lib.Interp(_lib.INTERP_CLOCK, 0, 0.0, 0.0)
+    _lib.call("dpwa_average", _lib.F32 if dtype == "f32" else _lib.BF16, ptr(p), ptr(slot), n, ctypes.byref(cfg),
+              ptr(clock), 1.0, ptr(coef), ptr(snap) if write_through else None, stream(), None, None)
+    torch.cuda.synchronize()
+    got = p.cpu().numpy() if dtype == "f32" else to_u16(p)
+    assert olerp.bits_equal(got, exp)
+    c = _lib.Coef.from_buffer_copy(coef.cpu().numpy().tobytes())
+    assert c.status == 0 and c.factor == f
+    assert clock[1].item() == new_clock      # dpwa.py:150
+    if write_through and n:
+        assert torch.equal(snap.view(torch.uint8), p.view(torch.uint8))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fused_average_zero_division_still_writes_the_snapshot(dtype):
+    """Loss interpolation with loss + peer_loss == 0 raises ZeroDivisionError in the reference
+    (interpolation.py:31-33): the parameters and clock stay, and a write-through snapshot
+    still receives the (unchanged) parameters, ragged tail included."""
+    n = 4099
+    p = torch.randn(n, device=DEV).to(dtype)
+    before = p.clone()
+    slot = average_slot(torch.randn(n, device=DEV).to(dtype), 5.0, 0.0)
+    snap = torch.zeros_like(p)
+    clock = torch.tensor([2.0, -1.0], dtype=torch.float64, device=DEV)
+    coef = torch.zeros(32, dtype=torch.uint8, device=DEV)
+    cfg = _lib.Interp(_lib.INTERP_LOSS, 0, 0.0, 0.0)
+    _lib.call("dpwa_average", _lib.F32 if dtype == torch.float32 else _lib.BF16, ptr(p), ptr(slot), n,
+              ctypes.byref(cfg), ptr(clock), 0.0, ptr(coef), ptr(snap), stream(), None, None)
+    torch.cuda.synchronize()
+    assert _lib.Coef.from_buffer_copy(coef.cpu().numpy().tobytes()).status == _lib.STATUS_ZERO_DIVISION
+    assert torch.equal(p, before) and torch.equal(snap, before)
+    assert clock[1].item() == 2.0
