@@ -289,7 +289,7 @@ def parity_key(trial):
     kind, _, mode = trial.rpartition("/")
     wt = "+wt" if mode.endswith("+wt") else ""
     base = mode.replace("+wt", "").partition(":")[0]
-    pull = {"copy": "copy", "kernel": "kernel:256", "relay": "relay:32"}[base]
+    pull = {"copy": "copy", "kernel": "kernel:256", "relay": "relay:32", "relay-avg": "relay-avg:32"}[base]
     return "%s/%s%s" % (kind or "lockstep", pull, wt)
 
 
@@ -696,7 +696,7 @@ def main():
         else:
             transports = []
             if args.gossip != "async":
-                transports += ["lockstep/copy", "lockstep/kernel:256", "lockstep/relay:32"]
+                transports += ["lockstep/copy", "lockstep/kernel:256", "lockstep/relay:32", "lockstep/relay-avg:32"]
             if args.gossip != "lockstep":
                 transports += ["async/copy", "async/kernel:256", "async/copy+wt", "async/kernel:256+wt"]
         res = parity_leg(world, rank, local_rank, device, tmp, transports, args.dist_backend)
@@ -725,7 +725,8 @@ def main():
         progress("binding %d lock-step learner(s)" % len(learners))
         run(2, 2, False, 1000)   # binds the learners (IPC exchange) before the transport is chosen
         modes = [args.pull] if args.pull != "auto" else ["copy", "kernel:256", "kernel:1024", "relay:32",
-                                                         "relay:128", "relay:512"]
+                                                         "relay:128", "relay:512", "relay-avg:32",
+                                                         "relay-avg:128", "relay-avg:512"]
         trial_steps = max(10, args.steps // 10)
         if args.gossip != "async":
             for mode in [m for m in modes if verified(m)]:   # short timed trials; the fastest is used below

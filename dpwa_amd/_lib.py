@@ -107,7 +107,7 @@ SIGNATURES = {
     "dpwa_learner_relay_attach_fds": [_vp, _int, _int, _vp, _i64, _pint, _int, _i64],
     "dpwa_learner_relay_wait": [_vp, _vp],
     "dpwa_learner_relay_phase1": [_vp, _vp, _u64, _int, _vp],
-    "dpwa_learner_relay_phase2": [_vp, _vp, _int, _u64, _int],
+    "dpwa_learner_relay_phase2": [_vp, _vp, _int, _u64, _int, _int],
     "dpwa_learner_side_stream": [_vp, ctypes.POINTER(_vp)],
     "dpwa_learner_time_fetches": [_vp, _int],
     "dpwa_learner_read_fetch_times": [_vp, ctypes.POINTER(ctypes.c_float), _int, ctypes.POINTER(_int)],

@@ -242,19 +242,43 @@ template <int POLICY> struct LerpPolicy {
     static constexpr int store = snap_store | ((POLICY & 8) ? kAuxStream : 0);
 };
 
+// Where the peer's bytes are.  ContigSrc: one buffer (a staging buffer, or a peer's slot
+// read in place).  StripeSrc: the relay's stripes, stripe s at src[s] (k_lerp_relay).
+struct ContigSrc {
+    const char *p;
+    // base such that base + byte_offset addresses the span starting at span_off
+    __device__ __forceinline__ const char *span_base(int64_t) const { return p; }
+    __device__ __forceinline__ const char *at(int64_t byte) const { return p + byte; }
+};
+
+struct StripeSrc {
+    const char *src[kMaxRelayRanks];
+    int64_t stripe;    // a multiple of every span (4 KiB multiple): no span straddles stripes
+    __device__ __forceinline__ const char *span_base(int64_t span_off) const
+    {
+        const int64_t s = span_off / stripe;
+        return src[s] - s * stripe;
+    }
+    __device__ __forceinline__ const char *at(int64_t byte) const
+    {
+        const int64_t s = byte / stripe;
+        return src[s] + (byte - s * stripe);
+    }
+};
+
 // One 16-byte item per lane; items beyond n/PER (the ragged tail) go to block 0.
 // DUAL also stores the result into args.snap (write-through snapshot: the next publish of
 // these parameters then needs no copy).  BLOCK lanes per workgroup (kStreamBlock).
-template <class Ops, int MODE, bool DUAL, int BLOCK = kBlock, int POLICY = 0>
-__global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ param,
-                                                const typename Ops::V *__restrict__ peer, int64_t n, LerpArgs args)
+template <class Ops, int MODE, bool DUAL, int BLOCK, int POLICY, class Src>
+__device__ __forceinline__ void lerp_span(typename Ops::V *__restrict__ param, const Src &src, int64_t n,
+                                          const LerpArgs &args)
 {
     using V = typename Ops::V;
     constexpr int SPAN = BLOCK * 16;
     const int64_t nv = n / Ops::PER;
     const int64_t span_off = (int64_t)blockIdx.x * SPAN;
     const int lane_off = threadIdx.x * 16;
-    const __amdgpu_buffer_rsrc_t rq = span_rsrc<SPAN>(peer, span_off, nv * 16);
+    const __amdgpu_buffer_rsrc_t rq = span_rsrc<SPAN>(src.span_base(span_off), span_off, nv * 16);
     const __amdgpu_buffer_rsrc_t rp = span_rsrc<SPAN>(param, span_off, nv * 16);
     // issue this lane's loads before anything else
     const V q = span_load<V>(rq, lane_off);
@@ -300,13 +324,30 @@ __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ pa
         if (DUAL) span_store<V, LerpPolicy<POLICY>::snap_store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, r);
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
-        typename Ops::S *ps = reinterpret_cast<typename Ops::S *>(param);
-        const typename Ops::S *qs = reinterpret_cast<const typename Ops::S *>(peer);
+        using S = typename Ops::S;
+        S *ps = reinterpret_cast<S *>(param);
         const int64_t j = nv * Ops::PER + threadIdx.x;
-        const typename Ops::S r = Ops::lerp_s(a, b, qs[j], ps[j]);
+        const S r = Ops::lerp_s(a, b, *reinterpret_cast<const S *>(src.at(j * (int64_t)sizeof(S))), ps[j]);
         ps[j] = r;
-        if (DUAL) reinterpret_cast<typename Ops::S *>(args.snap)[j] = r;
+        if (DUAL) reinterpret_cast<S *>(args.snap)[j] = r;
     }
+}
+
+template <class Ops, int MODE, bool DUAL, int BLOCK = kBlock, int POLICY = 0>
+__global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ param,
+                                                const typename Ops::V *__restrict__ peer, int64_t n, LerpArgs args)
+{
+    lerp_span<Ops, MODE, DUAL, BLOCK, POLICY>(param, ContigSrc{(const char *)peer}, n, args);
+}
+
+// The relay's fused second phase: the fused average reads the peer's snapshot stripe by stripe
+// where the relay left it (stripe s in rank s's relay buffer, the peer's own stripe in its slot,
+// ours in local HBM) instead of gathering it into staging first.
+template <class Ops, bool DUAL>
+__global__ __launch_bounds__(kStreamBlock) void k_lerp_relay(typename Ops::V *__restrict__ param, int64_t n,
+                                                             LerpArgs args, StripeSrc src)
+{
+    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, 0>(param, src, n, args);
 }
 
 // Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
@@ -454,6 +495,52 @@ hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t 
     args.fused = fa;
     args.snap = snap;
     return launch_any(dtype, COEF_FUSED, param, peer, n, args, s, timing);
+}
+
+__global__ void k_acquire_system();
+
+template <class Ops, bool DUAL>
+static void launch_relay_kernel(void *param, int64_t n, const LerpArgs &args, const StripeSrc &src, hipStream_t s,
+                                const LaunchTiming *timing)
+{
+    const int64_t g = (n / Ops::PER) / kStreamBlock + 1;
+    if (timing)
+        hipExtLaunchKernelGGL((k_lerp_relay<Ops, DUAL>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s, timing->start,
+                              timing->stop, 0, (typename Ops::V *)param, n, args, src);
+    else
+        hipLaunchKernelGGL((k_lerp_relay<Ops, DUAL>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s,
+                           (typename Ops::V *)param, n, args, src);
+}
+
+hipError_t launch_average_relay(int32_t dtype, void *param, int64_t n, const FusedArgs &fa, void *snap,
+                                const RelayArgs &a, int my_pick, hipStream_t s, const LaunchTiming *timing)
+{
+    if (n < 0 || a.world < 1 || a.world > kMaxRelayRanks || my_pick < 0 || my_pick >= a.world ||
+        my_pick == a.rank || a.stripe <= 0 || a.stripe % (kStreamBlock * 16) || !aligned16(param) ||
+        (snap && !aligned16(snap)))
+        return hipErrorInvalidValue;
+    const int j = my_pick;
+    StripeSrc src;
+    for (int r = 0; r < a.world; ++r)   // where stripe r of j's snapshot is (k_relay_phase2's sources)
+        src.src[r] = r == j        ? a.slots[j] + a.slot_off + DPWA_SLOT_PAYLOAD_OFFSET + (int64_t)r * a.stripe
+                     : r == a.rank ? a.relay_mine + (int64_t)j * a.stripe
+                                   : a.relays[r] + (int64_t)j * a.stripe;
+    for (int r = a.world; r < kMaxRelayRanks; ++r) src.src[r] = nullptr;
+    src.stripe = a.stripe;
+    LerpArgs args{};
+    args.fused = fa;
+    args.snap = snap;
+    hipLaunchKernelGGL(k_acquire_system, dim3(256), dim3(64), 0, s);   // remote lines in L2 are stale
+    if (dtype == DPWA_F32) {
+        if (snap) launch_relay_kernel<OpsF32, true>(param, n, args, src, s, timing);
+        else launch_relay_kernel<OpsF32, false>(param, n, args, src, s, timing);
+    } else if (dtype == DPWA_BF16) {
+        if (snap) launch_relay_kernel<OpsBF16, true>(param, n, args, src, s, timing);
+        else launch_relay_kernel<OpsBF16, false>(param, n, args, src, s, timing);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- publish

@@ -82,6 +82,11 @@ struct RelayArgs {
     int32_t world, rank;
 };
 hipError_t launch_relay(int phase, const RelayArgs &a, int blocks_per_part, hipStream_t s);
+// The relay's phase 2 fused into the average: the fused average of `param` reading stripe r of
+// my_pick's snapshot where phase 1 left it (k_lerp_relay), preceded by a system-scope acquire.
+// The header is read from fa.hdr (my_pick's slot).  param / snap 16-B aligned.
+hipError_t launch_average_relay(int32_t dtype, void *param, int64_t n, const FusedArgs &fa, void *snap,
+                                const RelayArgs &a, int my_pick, hipStream_t s, const LaunchTiming *timing = nullptr);
 // Publish of the header only (the payload was written through by the last average).
 hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *clock, double loss,
                                  const double *loss_dev, bool loss_f32, uint64_t version, bool system_release,

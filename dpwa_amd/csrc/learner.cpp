@@ -363,6 +363,12 @@ struct dpwa_learner {
     std::vector<DevMem> relay_imported;      // fd-imported relay buffers to unmap
     hipEvent_t ev_relay = nullptr;           // all relay work of the last round
     bool relay_pending = false;
+    // phase 2 deferred into the average (dpwa_learner_relay_phase2 with fuse != 0): the stripes
+    // are read where phase 1 left them by the next fused average, or gathered into staging
+    // first if the fetch is consumed any other way (relay_materialize)
+    bool relay_deferred = false;
+    RelayArgs relay_saved{};
+    int relay_saved_pick = -1, relay_saved_blocks = 0;
     // host readers of published slots (wire bridge) run on other threads
     std::mutex pub_mu;
     hipStream_t read_stream = nullptr;
@@ -854,6 +860,8 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
     return DPWA_OK;
 }
 
+static int relay_materialize(dpwa_learner *l);
+
 static FusedArgs fused_args(dpwa_learner *l, double loss, const double *loss_dev)
 {
     FusedArgs fa{};
@@ -876,6 +884,8 @@ int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dp
     if (l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_factor: factor already computed for this fetch");
     DeviceGuard dg(l->device);
     hipStream_t s = (hipStream_t)stream;
+    int rc = relay_materialize(l);
+    if (rc) return rc;
     if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
     HIP_TRY(launch_factor(fused_args(l, loss, loss_dev), s));
     HIP_TRY(hipEventRecord(l->ev_factor, s));
@@ -935,13 +945,29 @@ static int average_impl(dpwa_learner *l, void *flat, double loss, const double *
             fa.dtype = l->dtype;
         }
     }
-    if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
-    const LaunchTiming *timing = nullptr;
-    if (l->timing_armed && l->timing_used < (int)l->timing.size() && ((uintptr_t)flat & 15) == 0)
-        timing = &l->timing[l->timing_used++];
+    if (l->relay_deferred && (((uintptr_t)flat | (uintptr_t)snap) & 15) == 0) {
+        // the relay's phase 2 fused into the average: stripes read where phase 1 left them
+        const RelayArgs &a = l->relay_saved;
+        fa.hdr = (const dpwa_header *)(a.slots[l->relay_saved_pick] + a.slot_off);
+        HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));
+        const LaunchTiming *timing = nullptr;
+        if (l->timing_armed && l->timing_used < (int)l->timing.size())
+            timing = &l->timing[l->timing_used++];
+        HIP_TRY(launch_average_relay(l->dtype, flat, l->n, fa, snap, a, l->relay_saved_pick, s, timing));
+        HIP_TRY(hipEventRecord(l->ev_relay, s));   // the next round's barrier waits for these reads
+        l->relay_pending = true;
+        l->relay_deferred = false;
+    } else {
+        int rc = relay_materialize(l);
+        if (rc) return rc;
+        if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
+        const LaunchTiming *timing = nullptr;
+        if (l->timing_armed && l->timing_used < (int)l->timing.size() && ((uintptr_t)flat & 15) == 0)
+            timing = &l->timing[l->timing_used++];
+        HIP_TRY(launch_average(l->dtype, flat, l->src + kPayloadOff, l->n, fa, snap, s, timing));
+        HIP_TRY(staging_read(l, s));
+    }
     l->timing_armed = false;
-    HIP_TRY(launch_average(l->dtype, flat, l->src + kPayloadOff, l->n, fa, snap, s, timing));
-    HIP_TRY(staging_read(l, s));
     l->consume_stream = s;
     l->consumed_once = true;
     l->cur = (l->cur + 1) & 3;
@@ -1169,14 +1195,9 @@ int dpwa_learner_relay_phase1(dpwa_learner *l, const int32_t *picks_dev, uint64_
     return DPWA_OK;
 }
 
-int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_pick, uint64_t version, int blocks)
+// Phase 2 on the side stream: my_pick's stripes gathered into staging.
+static int relay_phase2_now(dpwa_learner *l, const RelayArgs &a, int my_pick, int blocks)
 {
-    if (!l || !l->relay_on || !picks_dev || blocks < 1)
-        return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_phase2: bad arguments");
-    RelayArgs a;
-    int rc = relay_args(l, picks_dev, version, a);
-    if (rc) return rc;
-    DeviceGuard dg(l->device);
     if (my_pick >= 0 && l->consumed_once && l->consume_stream) {   // WAR on staging
         HIP_TRY(hipEventRecord(l->ev_consumed, l->consume_stream));
         HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
@@ -1185,8 +1206,41 @@ int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_
     HIP_TRY(launch_relay(2, a, blocks, l->side));
     HIP_TRY(hipEventRecord(l->ev_relay, l->side));
     l->relay_pending = true;
-    if (my_pick >= 0) {
+    if (my_pick >= 0) HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
+    return DPWA_OK;
+}
+
+// A deferred phase 2 whose fetch is consumed other than by the fused average (the split
+// update_wait, a copy of the payload, an unaligned buffer): gather into staging now.  The side
+// stream is still ordered after phase 1 and the round's barrier.
+static int relay_materialize(dpwa_learner *l)
+{
+    if (!l->relay_deferred) return DPWA_OK;
+    l->relay_deferred = false;
+    return relay_phase2_now(l, l->relay_saved, l->relay_saved_pick, l->relay_saved_blocks);
+}
+
+int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_pick, uint64_t version, int blocks,
+                              int fuse)
+{
+    if (!l || !l->relay_on || !picks_dev || blocks < 1 || my_pick >= l->relay_world || my_pick == l->relay_rank)
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_relay_phase2: bad arguments");
+    RelayArgs a;
+    int rc = relay_args(l, picks_dev, version, a);
+    if (rc) return rc;
+    DeviceGuard dg(l->device);
+    l->relay_deferred = false;
+    if (fuse && my_pick >= 0) {
+        // everything the fused average needs is on the side stream now (phase 1, the barrier)
         HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
+        l->relay_saved = a;
+        l->relay_saved_pick = my_pick;
+        l->relay_saved_blocks = blocks;
+        l->relay_deferred = true;
+    } else if (!fuse || my_pick >= 0) {
+        if ((rc = relay_phase2_now(l, a, my_pick, blocks))) return rc;
+    }
+    if (my_pick >= 0) {
         l->src = l->staging;
         l->src_copied = true;
         l->src_stage = 0;
@@ -1289,6 +1343,8 @@ int dpwa_learner_wait_fetch(dpwa_learner *l, dpwa_stream_t stream)
     if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_wait_fetch: NULL learner");
     if (l->have_fetch && l->src_copied) {
         DeviceGuard dg(l->device);
+        int rc = relay_materialize(l);
+        if (rc) return rc;
         HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, l->ev_fetched, 0));
     }
     return DPWA_OK;
@@ -1325,6 +1381,8 @@ int dpwa_learner_copy_fetched(dpwa_learner *l, void *dst_dev, dpwa_stream_t stre
     if (!l->have_fetch || !l->src) return set_error(DPWA_ERR_STATE, "dpwa_learner_copy_fetched: no fetch in flight");
     DeviceGuard dg(l->device);
     hipStream_t s = (hipStream_t)stream;
+    int rc = relay_materialize(l);
+    if (rc) return rc;
     if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));
     if (l->payload_bytes)
         HIP_TRY(hipMemcpyAsync(dst_dev, l->src + kPayloadOff, l->payload_bytes, hipMemcpyDeviceToDevice, s));
@@ -1336,6 +1394,7 @@ int dpwa_learner_copy_fetched(dpwa_learner *l, void *dst_dev, dpwa_stream_t stre
 int dpwa_learner_cancel(dpwa_learner *l)
 {
     if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_cancel: NULL learner");
+    l->relay_deferred = false;   // nothing reads the stripes: no gather
     finish_fetch(l);
     return DPWA_OK;
 }

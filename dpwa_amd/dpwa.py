@@ -27,6 +27,7 @@ from .learner import DTYPES, Learner, loss_args
 from .sched import Scheduler, seed_key
 
 LOGGER = logging.getLogger(__name__)
+RELAY_PULLS = ("relay", "relay-avg")   # DistGroup's multi-link transports (dpwa_amd/group.py)
 
 
 class Struct:
@@ -443,7 +444,7 @@ class DpwaConnection:
         h = ctypes.c_void_p()
         _lib.call("dpwa_node_handles", self._node, ctypes.byref(h), None)
         self._learner = Learner(parameters.device, parameters.numel(), parameters.dtype, handle=h.value)
-        if self._pull.partition(":")[0] == "relay":
+        if self._pull.partition(":")[0] in RELAY_PULLS:
             if not hasattr(self._group, "relay_blocks"):
                 raise ValueError("the relay pull needs a DistGroup (one learner per rank)")
             self._group.relay_blocks = 1     # allocate + exchange the relay buffers in on_bind
@@ -453,21 +454,25 @@ class DpwaConnection:
 
     def set_pull(self, mode):
         """Transport of copying fetches: 'copy' (hipMemcpyAsync on the side stream),
-        'kernel[:blocks]' (pull kernel) or 'relay[:blocks]' (DistGroup only, multi-link
-        two-phase relay; the connection must have been created with pull='relay' so the
-        relay buffers exist).  Every rank must switch between the same two rounds."""
+        'kernel[:blocks]' (pull kernel), 'relay[:blocks]' (DistGroup only, multi-link
+        two-phase relay; the connection must have been created with a relay pull so the
+        relay buffers exist) or 'relay-avg[:blocks]' (the same relay with its second phase
+        fused into the average: the averaging kernel reads the peer's stripes where the first
+        phase left them).  Every rank must switch between the same two rounds."""
         kind, _, blocks = mode.partition(":")
-        if kind not in ("copy", "kernel", "relay"):
-            raise ValueError("pull must be 'copy', 'kernel[:blocks]' or 'relay[:blocks]', got %r" % mode)
+        if kind not in ("copy", "kernel") + RELAY_PULLS:
+            raise ValueError("pull must be 'copy', 'kernel[:blocks]', 'relay[:blocks]' or 'relay-avg[:blocks]', "
+                             "got %r" % mode)
         self._pull = mode
         learner = self._learner
         if learner is None:
             return
         torch.cuda.synchronize(learner.device)
-        if kind == "relay":
+        if kind in RELAY_PULLS:
             if not getattr(self._group, "relay_ready", False):
                 raise ValueError("relay pull: create the connection with pull='relay' under a DistGroup")
             self._group.relay_blocks = int(blocks or 64)
+            self._group.relay_fused = kind == "relay-avg"
             self._flags |= _lib.FLAG_PICK_ONLY
             return
         if getattr(self._group, "relay_blocks", 0):

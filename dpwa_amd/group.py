@@ -181,6 +181,7 @@ class DistGroup:
         self._flag = None
         self.relay_blocks = 0        # > 0: relay transport (set by the connection's pull mode)
         self.relay_ready = False     # relay buffers allocated and exchanged
+        self.relay_fused = False     # phase 2 read by the averaging kernel itself (pull "relay-avg")
         self._picks = None
         self._pick = None
 
@@ -295,7 +296,7 @@ class DistGroup:
             self._side.synchronize()
             self.dist.barrier(group=self.pg)
         _lib.call("dpwa_learner_relay_phase2", learner._h, self._picks.data_ptr(), pick, version,
-                  self.relay_blocks)
+                  self.relay_blocks, 1 if self.relay_fused else 0)
 
 
 class AsyncDistGroup(DistGroup):
@@ -314,7 +315,7 @@ class AsyncDistGroup(DistGroup):
         self.publish_timeout_ms = int(publish_timeout_ms if publish_timeout_ms is not None else 600_000)
 
     def on_bind(self, conn):
-        if getattr(conn, "_pull", "copy").partition(":")[0] == "relay" or self.relay_blocks:
+        if getattr(conn, "_pull", "copy").partition(":")[0] in ("relay", "relay-avg") or self.relay_blocks:
             raise ValueError("the relay pull needs lock-step rounds (DistGroup), not free-running ones")
         board = ctypes.c_void_p()
         bname = None

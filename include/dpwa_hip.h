@@ -215,7 +215,11 @@ int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *pay
  * fetch in flight (my_pick = rank averaged with, -1 none).  Both phases run on the learner's
  * side stream; picks_dev holds `world` int32 on this learner's device.
  * relay_wait makes `stream` wait for the previous round's relay work (call before the next
- * round's collective, so a slot or relay buffer is rewritten only after every reader). */
+ * round's collective, so a slot or relay buffer is rewritten only after every reader).
+ * phase2 with fuse != 0 gathers nothing yet: the next dpwa_learner_average(_through) reads the
+ * peer's stripes where phase 1 left them (one kernel instead of the gather + the average; the
+ * average's stream then carries the round's last reads of other ranks' relay buffers); any
+ * other use of the fetch (the split factor/lerp, copy_fetched, wait_fetch) gathers first. */
 int dpwa_learner_relay_enable(dpwa_learner *l, int world, int rank);
 int dpwa_learner_relay_handle(dpwa_learner *l, void *handle_out, int64_t handle_len);
 int dpwa_learner_relay_attach(dpwa_learner *l, int rank, int peer_id, const void *relay_handle,
@@ -226,7 +230,7 @@ int dpwa_learner_relay_wait(dpwa_learner *l, dpwa_stream_t stream);
 int dpwa_learner_relay_phase1(dpwa_learner *l, const int32_t *picks_dev, uint64_t version, int blocks,
                               dpwa_stream_t stream);
 int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_pick, uint64_t version,
-                              int blocks);
+                              int blocks, int fuse);
 /* Kernel timing for measurement.  time_averages allocates `capacity` begin/end event pairs
  * (0 frees them; synchronises the device).  After arm_timing, the next averaging launch
  * (average / average_through, 16-B aligned parameters) goes through hipExtLaunchKernelGGL

@@ -30,7 +30,10 @@ def free_port():
                                                        (3, "clock", 0.7, 0.0, "kernel"),
                                                        (2, "clock", 1.0, 0.0, "relay:8"),
                                                        (3, "loss", 0.7, 0.5, "relay"),
-                                                       (4, "clock", 0.6, 0.0, "relay:16")])
+                                                       (4, "clock", 0.6, 0.0, "relay:16"),
+                                                       (2, "clock", 1.0, 0.0, "relay-avg:8"),
+                                                       (3, "loss", 0.7, 0.5, "relay-avg"),
+                                                       (4, "clock", 0.6, 0.0, "relay-avg:16")])
 def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100_003, dtype="f32"):
     T = 12
     names = ["r%d" % i for i in range(world)]
@@ -52,7 +55,8 @@ def test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100
 
 @pytest.mark.parametrize("world,interp,fp,thr,pull", [(2, "clock", 1.0, 0.0, "copy"),
                                                        (3, "loss", 0.7, 0.5, "kernel:64"),
-                                                       (3, "clock", 0.8, 0.0, "relay:8")])
+                                                       (3, "clock", 0.8, 0.0, "relay:8"),
+                                                       (3, "clock", 0.8, 0.0, "relay-avg:8")])
 def test_ipc_gossip_bf16_matches_oracle(tmp_path, world, interp, fp, thr, pull):
     """bf16 through every pull (BASELINE configs[3-4] dtype) with an odd element count: the
     payload (2n bytes) is not a multiple of the 16-byte vector, so the copy engine, the pull
@@ -61,7 +65,7 @@ def test_ipc_gossip_bf16_matches_oracle(tmp_path, world, interp, fp, thr, pull):
     test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100_003, dtype="bf16")
 
 
-@pytest.mark.parametrize("pull", ["copy", "relay:64"])
+@pytest.mark.parametrize("pull", ["copy", "relay:64", "relay-avg:64"])
 def test_ipc_gossip_configs2_full_size(tmp_path, pull):
     """BASELINE configs[2] at its own size and interpolation through the multi-process path:
     100,000,000 fp32 per rank, clock interpolation, lock-step rounds over IPC-mapped slots
@@ -85,6 +89,7 @@ def test_ipc_gossip_configs2_full_size(tmp_path, pull):
 
 
 @pytest.mark.parametrize("n,interp,fp,thr,pull", [(1_000_000_000, "loss", 1.0, 0.5, "relay:128"),
+                                                  (1_000_000_000, "loss", 1.0, 0.5, "relay-avg:128"),
                                                   (7_000_000_000, "constant", 0.7, 0.0, "copy"),
                                                   (7_000_000_000, "constant", 0.7, 0.0, "kernel:512")])
 def test_ipc_gossip_configs3_4_full_size(tmp_path, n, interp, fp, thr, pull):
@@ -113,7 +118,7 @@ def test_ipc_gossip_configs3_4_full_size(tmp_path, n, interp, fp, thr, pull):
         assert olerp.bits_equal(got["params"], exp["params"][:, r]), r
 
 
-@pytest.mark.parametrize("pull", ["relay:8", "kernel"])
+@pytest.mark.parametrize("pull", ["relay:8", "relay-avg:8", "kernel"])
 def test_ipc_gossip_six_ranks(tmp_path, monkeypatch, pull):
     """Six ranks (the relay's stripes over more than four peers).  Six processes on one card
     oversubscribe its hardware queues with the default 4 per process, so the children get 2."""
@@ -121,12 +126,14 @@ def test_ipc_gossip_six_ranks(tmp_path, monkeypatch, pull):
     test_ipc_gossip_matches_oracle(tmp_path, 6, "clock", 0.8, 0.0, pull, n=65_537)
 
 
-def test_relay_tiny_payload(tmp_path):
-    """5 parameters over 4 ranks: one 32-B stripe, three empty ones."""
-    test_ipc_gossip_matches_oracle(tmp_path, 4, "constant", 1.0, 0.0, "relay:2", n=5)
+@pytest.mark.parametrize("pull", ["relay:2", "relay-avg:2"])
+def test_relay_tiny_payload(tmp_path, pull):
+    """5 parameters over 4 ranks: one stripe holding all 20 bytes, three empty ones (the fused
+    form reads one 16-B item and a one-element ragged tail from that stripe)."""
+    test_ipc_gossip_matches_oracle(tmp_path, 4, "constant", 1.0, 0.0, pull, n=5)
 
 
-@pytest.mark.parametrize("pull", ["copy", "relay:8"])
+@pytest.mark.parametrize("pull", ["copy", "relay:8", "relay-avg:8"])
 def test_ipc_gossip_with_injected_faults(tmp_path, pull):
     """Remote peers marked slow (timeouts), down (refused) or dead (removed) steer the
     native scheduler exactly as the reference's TxThread: checked against the oracle fed
@@ -175,7 +182,8 @@ def test_ipc_gossip_with_injected_faults(tmp_path, pull):
 
 
 @pytest.mark.parametrize("world,interp,fp,thr,pull", [(2, "clock", 1.0, 0.0, "copy"), (3, "loss", 0.7, 0.5, "kernel:64"),
-                                                       (3, "clock", 0.8, 0.0, "relay:8")])
+                                                       (3, "clock", 0.8, 0.0, "relay:8"),
+                                                       (3, "clock", 0.8, 0.0, "relay-avg:8")])
 def test_ipc_gossip_vmm_shared_slots(tmp_path, monkeypatch, world, interp, fp, thr, pull):
     """DPWA_VMM=1: the snapshot slots (and relay buffers) are hipMemCreate chunks shared as fds
     over a Unix socket -- the form every allocation of 1.5 GiB and more takes, since

@@ -20,8 +20,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
-TRANSPORTS = ["lockstep/copy", "lockstep/kernel:256", "lockstep/relay:32", "async/copy", "async/kernel:256",
-              "async/copy+wt", "async/kernel:256+wt"]
+TRANSPORTS = ["lockstep/copy", "lockstep/kernel:256", "lockstep/relay:32", "lockstep/relay-avg:32", "async/copy",
+              "async/kernel:256", "async/copy+wt", "async/kernel:256+wt"]
 
 
 def free_port():
