@@ -246,6 +246,9 @@ template <int POLICY> struct LerpPolicy {
 // read in place).  StripeSrc: the relay's stripes, stripe s at src[s] (k_lerp_relay).
 struct ContigSrc {
     const char *p;
+    // byte offset of workgroup b's span: spans in order
+    template <int SPAN>
+    __device__ __forceinline__ int64_t span_of(uint32_t b) const { return (int64_t)b * SPAN; }
     // base such that base + byte_offset addresses the span starting at span_off
     __device__ __forceinline__ const char *span_base(int64_t) const { return p; }
     __device__ __forceinline__ const char *at(int64_t byte) const { return p + byte; }
@@ -254,6 +257,15 @@ struct ContigSrc {
 struct StripeSrc {
     const char *src[kMaxRelayRanks];
     int64_t stripe;    // a multiple of every span (4 KiB multiple): no span straddles stripes
+    int32_t parts;     // stripes (ranks)
+    // Consecutive workgroups take consecutive stripes (b % parts), so the workgroups in flight
+    // at any moment read from every stripe holder -- every xGMI link -- at once, not one
+    // stripe (one link) after another.
+    template <int SPAN>
+    __device__ __forceinline__ int64_t span_of(uint32_t b) const
+    {
+        return (int64_t)(b % (uint32_t)parts) * stripe + (int64_t)(b / (uint32_t)parts) * SPAN;
+    }
     __device__ __forceinline__ const char *span_base(int64_t span_off) const
     {
         const int64_t s = span_off / stripe;
@@ -276,7 +288,7 @@ __device__ __forceinline__ void lerp_span(typename Ops::V *__restrict__ param, c
     using V = typename Ops::V;
     constexpr int SPAN = BLOCK * 16;
     const int64_t nv = n / Ops::PER;
-    const int64_t span_off = (int64_t)blockIdx.x * SPAN;
+    const int64_t span_off = src.template span_of<SPAN>(blockIdx.x);
     const int lane_off = threadIdx.x * 16;
     const __amdgpu_buffer_rsrc_t rq = span_rsrc<SPAN>(src.span_base(span_off), span_off, nv * 16);
     const __amdgpu_buffer_rsrc_t rp = span_rsrc<SPAN>(param, span_off, nv * 16);
@@ -503,7 +515,8 @@ template <class Ops, bool DUAL>
 static void launch_relay_kernel(void *param, int64_t n, const LerpArgs &args, const StripeSrc &src, hipStream_t s,
                                 const LaunchTiming *timing)
 {
-    const int64_t g = (n / Ops::PER) / kStreamBlock + 1;
+    // every span of every stripe (the spans past the payload are range-checked away)
+    const int64_t g = (int64_t)src.parts * (src.stripe / (kStreamBlock * 16));
     if (timing)
         hipExtLaunchKernelGGL((k_lerp_relay<Ops, DUAL>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s, timing->start,
                               timing->stop, 0, (typename Ops::V *)param, n, args, src);
@@ -527,6 +540,7 @@ hipError_t launch_average_relay(int32_t dtype, void *param, int64_t n, const Fus
                                    : a.relays[r] + (int64_t)j * a.stripe;
     for (int r = a.world; r < kMaxRelayRanks; ++r) src.src[r] = nullptr;
     src.stripe = a.stripe;
+    src.parts = a.world;
     LerpArgs args{};
     args.fused = fa;
     args.snap = snap;
@@ -624,13 +638,15 @@ hipError_t launch_pull(void *dst, const void *src, int64_t nbytes, int max_block
 // from rank s's relay buffer, from its own relay buffer for s == r (local HBM) and from j
 // itself for s == j.  Every pair's xGMI link then carries at most one stripe per phase
 // instead of one link carrying the whole snapshot.
-// blockIdx.y selects the source (phase 1) or the stripe (phase 2); blockIdx.x strides it.
+// blockIdx.x selects the source (phase 1) or the stripe (phase 2) and blockIdx.y strides it:
+// consecutive workgroups (the dispatch order) take different sources, so every link is busy
+// from the start even when the grid exceeds what is resident at once.
 __global__ void k_release_system();
 
 __device__ __forceinline__ void copy16(u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, int64_t n16)
 {
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.y * kBlock;
+    int64_t i = (int64_t)blockIdx.y * kBlock + threadIdx.x;
     for (; i + 3 * stride < n16; i += 4 * stride) {
         u32x4 v0 = src[i], v1 = src[i + stride], v2 = src[i + 2 * stride], v3 = src[i + 3 * stride];
         dst[i] = v0;
@@ -650,7 +666,7 @@ __device__ __forceinline__ int64_t stripe_len(int s, int64_t stripe, int64_t pay
 
 __global__ __launch_bounds__(kBlock) void k_relay_phase1(RelayArgs a)
 {
-    const int j = blockIdx.y;
+    const int j = blockIdx.x;
     if (j == a.rank) return;
     bool active = false;                                   // does any rank (me included) need j?
     for (int i = 0; i < a.world; ++i) active |= (a.picks[i] == j);
@@ -665,8 +681,8 @@ __global__ __launch_bounds__(kBlock) void k_relay_phase2(RelayArgs a)
 {
     const int j = a.picks[a.rank];
     if (j < 0) return;
-    const int s = blockIdx.y;
-    if (s == 0 && blockIdx.x == 0 && threadIdx.x < 16)     // the 256-B header, straight from j
+    const int s = blockIdx.x;
+    if (s == 0 && blockIdx.y == 0 && threadIdx.x < 16)     // the 256-B header, straight from j
         reinterpret_cast<u32x4 *>(a.staging)[threadIdx.x] =
             reinterpret_cast<const u32x4 *>(a.slots[j] + a.slot_off)[threadIdx.x];
     const int64_t len = stripe_len(s, a.stripe, a.payload);
@@ -679,7 +695,7 @@ __global__ __launch_bounds__(kBlock) void k_relay_phase2(RelayArgs a)
 hipError_t launch_relay(int phase, const RelayArgs &a, int blocks_per_part, hipStream_t s)
 {
     if (a.world < 1 || a.world > kMaxRelayRanks || (a.stripe & 15) || (a.payload & 15)) return hipErrorInvalidValue;
-    dim3 grid((uint32_t)blocks_per_part, (uint32_t)a.world);
+    dim3 grid((uint32_t)a.world, (uint32_t)blocks_per_part);
     hipLaunchKernelGGL(k_acquire_system, dim3(256), dim3(64), 0, s);   // both phases read peers
     if (phase == 1) {   // the relay buffer is read by other GPUs: write it back from the L2s
         hipLaunchKernelGGL(k_relay_phase1, grid, dim3(kBlock), 0, s, a);
