@@ -49,9 +49,12 @@ struct LaunchTiming {
     hipEvent_t start, stop;
 };
 
-// Fused factor + lerp (one launch); a non-null `snap` also receives the result.
+// Fused factor + lerp (one launch); a non-null `snap` also receives the result.  `reverse`:
+// the workgroups take the spans from the end of the buffer backwards (same bytes, same
+// results; what a pass reads first is then what the previous pass in the other direction
+// wrote last).
 hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa,
-                          void *snap, hipStream_t s, const LaunchTiming *timing = nullptr);
+                          void *snap, hipStream_t s, const LaunchTiming *timing = nullptr, bool reverse = false);
 
 // Factor + clock only (one thread).
 hipError_t launch_factor(const FusedArgs &fa, hipStream_t s);
