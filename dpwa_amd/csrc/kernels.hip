@@ -192,7 +192,6 @@ struct LerpArgs {
     const dpwa_coef *coef;       // COEF_DEV
     FusedArgs fused;             // COEF_FUSED
     void *snap;                  // DUAL: second destination (the next snapshot's payload)
-    int32_t reverse;             // spans in descending order (see launch_average)
 };
 
 // ---------------------------------------------------------------- streaming buffer access
@@ -289,7 +288,7 @@ __device__ __forceinline__ void lerp_span(typename Ops::V *__restrict__ param, c
     using V = typename Ops::V;
     constexpr int SPAN = BLOCK * 16;
     const int64_t nv = n / Ops::PER;
-    const int64_t span_off = src.template span_of<SPAN>(args.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x);
+    const int64_t span_off = src.template span_of<SPAN>(blockIdx.x);
     const int lane_off = threadIdx.x * 16;
     const __amdgpu_buffer_rsrc_t rq = span_rsrc<SPAN>(src.span_base(span_off), span_off, nv * 16);
     const __amdgpu_buffer_rsrc_t rp = span_rsrc<SPAN>(param, span_off, nv * 16);
@@ -502,12 +501,11 @@ hipError_t launch_lerp(int32_t dtype, void *param, const void *peer, int64_t n, 
 }
 
 hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa, void *snap,
-                          hipStream_t s, const LaunchTiming *timing, bool reverse)
+                          hipStream_t s, const LaunchTiming *timing)
 {
     LerpArgs args{};
     args.fused = fa;
     args.snap = snap;
-    args.reverse = reverse ? 1 : 0;
     return launch_any(dtype, COEF_FUSED, param, peer, n, args, s, timing);
 }
 

@@ -49,12 +49,9 @@ struct LaunchTiming {
     hipEvent_t start, stop;
 };
 
-// Fused factor + lerp (one launch); a non-null `snap` also receives the result.  `reverse`:
-// the workgroups take the spans from the end of the buffer backwards (same bytes, same
-// results; what a pass reads first is then what the previous pass in the other direction
-// wrote last).
+// Fused factor + lerp (one launch); a non-null `snap` also receives the result.
 hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa,
-                          void *snap, hipStream_t s, const LaunchTiming *timing = nullptr, bool reverse = false);
+                          void *snap, hipStream_t s, const LaunchTiming *timing = nullptr);
 
 // Factor + clock only (one thread).
 hipError_t launch_factor(const FusedArgs &fa, hipStream_t s);

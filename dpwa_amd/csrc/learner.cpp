@@ -367,7 +367,6 @@ struct dpwa_learner {
     // are read where phase 1 left them by the next fused average, or gathered into staging
     // first if the fetch is consumed any other way (relay_materialize)
     bool relay_deferred = false;
-    bool reverse_next = false;    // direction of the next average's pass (alternating, see below)
     RelayArgs relay_saved{};
     int relay_saved_pick = -1, relay_saved_blocks = 0;
     // host readers of published slots (wire bridge) run on other threads
@@ -965,15 +964,7 @@ static int average_impl(dpwa_learner *l, void *flat, double loss, const double *
         const LaunchTiming *timing = nullptr;
         if (l->timing_armed && l->timing_used < (int)l->timing.size() && ((uintptr_t)flat & 15) == 0)
             timing = &l->timing[l->timing_used++];
-        // DPWA_LERP_ALTERNATE=1: consecutive averages of this learner sweep the buffer in
-        // opposite directions (tuning)
-        static const bool alternate = [] {
-            const char *e = getenv("DPWA_LERP_ALTERNATE");
-            return e && atoi(e) == 1;
-        }();
-        const bool reverse = alternate && l->reverse_next;
-        l->reverse_next = !l->reverse_next;
-        HIP_TRY(launch_average(l->dtype, flat, l->src + kPayloadOff, l->n, fa, snap, s, timing, reverse));
+        HIP_TRY(launch_average(l->dtype, flat, l->src + kPayloadOff, l->n, fa, snap, s, timing));
         HIP_TRY(staging_read(l, s));
     }
     l->timing_armed = false;

@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B of DPWA_LERP_ALTERNATE (consecutive averages of a learner sweep in opposite directions)
-# on the default bench loop, interleaved, plus the gossip tests with it on.
+# A/B of a sweep-direction knob (DPWA_LERP_ALTERNATE, since removed): consecutive
+# averages of a learner sweeping in opposite directions.  Kept as the record of that experiment.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
