@@ -167,3 +167,18 @@ def test_gpu_key_places_the_node(tmp_path):
     with pytest.raises(ValueError, match="gpu 1"):
         conn.update_send(torch.zeros(4, device="meta"), 1.0)
     conn.close()
+
+
+def test_pull_modes_are_validated_before_binding(tmp_path):
+    """set_pull accepts the transports DistGroup and the board offer (copy, kernel, relay,
+    relay-avg, each with an optional block count) and refuses anything else; nothing touches
+    the GPU before the connection is bound."""
+    from dpwa_amd.launch import write_config
+    cfg = write_config(str(tmp_path / "p.yaml"), ["a", "b"], interpolation="constant")
+    conn = DpwaConnection("a", cfg, group=LocalGroup())
+    for mode in ("copy", "kernel", "kernel:256", "relay", "relay:32", "relay-avg", "relay-avg:128"):
+        conn.set_pull(mode)
+        assert conn._pull == mode
+    for bad in ("rccl", "relay_avg", "push:32", ""):
+        with pytest.raises(ValueError, match="relay-avg"):
+            conn.set_pull(bad)
