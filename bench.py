@@ -947,6 +947,17 @@ def main():
                         "side-stream events around each copying fetch (mean over ranks; null for the relay); "
                         "peak = MI355X xGMI spec per link, both directions together",
             }
+            if sel_mode.startswith("relay"):
+                # every directed link carries at most one stripe per phase, two per round
+                link_bytes = 2 * ((args.numel * esize + 15) // 16 * 16) // world
+                out["xgmi"]["relay"] = {
+                    "bytes_per_link_per_round": link_bytes,
+                    "round_us": round(1e6 * elapsed / args.steps, 2),
+                    "achieved_gbs_per_link_direction": round(link_bytes / (elapsed / args.steps) / 1e9, 1),
+                    "peak_link_gbs_per_direction": XGMI_LINK_GBS / 2,
+                    "note": "the relay's busiest directed link per round over the whole round's time "
+                            "(barriers and the average included): a lower bound on the link rate",
+                }
         if secondary is not None:
             s_wt, (w_el, w_avg, w_rounds, (w_ms, _)) = secondary
             w_us = float(np.nanmean(w_ms) * 1e3)
