@@ -65,6 +65,9 @@ def main(argv=None):
     ap.add_argument("--interpolation", default="constant")
     ap.add_argument("--gossip", default="async", choices=["lockstep", "async"],
                     help="under torchrun: lock-step rounds (DistGroup) or free-running ones (gossip board)")
+    ap.add_argument("--pull", default=None,
+                    help="under torchrun: copy | kernel[:blocks] | relay[:blocks] | relay-avg[:blocks] "
+                         "(the relays need --gossip lockstep)")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -114,6 +117,8 @@ def main(argv=None):
         return time.perf_counter() - t0
 
     group = {"group": args.gossip} if world > 1 else {}
+    if world > 1 and args.pull:
+        group["pull"] = args.pull
     adapters = [DpwaPyTorchAdapter(nets[i], names[g], cfg, seed=100 + g, **group) for i, g in enumerate(mine)]
     run(args.warmup, False)
     run(args.warmup, True, adapters)
