@@ -44,6 +44,7 @@ import torch.distributed as dist  # noqa: E402
 
 XGMI_LINK_GBS = 153.6          # MI355X xGMI per link (spec, both directions)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_MEASURED_GBS = 6290.0      # the guide's measured HBM ceiling (float4 copy, MI355X_MICROARCH.md)
 RESNET18_NUMEL = 11_173_962    # examples/pytorch-cifar/models/resnet.py ResNet18
 REF_SAMPLE_MAX = 32_000_000    # cap on the reference-round CPU sample (elements)
 # BASELINE.json north_star sizes, each in its config's dtype (configs[1..4])
@@ -931,6 +932,9 @@ def main():
                             "is partly Infinity-Cache resident, so this live figure is warmer than the basis",
                 },
                 "traffic_source": traffic_src,
+                "vs_measured_ceiling": {"gbs": HBM_MEASURED_GBS, "frac": round(achieved / HBM_MEASURED_GBS, 4),
+                                        "source": "MI355X_MICROARCH.md: 6.29 TB/s measured for a float4 copy "
+                                                  "(79 % of the 8 TB/s spec); peak above stays the spec"},
             },
         }
         if pull_trials:
