@@ -928,8 +928,12 @@ def main():
                               + ", every %d-th step of the timed loop" % args.sample_every,
                     "event_bracket_us": (round(float(np.nanmean(bracket_ms) * 1e3), 2)
                                          if args.timing != "dispatch" else None),
-                    "note": "inside the gossip round the peer snapshot was written just before the average and "
-                            "is partly Infinity-Cache resident, so this live figure is warmer than the basis",
+                    "note": ("inside the gossip round the peer snapshot was written just before the average and "
+                             "is partly Infinity-Cache resident, so this live figure is warmer than the basis"
+                             if world == 1 else
+                             "the averaging kernel of the timed rounds: it reads the staged peer snapshot (copy / "
+                             "kernel / relay pulls) or, under relay-avg, the peer's stripes over xGMI itself, so "
+                             "there it is link-bound and its bytes are not all HBM bytes"),
                 },
                 "traffic_source": traffic_src,
                 "vs_measured_ceiling": {"gbs": HBM_MEASURED_GBS, "frac": round(achieved / HBM_MEASURED_GBS, 4),
