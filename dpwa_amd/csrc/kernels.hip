@@ -236,10 +236,14 @@ __device__ __forceinline__ void span_store(__amdgpu_buffer_rsrc_t r, int lane_of
 // policy; the result is stored `sc1`, with bit 2 `sc0 sc1`, with bit 4 `nt sc1`.
 template <int POLICY> struct LerpPolicy {
     static constexpr int param_load = (POLICY & 1) ? 0 : kAuxStream;
-    static constexpr int snap_store = kAuxStore | ((POLICY & 2) ? 1 : 0) | ((POLICY & 4) ? kAuxStream : 0);
+    static constexpr int base_store = kAuxStore | ((POLICY & 2) ? 1 : 0) | ((POLICY & 4) ? kAuxStream : 0);
+    // bit 16: only the next snapshot is stored `nt` (a co-resident peer reads it two averages
+    // later; this learner's parameters, re-read by its next average one average later, keep
+    // the Infinity Cache)
+    static constexpr int snap_store = base_store | ((POLICY & 16) ? kAuxStream : 0);
     // bit 8: the parameters (re-read only two averages later, past the Infinity Cache's
     // reach) are stored `nt`, leaving the cache to the snapshot the peer reads next
-    static constexpr int store = snap_store | ((POLICY & 8) ? kAuxStream : 0);
+    static constexpr int store = base_store | ((POLICY & 8) ? kAuxStream : 0);
 };
 
 // Where the peer's bytes are.  ContigSrc: one buffer (a staging buffer, or a peer's slot
@@ -434,7 +438,7 @@ static int lerp_policy()
     static const int forced = [] {
         const char *e = getenv("DPWA_LERP_POLICY");
         const int p = e ? atoi(e) : 0;
-        return (p >= 0 && p <= 15) ? p : 0;
+        return (p >= 0 && p <= 31) ? p : 0;
     }();
     return forced;
 }
@@ -454,6 +458,7 @@ static hipError_t launch_mode(void *param, const void *peer, int64_t n, const Le
             case 5: return launch_blocks<Ops, MODE, DUAL, 64, 5>(param, peer, n, args, s, timing);
             case 8: return launch_blocks<Ops, MODE, DUAL, 64, 8>(param, peer, n, args, s, timing);
             case 9: return launch_blocks<Ops, MODE, DUAL, 64, 9>(param, peer, n, args, s, timing);
+            case 16: return launch_blocks<Ops, MODE, DUAL, 64, 16>(param, peer, n, args, s, timing);
             default: return launch_blocks<Ops, MODE, DUAL, 64>(param, peer, n, args, s, timing);
             }
         case 128: return launch_blocks<Ops, MODE, DUAL, 128>(param, peer, n, args, s, timing);
