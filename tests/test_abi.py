@@ -56,3 +56,17 @@ def test_no_gpu_fails_loudly():
     from dpwa_amd.interpolation import ConstantInterpolation
     with pytest.raises(_lib.DpwaError):
         Learner(torch.device("cuda", 0), 16, torch.float32, ConstantInterpolation(0.5).device_config(0.0))
+
+
+def test_binding_arity_matches_header_declarations():
+    """Every entry point's ctypes argument list has as many entries as its declaration in
+    include/dpwa_hip.h has parameters (a signature changed on one side only would pass the
+    symbol check and then misread its arguments)."""
+    text = re.sub(r"/\*.*?\*/", "", open(_lib.HEADER_PATH).read(), flags=re.S)
+    decls = re.findall(r"\b(?:int|int32_t|void|const char \*)\s*\**(dpwa_\w+)\s*\(([^)]*)\)\s*;", text)
+    assert len(decls) >= 80
+    for name, params in decls:
+        params = params.strip()
+        count = 0 if params in ("", "void") else params.count(",") + 1
+        assert name in _lib.SIGNATURES, name
+        assert len(_lib.SIGNATURES[name]) == count, (name, count, len(_lib.SIGNATURES[name]))
