@@ -9,23 +9,30 @@ Workload (BASELINE.json configs[1]): a synthetic 11,173,962-element fp32 paramet
 vector (ResNet-18 size) per learner, N(0,1) data, constant interpolation 0.5,
 fetch_probability 1.
   * ``--gpus 1``: two learners co-resident on cuda:0 (the minimal non-degenerate gossip:
-    each averages with the other's snapshot, read in place from HBM).
-  * ``--gpus N`` (torchrun): one learner per GPU; peers' snapshot slots are mapped into each
-    process (hipIpc handles; fds of hipMemCreate chunks from 1.5 GiB up) and pulled over xGMI
-    on each learner's side stream.  Short trials of
-    lock-step rounds (RCCL barrier; copy / kernel / relay pulls) and free-running rounds
-    (gossip board) pick the transport of the timed run.  Per-GPU work is fixed -> "scaling":
-    "weak".  Every rank logs its phases to stderr (``[bench rN +s]``), so a multi-GPU run that
-    stops names the phase it stopped in.
+    each averages with the other's snapshot, read in place from HBM); both averages of a
+    round run as one batched dispatch (``DpwaConnection.update_wait_average_many``).
+  * ``--gpus N``: one learner per GPU, one process per GPU.  Under an external launcher
+    (``torch.distributed.run``, WORLD_SIZE set) every process is a rank; without one, this
+    script starts ``torch.distributed.run`` itself as a child process (before anything touches
+    a GPU), relays its output and exits with its code.  Peers' snapshot slots are mapped into
+    each process (hipIpc handles; fds of hipMemCreate chunks from 1.5 GiB up) and pulled over
+    xGMI on each learner's side stream.  Interleaved, wall-time-bounded trials of lock-step
+    rounds (RCCL barrier; copy / kernel / relay pulls) and free-running rounds (gossip board)
+    pick the transport of the timed run by the median rate.  Per-GPU work is fixed ->
+    "scaling": "weak".  Every rank logs its phases to stderr (``[bench rN +s]``).
 
 ``value`` = algorithmic averaged bytes (3 * numel * sizeof(dtype) per completed
 averaging) summed over all learners / the max-over-ranks wall time of the
-K timed steps.  ``roofline`` prices the lerp kernel alone from HIP events recorded around
-every lerp launch on the stream it runs on.  ``parity`` (at N>1 before the trials, so only verified transports are timed) checks every
-transport bit for bit against the oracle.  ``cpu_baseline`` times the reference's own CPU
-round restated (oracle/ref_round.py: two learner processes on localhost TCP, pickle framing,
-numpy fp32 lerp -- the path this one replaces) on the box's host cores before the GPU is
-touched, and beside it the C oracle's round (publish copy + averaging) on one host core.
+K timed steps, from a pass with no instrumentation.  ``roofline`` prices the averaging
+kernel alone, cold, per launch (dispatch begin/end events); ``roofline.in_loop`` times the same
+kernel inside the gossip loop in a separate sampled pass.  ``parity`` (at N>1 before the
+trials, so only verified transports are timed) checks every transport bit for bit against the
+oracle, each transport isolated (an error becomes ``false``, not a teardown), with a watchdog
+that prints a partial line and exits non-zero if a phase overruns.  ``cpu_baseline`` times the
+reference's own CPU round restated (oracle/ref_round.py: two learner processes on localhost
+TCP, pickle framing, numpy fp32 lerp -- the path this one replaces) on the box's host cores
+before the GPU is touched, and beside it the averaging arithmetic on the host (C oracle, numpy
+single thread, torch-CPU on every thread) at every north_star size.
 """
 import argparse
 import ctypes
@@ -33,6 +40,7 @@ import json
 import os
 import sys
 import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -47,8 +55,13 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_MEASURED_GBS = 6290.0      # the guide's measured HBM ceiling (float4 copy, MI355X_MICROARCH.md)
 RESNET18_NUMEL = 11_173_962    # examples/pytorch-cifar/models/resnet.py ResNet18
 REF_SAMPLE_MAX = 32_000_000    # cap on the reference-round CPU sample (elements)
+NUMPY_SAMPLE_MAX = 1_000_000_000   # numpy single-thread rows above this run on a bounded chunk
 # BASELINE.json north_star sizes, each in its config's dtype (configs[1..4])
 SWEEP = ((RESNET18_NUMEL, "f32"), (100_000_000, "f32"), (1_000_000_000, "bf16"), (7_000_000_000, "bf16"))
+METRIC = "pairwise-average GB/s (% HBM peak) + gossip rounds/s"
+# The cold streaming ceiling of the write-through kernel's access mix (2 reads : 2 writes) at
+# 11.17M fp32, per launch, measured by tools/stream_tune.hip (profiles/r02_stream_tune_11m.log).
+MIX_CEILING_11M = {"mix": "2R:2W", "frac": 0.759, "source": "profiles/r02_stream_tune_11m.log ('dual 64x1')"}
 
 
 _T0 = time.perf_counter()
@@ -60,7 +73,7 @@ def progress(msg):
     sys.stderr.flush()      # one write per line: ranks share the stream
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -74,6 +87,8 @@ def parse():
                     help="reported loss: 1.0, or SURVEY §8d C4's 2exp(-t/200)+0.05U (crosses a threshold)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-rows", action="store_true",
+                    help="skip the host averaging-arithmetic rows at every north_star size")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the sweeps over the north_star sizes (cold kernel, and whole rounds at N=1)")
@@ -83,32 +98,161 @@ def parse():
                          "or full (a 2*N*s snapshot copy every round); at N>1 free-running trials try both")
     ap.add_argument("--no-secondary", action="store_true", help="skip the run of the other publish form")
     ap.add_argument("--no-write-through", action="store_true", help="same as --publish full --no-secondary")
-    ap.add_argument("--sample-every", type=int, default=8,
-                    help="time the averaging kernel every k-th step (a timed launch costs a few µs)")
+    ap.add_argument("--no-batch", action="store_true",
+                    help="N=1: one averaging dispatch per learner instead of one batched dispatch per round")
+    ap.add_argument("--sample-every", type=int, default=4,
+                    help="in-loop kernel timing pass: time the averaging dispatch every k-th step")
     ap.add_argument("--timing", choices=["dispatch", "bracket", "both"], default="dispatch",
-                    help="averaging-kernel timing: its own dispatch events (hipExtLaunchKernelGGL), an event "
-                         "pair recorded around the launch, or both")
+                    help="averaging-kernel timing in the sampled pass: its own dispatch events "
+                         "(hipExtLaunchKernelGGL), an event pair recorded around the launch, or both")
     ap.add_argument("--streams", default="one", choices=["one", "per-learner"],
-                    help="stream per co-resident learner (their kernels may overlap) or one shared stream")
+                    help="stream per co-resident learner (their kernels may overlap; no batching) or one stream")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (gloo only to rehearse on one GPU)")
     ap.add_argument("--pull", default="auto",
                     help="N>1 fetch transport: copy (hipMemcpyAsync), kernel[:blocks], relay[:blocks] "
-                         "(two-phase multi-link), or auto (fastest of a short trial)")
+                         "(two-phase multi-link), or auto (median of interleaved trials)")
     ap.add_argument("--gossip", default="auto", choices=["auto", "lockstep", "async"],
                     help="N>1: lock-step rounds (DistGroup), free-running rounds (AsyncDistGroup, gossip "
-                         "board), or a short trial of both keeping the faster")
+                         "board), or trials of both keeping the faster")
+    ap.add_argument("--trial-ms", type=float, default=50.0,
+                    help="N>1: minimum wall time of one transport trial (and at least 30 rounds)")
+    ap.add_argument("--trial-passes", type=int, default=3, help="N>1: interleaved passes over the candidates")
     ap.add_argument("--compute-us", type=float, default=1000.0,
                     help="per-learner synthetic training step (bf16 GEMM loop) for the 'overlap' field; 0 = skip")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the parity leg (a short gossip through every transport, checked against the oracle)")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py over rocprofv3 FETCH_SIZE/WRITE_SIZE passes of "
-                         "tools/cold_sweep.py) to report; default profiles/traffic_r02_<publish form>.json")
-    args = ap.parse_args()
+                         "tools/cold_sweep.py) to report; default profiles/traffic_r03_<publish form>.json")
+    ap.add_argument("--phase-scale", type=float, default=1.0,
+                    help="multiplies every watchdog phase budget (slow rehearsals)")
+    ap.add_argument("--launch-timeout", type=float, default=3000.0,
+                    help="self-launch (N>1 without torchrun): seconds before the child job is stopped")
+    args = ap.parse_args(argv)
     if args.no_write_through:
         args.publish, args.no_secondary = "full", True
     return args
+
+
+def base_line(args, world):
+    """The keys every output line carries, the partial one included."""
+    return {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic N(0,1) flat parameter vectors (no dataset needed)"}
+
+
+# ---------------------------------------------------------------- robustness of the N>1 run
+def self_launch(args, argv):
+    """`--gpus N` (N > 1) without an external launcher: run torch.distributed.run as a CHILD
+    process (this process never touches a GPU and never re-execs), relay its stdout, and exit
+    with its code.  If the job ends without a result line, print one saying so."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + list(argv)
+    progress("self-launch: %s" % " ".join(cmd[1:]))
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, start_new_session=True)
+
+    def stop():
+        progress("self-launch: %.0f s limit reached, stopping the job" % args.launch_timeout)
+        for sig, wait in ((signal.SIGTERM, 15), (signal.SIGKILL, 0)):
+            try:
+                os.killpg(p.pid, sig)
+            except ProcessLookupError:
+                return
+            try:
+                p.wait(wait)
+                return
+            except subprocess.TimeoutExpired:
+                pass
+
+    timer = threading.Timer(args.launch_timeout, stop)
+    timer.daemon = True
+    timer.start()
+    got = False
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+        got = got or (line.lstrip().startswith("{") and '"metric"' in line)
+    rc = p.wait()
+    timer.cancel()
+    if not got:
+        out = base_line(args, args.gpus)
+        out["error"] = "torch.distributed.run exited with %d without a result line" % rc
+        print(json.dumps(out), flush=True)
+        rc = rc or 1
+    return rc
+
+
+class Watchdog:
+    """Per-rank deadline on the current phase.  When a phase overruns (a hung collective, a
+    stalled pull, a rank that died inside a collective), rank 0 prints the partial result line
+    (phase reached, parity so far, the phase's transport false), every rank dumps its threads,
+    and the process exits with status 3 -- so the job ends within the bound with a line."""
+
+    def __init__(self, args, world, rank):
+        self.args, self.world, self.rank = args, world, rank
+        self.phase, self.deadline = "start", None
+        self.parity = {}
+        self.transport = None
+        self._lock = threading.Lock()
+        t = threading.Thread(target=self._run, name="bench-watchdog", daemon=True)
+        t.start()
+
+    def enter(self, phase, seconds, transport=None):
+        with self._lock:
+            self.phase = phase
+            self.transport = transport
+            self.deadline = time.monotonic() + seconds * self.args.phase_scale
+        progress(phase)
+
+    def idle(self):
+        with self._lock:
+            self.deadline = None
+
+    def _run(self):
+        import faulthandler
+        while True:
+            time.sleep(1.0)
+            with self._lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                phase, transport = self.phase, self.transport
+            if not late:
+                continue
+            progress("WATCHDOG: phase '%s' overran its budget; exiting" % phase)
+            if self.rank == 0:
+                out = base_line(self.args, self.world)
+                out["error"] = "watchdog: phase '%s' overran its budget" % phase
+                out["phase"] = phase
+                parity = dict(self.parity)
+                if transport is not None:
+                    parity[transport] = False
+                out["parity"] = parity
+                sys.stdout.write(json.dumps(out) + "\n")
+                sys.stdout.flush()
+            faulthandler.dump_traceback(all_threads=True)
+            sys.stderr.flush()
+            os._exit(3)
+
+
+def injected(transport, rank, where):
+    """DPWA_BENCH_INJECT="<transport>@<rank>[:start|:end]" (test hook): raise inside that
+    parity transport on that rank, at its start (before its first collective: the other ranks
+    then block in one, and the watchdog ends the job) or at its end (after its rounds: the
+    transport's isolation turns it into parity false)."""
+    spec = os.environ.get("DPWA_BENCH_INJECT", "")
+    for item in filter(None, spec.split(",")):
+        t, _, rest = item.partition("@")
+        r, _, w = rest.partition(":")
+        if t == transport and int(r or 0) == rank and (w or "end") == where:
+            return True
+    return False
 
 
 def write_config(path, names, interp, fetch_probability=1.0, divergence_threshold=0.0):
@@ -122,12 +266,80 @@ def write_config(path, names, interp, fetch_probability=1.0, divergence_threshol
         f.write("\n".join(lines) + "\n")
 
 
-def cpu_baseline(numel, seconds):
+# ---------------------------------------------------------------- CPU baselines (before the GPU)
+def _timed(fn, seconds, min_rounds=1):
+    rounds, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        rounds += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and rounds >= min_rounds:
+            return rounds, el
+
+
+def cpu_restatement_rows(seconds):
+    """BASELINE.md CPU item 2: the averaging statement of pytorch.py:68 restated on the host at
+    every north_star size -- numpy fp32 on one thread (a*t + b*p with f32 scalars, separately
+    rounded; above NUMPY_SAMPLE_MAX elements on a bounded chunk of the workload) and torch-CPU
+    eager in the config's dtype on every torch thread (fp32 also at 1B).  Reported like `value`:
+    3*N*s averaged bytes per evaluation / time."""
+    rows = []
+    cores, threads = os.cpu_count(), torch.get_num_threads()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = None
+    g = torch.Generator().manual_seed(0)
+    for numel, dt in SWEEP:
+        esize = 4 if dt == "f32" else 2
+        forms = [("torch_cpu", dt)] + ([("torch_cpu", "f32")] if dt == "bf16" and numel <= 1_000_000_000 else [])
+        for kind, fdt in forms:
+            tdtype = torch.float32 if fdt == "f32" else torch.bfloat16
+            fs = 4 if fdt == "f32" else 2
+            p = torch.empty(numel, dtype=tdtype).uniform_(-1.0, 1.0, generator=g)
+            q = torch.empty(numel, dtype=tdtype).uniform_(-1.0, 1.0, generator=g)
+            box = [p]
+
+            def torch_round():
+                box[0] = 0.5 * q + (1.0 - 0.5) * box[0]
+
+            rounds, el = _timed(torch_round, seconds)
+            rows.append({"numel": numel, "dtype": fdt, "config_dtype": dt, "kind": kind, "threads": threads,
+                         "cpu_count": cores, "affinity_cpus": affinity, "rounds": rounds,
+                         "ms_per_round": round(1e3 * el / rounds, 3),
+                         "gbs": round(rounds * 3 * numel * fs / el / 1e9, 3),
+                         "statement": "factor * t + (1 - factor) * p, torch eager (pytorch.py:68)"})
+            del p, q, box
+        m = min(numel, NUMPY_SAMPLE_MAX)
+        pn = torch.empty(m, dtype=torch.float32).uniform_(-1.0, 1.0, generator=g).numpy()
+        qn = torch.empty(m, dtype=torch.float32).uniform_(-1.0, 1.0, generator=g).numpy()
+        a, b = np.float32(0.5), np.float32(1.0 - 0.5)
+        pbox = [pn]
+
+        def numpy_round():
+            pbox[0] = a * qn + b * pbox[0]
+
+        rounds, el = _timed(numpy_round, seconds)
+        rows.append({"numel": numel, "dtype": "f32", "config_dtype": dt, "kind": "numpy_1thread", "threads": 1,
+                     "cpu_count": cores, "affinity_cpus": affinity, "rounds": rounds,
+                     "ms_per_round": round(1e3 * el / rounds * numel / m, 3),
+                     "gbs": round(rounds * 3 * m * 4 / el / 1e9, 3),
+                     "sample": ("whole vector" if m == numel else
+                                "bounded: a %d-element chunk of the %d-element workload (rate is per byte; "
+                                "ms_per_round scaled to the whole vector)" % (m, numel)),
+                     "statement": "a * t + b * p, numpy float32, f32 scalars (restatement of pytorch.py:68)"})
+        del pn, qn, pbox
+        _ = esize
+    return rows
+
+
+def cpu_baseline(numel, seconds, rows=True):
     """The reference's CPU round (update_send -> TCP fetch -> update_wait; oracle/ref_round.py,
     which cites dpwa/adapters/pytorch.py, dpwa/conn.py and dpwa/messaging.py line by line)
     between two learner processes on this host, timed for ~`seconds`; reported like `value`
     (3*numel*4 averaged bytes per completed averaging).  Beside it, the C oracle running the
-    same round's arithmetic on one host core (publish copy + averaging)."""
+    same round's arithmetic on one host core (publish copy + averaging), and (rows) the
+    averaging statement restated with numpy / torch-CPU at every north_star size."""
     from oracle import lerp as olerp
     from oracle import ref_round
     # one reference round at 100M fp32 already takes seconds: larger vectors are sampled
@@ -179,15 +391,37 @@ def cpu_baseline(numel, seconds):
         "sample": "%d evaluations of the reference's lerp statement (pytorch.py:68) as torch-CPU fp32 eager ops "
                   "over %d elements, %.1f s" % (rounds, numel, el),
         "ms_per_round": 1e3 * el / rounds}
+    del param, peer, slot, tp, tq
+    if rows:
+        out["restatement_rows"] = cpu_restatement_rows(max(1.0, seconds / 8))
+        out["restatement_note"] = ("BASELINE.md CPU item 2: numpy fp32 one thread, torch-CPU in the config dtype "
+                                   "(and fp32 to 1B) on every torch thread, at 11.17M / 100M / 1B / 7B; "
+                                   "cpu_count = os.cpu_count(), threads = torch.get_num_threads()")
     return out
 
 
 # ---------------------------------------------------------------- parity leg (checker)
-# After the timed region: a short deterministic gossip through every transport the run
-# used, checked bit for bit against the oracle (oracle/ is imported only here and by the
-# cpu_baseline leg, as the checker -- never on the measured path).
+# A short deterministic gossip through every transport the run uses, checked bit for bit
+# against the oracle (oracle/ is imported only here and by the cpu_baseline leg, as the
+# checker -- never on the measured path).
 PARITY_N, PARITY_T, PARITY_FP = 1_000_003, 12, 0.7
 PARITY_ASYNC_T = 16
+PARITY_PHASE_S = 180.0          # watchdog budget of one parity transport
+
+
+def parity_transports(world, gossip="auto"):
+    """Every transport the run can time, plus the fd-shared (hipMemCreate, DPWA_VMM=1) slot
+    path that configs[3]/[4] use above 1.5 GiB, through the lock-step fused relay (slots and
+    relay buffers fd-imported) and the free-running board."""
+    if world == 1:
+        return ["local"]
+    t = []
+    if gossip != "async":
+        t += ["lockstep/copy", "lockstep/kernel:256", "lockstep/relay:32", "lockstep/relay-avg:32",
+              "lockstep/relay-avg:32+vmm"]
+    if gossip != "lockstep":
+        t += ["async/copy", "async/kernel:256", "async/copy+wt", "async/kernel:256+wt", "async/copy+vmm"]
+    return t
 
 
 def parity_init(g, n):
@@ -203,15 +437,18 @@ def parity_loss(g, r, wait):
     return 0.95 * x if wait else x
 
 
-def parity_lockstep(names, mine, cfg, group, pull, device, n=PARITY_N, T=PARITY_T):
+def parity_lockstep(names, mine, cfg, group, pull, device, n=PARITY_N, T=PARITY_T, conns=None, batch=False):
     """T lock-step rounds (clock interpolation, fetch_probability PARITY_FP) of the learners
     `mine` = [(name, g)] through the drop-in API: the training step adds a seeded delta; two
     of three rounds average with the fused kernel and write-through snapshots (the adapter's
-    default), every third through the split update_wait + average.  Returns per learner g the
-    per-round (sha1 of the parameters, clock, peer averaged with)."""
+    default; with `batch`, all of this process's learners in one dispatch), every third through
+    the split update_wait + average.  Returns per learner g the per-round (sha1 of the
+    parameters, clock, peer averaged with).  `conns` (a list) receives the connections as they
+    are made, so a caller can close them after a failure."""
     import hashlib
     from dpwa_amd import DpwaConnection
-    conns, flats = [], []
+    conns = [] if conns is None else conns
+    flats = []
     for name, g in mine:
         conns.append(DpwaConnection(name, cfg, seed=900 + g, group=group, pull=pull))
         flats.append(torch.from_numpy(parity_init(g, n)).to(device))
@@ -223,14 +460,19 @@ def parity_lockstep(names, mine, cfg, group, pull, device, n=PARITY_N, T=PARITY_
         for flat, (_, g) in zip(flats, mine):
             flat.add_(torch.from_numpy(parity_delta(g, r, n)).to(device))
         got = []
-        for conn, flat, (_, g) in zip(conns, flats, mine):
-            if r % 3 == 2:
-                payload, factor = conn.update_wait(parity_loss(g, r, True))
-                if payload is not None:
-                    conn.average(flat)
-            else:
-                payload, _ = conn.update_wait_average(flat, parity_loss(g, r, True), write_through=True)
-            got.append(payload.peer if payload is not None else "")
+        if r % 3 != 2 and batch:
+            res = DpwaConnection.update_wait_average_many(conns, flats, [parity_loss(g, r, True) for _, g in mine],
+                                                          write_through=True)
+            got = [p.peer if p is not None else "" for p, _ in res]
+        else:
+            for conn, flat, (_, g) in zip(conns, flats, mine):
+                if r % 3 == 2:
+                    payload, factor = conn.update_wait(parity_loss(g, r, True))
+                    if payload is not None:
+                        conn.average(flat)
+                else:
+                    payload, _ = conn.update_wait_average(flat, parity_loss(g, r, True), write_through=True)
+                got.append(payload.peer if payload is not None else "")
         for conn, flat, (_, g), peer in zip(conns, flats, mine, got):
             rec[g].append((hashlib.sha1(flat.cpu().numpy().tobytes()).hexdigest(), conn.clock, peer))
     torch.cuda.synchronize()
@@ -253,16 +495,18 @@ def parity_lockstep_expected(names, n=PARITY_N, T=PARITY_T):
                 for r in range(T)] for g in range(G)}
 
 
-def parity_async(names, rank, cfg, pull, device, n=PARITY_N, T=PARITY_ASYNC_T, write_through=False):
+def parity_async(names, rank, cfg, pull, device, n=PARITY_N, T=PARITY_ASYNC_T, write_through=False, conns=None):
     """Free-running rounds over the gossip board (AsyncDistGroup): each round publishes, runs
     an uneven synthetic step that sets the parameters to the checker's known values for
     (rank, round) and averages with whatever version the board hands out.  Without
     write-through the publish comes after that step (it publishes the known values); with it,
-    before (it publishes what the last average wrote through).  Returns (conn, params,
-    clocks, peers, versions)."""
+    before (it publishes what the last average wrote through).  Returns (params, clocks,
+    peers, versions)."""
     from dpwa_amd import DpwaConnection
     from oracle.async_check import async_base, async_loss
     conn = DpwaConnection(names[rank], cfg, seed=700 + rank, group="async", pull=pull)
+    if conns is not None:
+        conns.append(conn)
     rng = np.random.default_rng(rank)
     flat = torch.from_numpy(async_base(rank, -1, n)).to(device)
     bases = [torch.from_numpy(async_base(rank, r, n)).to(device) for r in range(T)]
@@ -280,7 +524,7 @@ def parity_async(names, rank, cfg, pull, device, n=PARITY_N, T=PARITY_ASYNC_T, w
         params[r] = flat.cpu().numpy()
         clocks[r] = conn.clock
     torch.cuda.synchronize()
-    return conn, params, clocks, peers, versions
+    return params, clocks, peers, versions
 
 
 def parity_key(trial):
@@ -294,96 +538,178 @@ def parity_key(trial):
     return "%s/%s%s" % (kind or "lockstep", pull, wt)
 
 
-def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backend):
+class _Env:
+    """Sets environment variables for the duration of a with-block (DPWA_VMM for +vmm)."""
+
+    def __init__(self, **kv):
+        self.kv, self.old = kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = os.environ.get(k)
+            os.environ[k] = v
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backend, ctl=None, watchdog=None):
     """Runs the parity workload through `transports` and returns {transport: bool} on every
     rank (rank 0 compares the lock-step digests with the oracle; each rank checks its own
-    free-running rounds)."""
+    free-running rounds).  Each transport is isolated: an exception on any rank becomes that
+    transport's `false` (the ranks agree over `ctl`, a gloo group, in the same collectives
+    whatever happened), and its connections are closed before the next one starts.  A hang
+    inside a transport is the watchdog's."""
     names = ["w%d" % (g + 1) for g in range(max(world, 2))]
     cfg = os.path.join(cfg_dir, "parity.yaml")
     write_config(cfg, names, "clock", PARITY_FP, 0.0)
+    if world > 1 and ctl is None:
+        ctl = dist.new_group(backend="gloo")
     result = {}
     expected = parity_lockstep_expected(names) if rank == 0 else None
     for t in transports:
-        progress("parity %s" % t)
+        if watchdog is not None:
+            watchdog.enter("parity %s" % t, PARITY_PHASE_S, transport=t)
+        else:
+            progress("parity %s" % t)
         kind, _, pull = t.partition("/")
-        if kind == "local":                   # one GPU: both learners in this process
-            from dpwa_amd.group import LocalGroup
-            conns, rec = parity_lockstep(names, [(names[0], 0), (names[1], 1)], cfg, LocalGroup(), None, device)
-            result[t] = rec == expected
+        vmm = pull.endswith("+vmm")
+        pull = pull.replace("+vmm", "")
+        conns, err, rec, check = [], None, None, None
+        try:
+            with _Env(DPWA_VMM="1") if vmm else _Env():
+                if injected(t, rank, "start"):
+                    raise RuntimeError("injected failure (DPWA_BENCH_INJECT, start)")
+                if kind == "local":                   # one GPU: both learners in this process, batched
+                    from dpwa_amd.group import LocalGroup
+                    _, rec = parity_lockstep(names, [(names[0], 0), (names[1], 1)], cfg, LocalGroup(), None, device,
+                                             conns=conns, batch=True)
+                elif kind == "lockstep":
+                    _, r = parity_lockstep(names, [(names[rank], rank)], cfg, "lockstep", pull, device, conns=conns)
+                    rec = r[rank]
+                else:                                  # async: free-running over the gossip board
+                    wt = pull.endswith("+wt")
+                    check = parity_async(names, rank, cfg, pull.replace("+wt", ""), device, write_through=wt,
+                                         conns=conns)
+                if injected(t, rank, "end"):
+                    raise RuntimeError("injected failure (DPWA_BENCH_INJECT, end)")
+        except Exception as e:   # noqa: BLE001 -- reported as this transport's parity false
+            err = "%s: %s" % (type(e).__name__, e)
+            progress("parity %s FAILED on rank %d: %s" % (t, rank, err))
+        finally:
+            for c in conns:
+                try:
+                    c.close()
+                except Exception as e:   # noqa: BLE001
+                    progress("parity %s: close failed: %s" % (t, e))
+        if kind == "local":
+            ok = err is None and rec == expected
         elif kind == "lockstep":
-            conns, rec = parity_lockstep(names, [(names[rank], rank)], cfg, "lockstep", pull, device)
             got = [None] * world
-            dist.all_gather_object(got, rec[rank])
-            ok = torch.tensor([1 if rank != 0 or all(got[g] == expected[g] for g in range(world)) else 0],
-                              dtype=torch.int32, device=device if dist_backend == "nccl" else "cpu")
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            result[t] = bool(ok.item())
-        else:                                  # async: free-running over the gossip board
-            from oracle.async_check import AsyncRuns, async_base
-            wt = pull.endswith("+wt")
-            conn, params, clocks, peers, versions = parity_async(names, rank, cfg, pull.replace("+wt", ""), device,
-                                                                 write_through=wt)
-            conns = [conn]
-            got = [None] * world
-            dist.all_gather_object(got, (peers, versions))
-            check = AsyncRuns(names, {g: got[g][0] for g in range(world)}, {g: got[g][1] for g in range(world)},
-                              "clock", None, 0.0)
-            if wt:   # each rank vouches for the averages of its own published versions (digests)
-                mine = check.served(rank, lambda v: async_base(rank, -1, PARITY_N) if v == 1 else params[v - 2],
-                                    PARITY_N)
-                served = [None] * world
-                dist.all_gather_object(served, mine)
-                vouched = {}
-                for d in served:
-                    vouched.update(d)
-                bad = check.check_rank_digests(rank, params, clocks, PARITY_N, vouched)
-            else:
-                bad = check.check_rank(rank, params, clocks, PARITY_N)
-            if bad:
-                print("parity %s rank %d: %s" % (t, rank, bad[:3]), file=sys.stderr, flush=True)
-            ok = torch.tensor([0 if bad else 1], dtype=torch.int32,
-                              device=device if dist_backend == "nccl" else "cpu")
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            result[t] = bool(ok.item())
-        torch.cuda.synchronize()
+            dist.all_gather_object(got, rec if err is None else None, group=ctl)
+            ok = rank != 0 or (all(g is not None for g in got) and all(got[g] == expected[g] for g in range(world)))
+        else:
+            ok = _async_verdict(t, names, world, rank, check, err, ctl)
+        if err is not None:
+            ok = False
+        result[t] = bool(_agree(ok, world, ctl) if world > 1 else ok)
+        if watchdog is not None:
+            watchdog.parity[t] = result[t]
+        try:
+            torch.cuda.synchronize()
+        except Exception as e:   # noqa: BLE001
+            progress("parity %s: synchronize failed: %s" % (t, e))
         if world > 1:
-            dist.barrier()
-        for c in conns:
-            c.close()
-        if world > 1:
-            dist.barrier()
+            dist.barrier(group=ctl)
+    if watchdog is not None:
+        watchdog.idle()
     return result
 
 
-def cold_kernel(numel, dtype, device, write_through=False, launches=64):
-    """The product averaging kernel (dpwa_average: k_lerp<Ops, COEF_FUSED, write_through> -- fp64
-    device factor + lerp in place, and with write_through the result also stored into a
-    snapshot payload) alone, over rotating buffers (> 1.2 GB of other traffic between
-    two uses of a buffer, so nothing is served from the 256 MiB Infinity Cache).  Every launch
-    is timed by its own dispatch begin/end events (hipExtLaunchKernelGGL), as rocprofv3 times
-    a kernel: the inter-kernel gaps of a back-to-back batch are not counted.  Also returns the
-    rate of one event pair around the whole batch (which does include the gaps)."""
+def _agree(ok, world, ctl):
+    """All ranks' verdicts, AND-ed, on every rank (a gloo all_gather: the CPU control group)."""
+    if world <= 1:
+        return bool(ok)
+    got = [None] * world
+    dist.all_gather_object(got, bool(ok), group=ctl)
+    return all(got)
+
+
+def _async_verdict(t, names, world, rank, check, err, ctl):
+    """Free-running rounds: every rank checks its own rounds version by version against
+    oracle/async_check.py; the (peers, versions) of every rank are gathered first (every rank
+    enters the same collectives whether or not its run failed)."""
+    from oracle.async_check import AsyncRuns, async_base
+    wt = t.endswith("+wt")
+    got = [None] * world
+    dist.all_gather_object(got, (check[2], check[3]) if check is not None else None, group=ctl)
+    if any(g is None for g in got):     # every rank sees it: none enters the next collective
+        return False
+    params, clocks = check[0], check[1]
+    runs = AsyncRuns(names, {g: got[g][0] for g in range(world)}, {g: got[g][1] for g in range(world)},
+                     "clock", None, 0.0)
+    if wt:   # each rank vouches for the averages of its own published versions (digests)
+        mine = runs.served(rank, lambda v: async_base(rank, -1, PARITY_N) if v == 1 else params[v - 2], PARITY_N)
+        served = [None] * world
+        dist.all_gather_object(served, mine, group=ctl)
+        vouched = {}
+        for d in served:
+            vouched.update(d)
+        bad = runs.check_rank_digests(rank, params, clocks, PARITY_N, vouched)
+    else:
+        bad = runs.check_rank(rank, params, clocks, PARITY_N)
+    if bad:
+        print("parity %s rank %d: %s" % (t, rank, bad[:3]), file=sys.stderr, flush=True)
+    return not bad
+
+
+# ---------------------------------------------------------------- kernel measurements
+def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners=1):
+    """The product averaging kernel alone over rotating buffers (> 1.2 GB of other traffic
+    between two uses of a buffer, so nothing is served from the 256 MiB Infinity Cache).  With
+    learners == 1 it is dpwa_average (k_lerp<Ops, COEF_FUSED, write_through>: fp64 device
+    factor + lerp in place, with write_through the result also stored into a snapshot
+    payload); with learners > 1, dpwa_average_many: that many independent averages in ONE
+    dispatch (k_lerp_batch, the N=1 loop's kernel).  Every launch is timed by its own dispatch
+    begin/end events (hipExtLaunchKernelGGL), as rocprofv3 times a kernel: the inter-kernel
+    gaps of a back-to-back batch are not counted.  Also returns the rate of one event pair
+    around the whole batch (which does include the gaps)."""
     from dpwa_amd import _lib
     esize = 4 if dtype == torch.float32 else 2
     nbuf = 3 if write_through else 2
-    pairs = max(2, int(np.ceil(1.2e9 / (nbuf * numel * esize))))
-    launches = max(2 * pairs, min(launches, int(np.ceil(64 * 134e6 / (3 * numel * esize)))))
+    per_set = learners * nbuf * numel * esize
+    sets = max(2, int(np.ceil(1.2e9 / per_set)))
+    launches = max(2 * sets, min(launches, int(np.ceil(64 * 134e6 / (3 * learners * numel * esize)))))
     hdr = _lib.SLOT_PAYLOAD_OFFSET // esize
-    params, slots, snaps = [], [], []
-    for _ in range(pairs):
-        params.append(torch.empty(numel, device=device, dtype=dtype).normal_())
-        # a snapshot slot as the learner lays it out: header (zeros) and pad, then the payload
-        slot = torch.zeros(hdr + numel, device=device, dtype=dtype)
-        slot[hdr:].normal_()
-        slots.append(slot)
-        # the write-through destination is the payload of another slot
-        snaps.append(torch.empty(hdr + numel, device=device, dtype=dtype)[hdr:] if write_through else None)
-    clock = torch.zeros(2, device=device, dtype=torch.float64)
-    coef = torch.zeros(4, device=device, dtype=torch.float64)           # dpwa_coef, 32 B
+    bufs = []       # per set: [(param, slot, snap)] * learners
+    for _ in range(sets):
+        entries = []
+        for _ in range(learners):
+            param = torch.empty(numel, device=device, dtype=dtype).normal_()
+            # a snapshot slot as the learner lays it out: header (zeros) and pad, then the payload
+            slot = torch.zeros(hdr + numel, device=device, dtype=dtype)
+            slot[hdr:].normal_()
+            # the write-through destination is the payload of another slot
+            snap = torch.empty(hdr + numel, device=device, dtype=dtype)[hdr:] if write_through else None
+            entries.append((param, slot, snap))
+        bufs.append(entries)
+    clocks = torch.zeros(learners, 2, device=device, dtype=torch.float64)
+    coefs = torch.zeros(learners, 4, device=device, dtype=torch.float64)           # dpwa_coef, 32 B
     cfg = _lib.Interp(_lib.INTERP_CONSTANT, 0, 0.5, 0.0)
     dt = _lib.F32 if dtype == torch.float32 else _lib.BF16
     s = _lib.stream_handle(None)
-    f = _lib.load().dpwa_average
+    lib = _lib.load()
+    descs = []
+    for entries in bufs:
+        d = (_lib.AverageDesc * learners)()
+        for j, (param, slot, snap) in enumerate(entries):
+            d[j] = _lib.AverageDesc(param.data_ptr(), slot.data_ptr(), numel, clocks[j].data_ptr(), 1.0,
+                                    coefs[j].data_ptr(), snap.data_ptr() if snap is not None else None)
+        descs.append(d)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
     for a, b in ev:          # create the events (the kernel dispatch then records into them)
         a.record()
@@ -391,14 +717,20 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64):
 
     def run(i, timed):
         a, b = ev[i] if timed else (None, None)
-        snap = snaps[i % pairs]
-        rc = f(dt, params[i % pairs].data_ptr(), slots[i % pairs].data_ptr(), numel, ctypes.byref(cfg),
-               clock.data_ptr(), 1.0, coef.data_ptr(), snap.data_ptr() if snap is not None else None, s,
-               a.cuda_event if timed else None, b.cuda_event if timed else None)
+        ea, eb = (a.cuda_event, b.cuda_event) if timed else (None, None)
+        if learners == 1:
+            param, slot, snap = bufs[i % sets][0]
+            rc = lib.dpwa_average(dt, param.data_ptr(), slot.data_ptr(), numel, ctypes.byref(cfg),
+                                  clocks[0].data_ptr(), 1.0, coefs[0].data_ptr(),
+                                  snap.data_ptr() if snap is not None else None, s, ea, eb)
+            name = "dpwa_average"
+        else:
+            rc = lib.dpwa_average_many(dt, descs[i % sets], learners, ctypes.byref(cfg), s, ea, eb)
+            name = "dpwa_average_many"
         if rc:
-            raise _lib.DpwaError("dpwa_average", rc, _lib.load().dpwa_last_error().decode())
+            raise _lib.DpwaError(name, rc, lib.dpwa_last_error().decode())
 
-    for i in range(pairs):
+    for i in range(sets):
         run(i, False)
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda._sleep(50_000_000)          # let the host queue the whole batch first
@@ -409,17 +741,18 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64):
     torch.cuda.synchronize()
     us = np.array([a.elapsed_time(b) * 1e3 for a, b in ev])
     batch_us = t0.elapsed_time(t1) * 1e3 / launches
-    del params, slots, snaps
+    del bufs, descs
     torch.cuda.empty_cache()
     return {"avg_launch_us": float(us.mean()), "median_launch_us": float(np.median(us)),
             "min_launch_us": float(us.min()), "max_launch_us": float(us.max()), "launches": launches,
-            "rotating_buffer_pairs": pairs, "batch_bracket_us": float(batch_us)}
+            "rotating_buffer_sets": sets, "learners_per_launch": learners, "batch_bracket_us": float(batch_us)}
 
 
-def round_sweep(device, cfg_dir, steps=20, warmup=3):
+def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True):
     """Whole gossip rounds (two co-resident learners, write-through publish, constant 0.5,
-    fetch_probability 1) at every north_star size in its config's dtype: the averaged GB/s
-    and rounds/s the north star asks for at 11M/100M/1B/7B on one GPU."""
+    fetch_probability 1, both averages in one dispatch) at every north_star size in its
+    config's dtype: the averaged GB/s and rounds/s the north star asks for at 11M/100M/1B/7B
+    on one GPU."""
     from dpwa_amd import DpwaConnection
     from dpwa_amd.group import LocalGroup
     rows = []
@@ -439,6 +772,9 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3):
         def step():
             for c, f in zip(conns, flats):
                 c.update_send(f, 1.0, reuse_snapshot=True)
+            if batch:
+                res = DpwaConnection.update_wait_average_many(conns, flats, [1.0, 1.0], write_through=True)
+                return sum(p is not None for p, _ in res)
             n = 0
             for c, f in zip(conns, flats):
                 n += c.update_wait_average(f, 1.0, write_through=True)[0] is not None
@@ -453,7 +789,7 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3):
         el = time.perf_counter() - t0
         rows.append({"numel": numel, "dtype": dt, "value": round(averaged * 3 * numel * esize / el / 1e9, 1),
                      "ms_per_step": round(1e3 * el / steps, 4), "gossip_rounds_per_s": round(2 * steps / el, 1),
-                     "steps": steps})
+                     "steps": steps, "batched": batch})
         for c in conns:
             c.close()
         del flats, conns
@@ -464,48 +800,70 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3):
 def size_sweep(device):
     """The averaging kernel, cold, per launch, at every north_star size (11.17M/100M fp32,
     1B/7B bf16), in both publish forms: plain (3*N*s bytes per launch) and write-through
-    (4*N*s: the next snapshot is written by the same pass)."""
+    (4*N*s: the next snapshot is written by the same pass); and at 11.17M / 100M the batched
+    dispatch of two learners' write-through averages (the N=1 loop's kernel, 2 x 4*N*s)."""
     rows = []
     for numel, dt in SWEEP:
         esize = 4 if dt == "f32" else 2
-        for wt in (False, True):
-            c = cold_kernel(numel, torch.float32 if dt == "f32" else torch.bfloat16, device, wt)
-            nbytes = (4 if wt else 3) * numel * esize
+        forms = [(False, 1), (True, 1)] + ([(True, 2)] if numel <= 100_000_000 else [])
+        for wt, learners in forms:
+            c = cold_kernel(numel, torch.float32 if dt == "f32" else torch.bfloat16, device, wt, learners=learners)
+            nbytes = learners * (4 if wt else 3) * numel * esize
             gbs = nbytes / (c["avg_launch_us"] * 1e-6) / 1e9
             rows.append({"numel": numel, "dtype": dt, "publish": "write-through" if wt else "full",
+                         "learners_per_launch": learners,
                          "bytes_per_launch": nbytes, "avg_launch_us": round(c["avg_launch_us"], 2),
                          "median_launch_us": round(c["median_launch_us"], 2), "achieved": round(gbs, 1),
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "launches": c["launches"],
-                         "rotating_buffer_sets": c["rotating_buffer_pairs"],
+                         "rotating_buffer_sets": c["rotating_buffer_sets"],
                          "batch_bracket_us": round(c["batch_bracket_us"], 2)})
     return rows
 
 
-def main():
-    args = parse()
+# ---------------------------------------------------------------- the run
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if args.gpus > 1 and world == 0:
+        # no launcher: start one as a child process before anything touches a GPU
+        sys.exit(self_launch(args, argv))
+    world = world or 1
     # a rank stopped from outside (the launcher after another rank failed, a time limit) prints
     # where every thread was before it goes
     import faulthandler
     import signal
     faulthandler.register(signal.SIGTERM, all_threads=True, chain=True)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit("--gpus %d but WORLD_SIZE %d (launch N>1 with torch.distributed.run)" % (args.gpus, world))
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    wd = Watchdog(args, world, rank)
     # the CPU baseline first, before anything touches the GPU (its learners are child processes)
-    progress("start: world %d, numel %d %s" % (world, args.numel, args.dtype))
-    cpu = cpu_baseline(args.numel, args.cpu_seconds) if world == 1 and not args.no_cpu_baseline else None
+    wd.enter("start: world %d, numel %d %s" % (world, args.numel, args.dtype), 600.0)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        wd.enter("cpu baseline", 600.0)
+        cpu = cpu_baseline(args.numel, args.cpu_seconds, rows=not args.no_cpu_rows)
     # one GPU per rank; the modulo only matters for rehearsals with more ranks than GPUs
+    wd.enter("gpu init", 600.0)
     device = torch.device("cuda", local_rank % torch.cuda.device_count())
     torch.cuda.set_device(device)
+    ctl = None
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:   # rehearsal of the N>1 path on fewer GPUs (RCCL refuses two ranks per GPU)
             dist.init_process_group("gloo")
+        ctl = dist.new_group(backend="gloo")    # control plane: object gathers, agreement, host barriers
+
+    def hbarrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier(group=ctl)
 
     from dpwa_amd import DpwaConnection
+    from dpwa_amd import _lib
     from dpwa_amd.group import LocalGroup
 
     dtype = torch.float32 if args.dtype == "f32" else torch.bfloat16
@@ -515,13 +873,22 @@ def main():
     if world == 1:
         names = ["w1", "w2"]
         write_config(cfg, names, args.interpolation, args.fetch_probability, args.divergence_threshold)
-        group = LocalGroup()
         mine = [(names[0], 0), (names[1], 1)]
     else:
         names = ["w%d" % (r + 1) for r in range(world)]
         write_config(cfg, names, args.interpolation, args.fetch_probability, args.divergence_threshold)
-        group = None
         mine = [(names[rank], rank)]
+
+    # At N>1 the parity leg runs first: a transport that fails it on this node's devices is
+    # reported (parity: false) and left out of the trials, so the timed run always uses a
+    # transport whose results matched the oracle.
+    parity = None
+    if world > 1 and not args.no_parity:
+        parity = parity_leg(world, rank, local_rank, device, tmp, parity_transports(world, args.gossip),
+                            args.dist_backend, ctl=ctl, watchdog=wd)
+
+    wd.enter("learners", 300.0)
+    group = LocalGroup() if world == 1 else None
     learners = []
     for name, seed in mine:
         g = torch.Generator(device=device).manual_seed(seed)
@@ -535,6 +902,7 @@ def main():
     # co-resident learners on their own streams (their kernels overlap) or all on one
     streams = ([torch.cuda.Stream(device) for _ in learners] if args.streams == "per-learner"
                else [stream for _ in learners])
+    batched = world == 1 and args.streams == "one" and not args.no_batch and len(learners) > 1
     # per-learner loss stream: constant 1.0, or SURVEY §8d C4's synthetic decay
     # l_t = 2 exp(-t/200) + 0.05 U(0,1) (seeded per learner) so a divergence threshold is crossed
     loss_rngs = [np.random.default_rng(7 + seed) for _, seed in mine]
@@ -544,15 +912,16 @@ def main():
         if args.loss_schedule == "constant":
             return 1.0
         return 2.0 * float(np.exp(-loss_t[0] / 200.0)) + 0.05 * float(loss_rngs[i].random())
-    from dpwa_amd import _lib
 
-    def run(steps, warmup, write_through, sample_every):
-        """`steps` timed lock-step rounds; the averaging kernel of every `sample_every`-th
-        step is timed by its own dispatch events (and, as a cross-check, bracketed by an
-        event pair on its stream)."""
+    def run(steps, warmup, write_through, sample_every=0):
+        """`steps` timed lock-step rounds.  sample_every == 0: nothing but the rounds (the
+        pass `value` comes from).  sample_every = k > 0: the averaging dispatch of every k-th
+        step is timed by its own dispatch events (and/or bracketed by an event pair on its
+        stream) -- the in-loop kernel figure, from a separate pass."""
         lerp_events = []
+        n_slots = (steps // sample_every + 1) * len(learners) if sample_every else 0
         events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                  for _ in range((steps // sample_every + 1) * len(learners))]
+                  for _ in range(n_slots)]
         lib = _lib.load()
         timed_learners = []
 
@@ -563,7 +932,20 @@ def main():
             for i, (conn, flat) in enumerate(learners):
                 with torch.cuda.stream(streams[i]):
                     conn.update_send(flat, losses[i], reuse_snapshot=write_through)
-            sample = timed and k % sample_every == 0
+            sample = timed and sample_every and k % sample_every == 0
+            if batched:
+                if sample:
+                    a, b = events[len(lerp_events)]
+                    if args.timing != "dispatch":
+                        a.record(stream)
+                    if args.timing != "bracket" and timed_learners:
+                        lib.dpwa_learner_arm_timing(timed_learners[0]._learner.handle)
+                res = DpwaConnection.update_wait_average_many([c for c, _ in learners], [f for _, f in learners],
+                                                              losses, write_through=write_through)
+                if sample and args.timing != "dispatch":
+                    b.record(stream)
+                    lerp_events.append((a, b))
+                return sum(p is not None for p, _ in res)
             for i, (conn, flat) in enumerate(learners):
                 st = streams[i]
                 with torch.cuda.stream(st):
@@ -571,7 +953,7 @@ def main():
                     if sample:
                         a, b = events[len(lerp_events)]
                         if world > 1 and args.timing != "dispatch":   # keep the pull wait out of the bracket
-                            _lib.load().dpwa_learner_wait_fetch(conn._learner.handle, st.cuda_stream)
+                            lib.dpwa_learner_wait_fetch(conn._learner.handle, st.cuda_stream)
                         if args.timing != "dispatch":
                             a.record(st)
                         if args.timing != "bracket" and conn in timed_learners:
@@ -586,13 +968,12 @@ def main():
 
         for k in range(warmup):
             step(k, False)
-        for conn, _ in learners:    # kernel-dispatch timing of the sampled averaging launches
-            if conn._learner is not None:
-                _lib.call("dpwa_learner_time_averages", conn._learner.handle, steps // sample_every + 1)
-                timed_learners.append(conn)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+        if sample_every:
+            for conn, _ in learners:    # kernel-dispatch timing of the sampled averaging launches
+                if conn._learner is not None:
+                    _lib.call("dpwa_learner_time_averages", conn._learner.handle, steps // sample_every + 1)
+                    timed_learners.append(conn)
+        hbarrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         averaged = 0
@@ -600,13 +981,12 @@ def main():
             averaged += step(k, True)
         torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
+            hbarrier()
         elapsed = time.perf_counter() - t0
         bracket_ms = np.array([a.elapsed_time(b) for a, b in lerp_events]) if lerp_events else np.array([np.nan])
         kern_us = []
         for conn in timed_learners:
-            buf = (ctypes.c_float * len(events))()
+            buf = (ctypes.c_float * max(1, len(events)))()
             cnt = ctypes.c_int()
             _lib.call("dpwa_learner_read_average_times", conn._learner.handle, buf, len(events), ctypes.byref(cnt))
             kern_us += list(buf[:cnt.value])
@@ -614,14 +994,11 @@ def main():
         if args.timing == "bracket":
             kern_us = list(bracket_ms * 1e3)
         lerp_ms = (np.array(kern_us) / 1e3 if kern_us else np.array([np.nan]), bracket_ms)
-        stats = torch.tensor([elapsed, float(averaged), float(len(learners) * steps)], dtype=torch.float64,
-                             device=device if args.dist_backend == "nccl" else "cpu")
+        stats = torch.tensor([elapsed, float(averaged), float(len(learners) * steps)], dtype=torch.float64)
         if world > 1:
-            tmax = stats[0:1].clone()
-            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-            sums = stats[1:].clone()
-            dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-            return float(tmax.item()), float(sums[0].item()), float(sums[1].item()), lerp_ms
+            got = [None] * world
+            dist.all_gather_object(got, stats.tolist(), group=ctl)
+            return (max(g[0] for g in got), sum(g[1] for g in got), sum(g[2] for g in got), lerp_ms)
         return elapsed, float(averaged), float(len(learners) * steps), lerp_ms
 
     def make_compute(target_us):
@@ -642,9 +1019,9 @@ def main():
         per_us = e0.elapsed_time(e1) * 1e3 / 20
         k = max(1, int(round(target_us / per_us)))
         if world > 1:            # every rank runs the same step
-            kt = torch.tensor([k], dtype=torch.int64, device=device if args.dist_backend == "nccl" else "cpu")
-            dist.all_reduce(kt, op=dist.ReduceOp.MAX)
-            k = int(kt.item())
+            got = [None] * world
+            dist.all_gather_object(got, k, group=ctl)
+            k = max(got)
 
         def compute():
             for _ in range(k):
@@ -663,103 +1040,105 @@ def main():
             for _ in learners:
                 compute()
             if gossip:
-                for i, (conn, flat) in enumerate(learners):
-                    payload, _ = conn.update_wait_average(flat, losses[i], write_through=wt_main)
-                    done += payload is not None
+                if batched:
+                    res = DpwaConnection.update_wait_average_many([c for c, _ in learners],
+                                                                  [f for _, f in learners], losses,
+                                                                  write_through=wt_main)
+                    done += sum(p is not None for p, _ in res)
+                else:
+                    for i, (conn, flat) in enumerate(learners):
+                        payload, _ = conn.update_wait_average(flat, losses[i], write_through=wt_main)
+                        done += payload is not None
             return done
 
         for _ in range(warmup):
             step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+        hbarrier()
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                          device=device if args.dist_backend == "nccl" else "cpu")
+            hbarrier()
+        el = time.perf_counter() - t0
         if world > 1:
-            dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        return float(el.item())
+            got = [None] * world
+            dist.all_gather_object(got, el, group=ctl)
+            el = max(got)
+        return el
 
     def set_pull(mode):
         for conn, _ in learners:
             conn.set_pull(mode)
         if world > 1:
-            dist.barrier()
-
-    def run_parity():
-        if world == 1:
-            transports = ["local"]
-        else:
-            transports = []
-            if args.gossip != "async":
-                transports += ["lockstep/copy", "lockstep/kernel:256", "lockstep/relay:32", "lockstep/relay-avg:32"]
-            if args.gossip != "lockstep":
-                transports += ["async/copy", "async/kernel:256", "async/copy+wt", "async/kernel:256+wt"]
-        res = parity_leg(world, rank, local_rank, device, tmp, transports, args.dist_backend)
-        res["workload"] = ("%d-element fp32 vector per learner, %d lock-step rounds (clock interpolation, "
-                           "fetch_probability %g, seeded training-step deltas, write-through and split rounds "
-                           "mixed), %d free-running rounds over the gossip board; every learner's parameters, "
-                           "clocks and peers compared bit for bit with oracle/gossip.py (lock-step) and "
-                           "oracle/async_check.py (per version read)"
-                           % (PARITY_N, PARITY_T, PARITY_FP, PARITY_ASYNC_T))
-        return res
-
-    # At N>1 the parity leg runs first: a transport that fails it on this node's devices is
-    # reported (parity: false) and left out of the trials, so the timed run always uses a
-    # transport whose results matched the oracle.
-    parity = run_parity() if world > 1 and not args.no_parity else None
+            hbarrier()
 
     def verified(trial):
         return parity is None or parity.get(parity_key(trial), False)
 
     pull_trials = {}
+    trial_errors = {}
     pull = args.pull
     wt_lockstep = args.publish == "write-through"     # free-running rounds always publish in full
     lockstep_learners = list(learners)
     async_learners = []
     if world > 1:
-        progress("binding %d lock-step learner(s)" % len(learners))
-        run(2, 2, False, 1000)   # binds the learners (IPC exchange) before the transport is chosen
+        wd.enter("binding %d lock-step learner(s)" % len(learners), 600.0)
+        run(2, 2, False)   # binds the learners (IPC exchange) before the transport is chosen
         modes = [args.pull] if args.pull != "auto" else ["copy", "kernel:256", "kernel:1024", "relay:32",
                                                          "relay:128", "relay:512", "relay-avg:32",
                                                          "relay-avg:128", "relay-avg:512"]
-        trial_steps = max(10, args.steps // 10)
+        cands = []          # (key, lockstep?, pull mode, write-through)
         if args.gossip != "async":
-            for mode in [m for m in modes if verified(m)]:   # short timed trials; the fastest is used below
-                set_pull(mode)
-                el, av, _, _ = run(trial_steps, 2, wt_lockstep, 1000)
-                pull_trials[mode] = round(av * 3 * args.numel * esize / el / 1e9, 2)
-                progress("trial %s: %.1f GB/s" % (mode, pull_trials[mode]))
+            cands += [(m, True, m, wt_lockstep) for m in modes if verified(m)]
         if args.gossip != "lockstep":
+            wd.enter("binding free-running learner(s)", 600.0)
             # free-running rounds over the gossip board, same learners' parameters (a second
             # set of nodes: a connection's group is fixed at construction)
             for (name, seed), (_, flat) in zip(mine, lockstep_learners):
                 conn = DpwaConnection(name, cfg, seed=1000 + seed, group="async", pull="copy")
                 async_learners.append((conn, flat))
             learners[:] = async_learners
-            progress("binding free-running learner(s)")
-            run(2, 2, False, 1000)
-            for mode in [m for m in modes if not m.startswith("relay")]:
-                wts = [wt for wt in ((False, True) if wt_lockstep else (False,))
-                       if verified("async/" + mode + ("+wt" if wt else ""))]
-                if not wts:
+            run(2, 2, False)
+            for m in [m for m in modes if not m.startswith("relay")]:
+                for wt in ((False, True) if wt_lockstep else (False,)):
+                    key = "async/" + m + ("+wt" if wt else "")
+                    if verified(key):
+                        cands.append((key, False, m, wt))
+        # interleaved passes, each trial >= --trial-ms and >= 30 rounds; the median decides
+        rounds_of = {key: 30 for key, _, _, _ in cands}
+        for p in range(max(1, args.trial_passes)):
+            for key, lock, m, wt in cands:
+                if key in trial_errors:
                     continue
-                set_pull(mode)
-                for wt in wts:
-                    el, av, _, _ = run(trial_steps, 2, wt, 1000)
-                    pull_trials["async/" + mode + ("+wt" if wt else "")] = \
-                        round(av * 3 * args.numel * esize / el / 1e9, 2)
-                    progress("trial async/%s%s: %.1f GB/s" % (mode, "+wt" if wt else "",
-                                                              pull_trials["async/" + mode + ("+wt" if wt else "")]))
-        if not pull_trials:
-            raise SystemExit("bench.py: no transport passed the parity check: %s"
-                             % {k: v for k, v in parity.items() if k != "workload"})
-        pull = max(pull_trials, key=pull_trials.get)
+                wd.enter("trial %s (pass %d)" % (key, p + 1), 120.0)
+                err = None
+                try:
+                    learners[:] = lockstep_learners if lock else async_learners
+                    set_pull(m)
+                    el, av, _, _ = run(rounds_of[key], 2, wt)
+                    gbs = av * 3 * args.numel * esize / el / 1e9
+                except Exception as e:   # noqa: BLE001 -- the transport leaves the trials
+                    err, el, gbs = "%s: %s" % (type(e).__name__, e), None, None
+                    progress("trial %s FAILED: %s" % (key, err))
+                if not _agree(err is None, world, ctl):
+                    trial_errors[key] = err or "failed on another rank"
+                    continue
+                pull_trials.setdefault(key, []).append(round(gbs, 2))
+                if p == 0:   # same on every rank: el is the max over ranks
+                    rounds_of[key] = max(30, int(np.ceil(args.trial_ms * 1e-3 / (el / rounds_of[key]))))
+                progress("trial %s: %.1f GB/s" % (key, gbs))
+        medians = {k: float(np.median(v)) for k, v in pull_trials.items()}
+        if not medians:
+            wd.idle()
+            if rank == 0:
+                out = base_line(args, world)
+                out["error"] = "no transport passed the parity check and its trials"
+                out["parity"] = parity
+                out["trial_errors"] = trial_errors
+                print(json.dumps(out), flush=True)
+            sys.exit(1)
+        pull = max(medians, key=medians.get)
         if pull.startswith("async/"):
             learners[:] = async_learners
             set_pull(pull[len("async/"):].replace("+wt", ""))
@@ -768,39 +1147,46 @@ def main():
             for conn, _ in async_learners:   # free their streams and slots (fewer HW queues in use)
                 conn.close()
             async_learners = []
-            torch.cuda.synchronize()
-            dist.barrier()
+            hbarrier()
             set_pull(pull)
     # trial key: "<mode>" (lock-step, publish per --publish) or "async/<mode>[+wt]"
     sel_async = pull.startswith("async/")
     sel_mode = pull.split("/")[-1].replace("+wt", "")
     wt_main = pull.endswith("+wt") if sel_async else wt_lockstep
-    progress("timed run: %s, %s publish" % (pull, "write-through" if wt_main else "full"))
-    elapsed, averaged, rounds, (lerp_ms, bracket_ms) = run(args.steps, args.warmup, wt_main, args.sample_every)
+    wd.enter("timed run: %s, %s publish" % (pull, "write-through" if wt_main else "full"),
+             600.0 + 0.05 * (args.steps + args.warmup))
+    elapsed, averaged, rounds, _ = run(args.steps, args.warmup, wt_main)
     progress("timed run: %.4f ms/step" % (1e3 * elapsed / args.steps))
+    # the averaging kernel inside the loop: a separate sampled pass of the same rounds
+    wd.enter("in-loop kernel timing", 600.0)
+    s_steps = max(args.steps, 8 * args.sample_every)
+    s_el, _, _, (lerp_ms, bracket_ms) = run(s_steps, 2, wt_main, args.sample_every)
     pull_us = []
     if world > 1 and not sel_mode.startswith("relay"):
         # the pull alone (side-stream events around each copying fetch), in a short extra run
+        wd.enter("pull timing", 300.0)
         p_steps = max(20, args.steps // 4)
         for conn, _ in learners:
             _lib.call("dpwa_learner_time_fetches", conn._learner.handle, p_steps + 4)
-        run(p_steps, 2, wt_main, 1000)
+        run(p_steps, 2, wt_main)
         for conn, _ in learners:
             buf = (ctypes.c_float * (p_steps + 4))()
             cnt = ctypes.c_int()
             _lib.call("dpwa_learner_read_fetch_times", conn._learner.handle, buf, p_steps + 4, ctypes.byref(cnt))
             pull_us += list(buf[2:cnt.value])     # the 2 warmup rounds' pulls are left out
             _lib.call("dpwa_learner_time_fetches", conn._learner.handle, 0)
-        t = torch.tensor([float(np.mean(pull_us)) if pull_us else float("nan")], dtype=torch.float64,
-                         device=device if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        pull_us = [float(t.item()) / world]
+        got = [None] * world
+        dist.all_gather_object(got, float(np.mean(pull_us)) if pull_us else float("nan"), group=ctl)
+        pull_us = [float(np.mean(got))]
     secondary = None
     if not args.no_secondary:      # the other publish form, same learners and transport, for comparison
-        progress("secondary publish form")
-        secondary = (not wt_main, run(args.steps, args.warmup, not wt_main, args.sample_every))
+        wd.enter("secondary publish form", 600.0)
+        s2 = run(args.steps, args.warmup, not wt_main)
+        s2_k = run(s_steps, 2, not wt_main, args.sample_every)
+        secondary = (not wt_main, s2, s2_k[3])
     overlap = None
     if args.compute_us > 0:
+        wd.enter("overlap", 600.0)
         compute, k_gemm, gemm_us = make_compute(args.compute_us)
         o_steps = max(20, args.steps // 4)
         progress("overlap: %d GEMMs per step" % k_gemm)
@@ -837,14 +1223,32 @@ def main():
             overlap["trials_ms_per_step"] = {m: round(1e3 * t / o_steps, 4) for m, t in o_trials.items()}
 
     if world == 1 and not args.no_parity:      # one transport (local): checked after the timed region
-        parity = run_parity()
+        parity = parity_leg(1, 0, 0, device, tmp, parity_transports(1), args.dist_backend, watchdog=wd)
+    if parity is not None:
+        parity["workload"] = ("%d-element fp32 vector per learner, %d lock-step rounds (clock interpolation, "
+                              "fetch_probability %g, seeded training-step deltas, write-through and split rounds "
+                              "mixed; at N=1 both learners' averages batched), %d free-running rounds over the "
+                              "gossip board; every learner's parameters, clocks and peers compared bit for bit with "
+                              "oracle/gossip.py (lock-step) and oracle/async_check.py (per version read); '+vmm': "
+                              "snapshot slots (and relay buffers) fd-shared hipMemCreate chunks, the configs[3]/[4] "
+                              "path" % (PARITY_N, PARITY_T, PARITY_FP, PARITY_ASYNC_T))
     used = "local" if world == 1 else parity_key(pull)
 
     unit_bytes = 3 * args.numel * esize
-    kbytes = (4 if wt_main else 3) * args.numel * esize     # the timed loop's averaging kernel, per launch
+    per_launch = len(learners) if batched else 1
+    kbytes = (4 if wt_main else 3) * args.numel * esize * per_launch   # the timed loop's averaging dispatch
     # the same kernel alone, cold (rotating buffers, per-launch dispatch events): the roofline's basis
-    progress("cold kernel")
-    cold = cold_kernel(args.numel, dtype, device, wt_main) if not args.no_cold else None
+    cold = None
+    if not args.no_cold:
+        wd.enter("cold kernel", 300.0)
+        cold = cold_kernel(args.numel, dtype, device, wt_main, learners=per_launch)
+    size_rows, round_rows = None, None
+    if world == 1 and not args.no_sweep:
+        wd.enter("size sweep", 900.0)
+        size_rows = size_sweep(device)
+        wd.enter("round sweep", 900.0)
+        round_rows = round_sweep(device, tmp, batch=batched)
+    wd.enter("report", 120.0)
     if rank == 0:
         value = averaged * unit_bytes / elapsed / 1e9
         lerp_us = float(np.nanmean(lerp_ms) * 1e3)
@@ -852,29 +1256,28 @@ def main():
         k_us = cold["avg_launch_us"] if cold else lerp_us
         achieved = kbytes / (k_us * 1e-6) / 1e9
         variant = "write-through" if wt_main else "full"
-        traffic = None
-        traffic_src = None
-        tpath = args.traffic or os.path.join(ROOT, "profiles", "traffic_r02_%s.json" % variant)
+        traffic, traffic_src = None, None
+        tname = "traffic_r03_%s%s.json" % (variant, "_x%d" % per_launch if per_launch > 1 else "")
+        tpath = args.traffic or os.path.join(ROOT, "profiles", tname)
         if os.path.exists(tpath):
             with open(tpath) as f:
                 tr = json.load(f)
             if (tr.get("numel") == args.numel and tr.get("dtype") == args.dtype and
-                    tr.get("publish", "full") == variant and tr.get("basis", "in-loop") == ("cold" if cold else "in-loop")):
+                    tr.get("publish", "full") == variant and tr.get("learners_per_launch", 1) == per_launch and
+                    tr.get("basis", "in-loop") == ("cold" if cold else "in-loop")):
                 traffic = tr.get("hbm_bytes_per_launch")
                 traffic_src = os.path.relpath(tpath, ROOT)
-        out = {
-            "metric": "pairwise-average GB/s (% HBM peak) + gossip rounds/s",
+        kname = ("dpwa::k_lerp_batch<Ops%s, %s> (%d learners' fused device factor + lerp%s in one dispatch)"
+                 % (args.dtype.upper(), "true" if wt_main else "false", per_launch,
+                    " + write-through of the next snapshot" if wt_main else "") if per_launch > 1 else
+                 "dpwa::k_lerp<Ops%s, COEF_FUSED, %s> (fused device factor + lerp%s)"
+                 % (args.dtype.upper(), "true" if wt_main else "false",
+                    " + write-through of the next snapshot" if wt_main else ""))
+        out = base_line(args, world)
+        out.update({
             "value": round(value, 2),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
             "dtype": "f32" if dtype == torch.float32 else "bf16",
-            "data": "synthetic N(0,1) flat parameter vectors (no dataset needed)",
             "config": {
                 "workload": ("%ssynthetic %d-element %s vector per learner%s, %s interpolation, "
                              "fetch_probability %g, divergence_threshold %g, %s loss, %s gossip rounds, %s publish"
@@ -886,6 +1289,8 @@ def main():
                 "learners_per_gpu": len(learners),
                 "numel": args.numel,
                 "publish": variant,
+                "averaging_dispatch": ("one batched dispatch per round for the %d co-resident learners" % per_launch
+                                       if per_launch > 1 else "one dispatch per learner per round"),
                 "transport": "in-place HBM read (co-resident peer)" if world == 1 else
                              "peer slot mapped into this process (hipIpc handle, or fds of hipMemCreate chunks from "
                              "1.5 GiB up) pulled over xGMI on a side stream (%s, %s rounds)"
@@ -893,6 +1298,7 @@ def main():
                 "parallelism": "gossip x%d" % int(rounds / args.steps),
                 "streams": args.streams,
             },
+            "value_basis": "the timed pass carries no instrumentation (no kernel timing, no events)",
             "gossip_rounds_per_s": round(rounds / elapsed, 1),
             "gossip_rounds_per_s_per_learner": round(rounds / elapsed / (rounds / args.steps), 1),
             "averagings": int(averaged),
@@ -903,13 +1309,13 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "dpwa::k_lerp<Ops%s, COEF_FUSED, %s> (fused device factor + lerp%s)"
-                          % (args.dtype.upper(), "true" if wt_main else "false",
-                             " + write-through of the next snapshot" if wt_main else ""),
+                "kernel": kname,
+                "learners_per_launch": per_launch,
                 "bytes_per_launch": kbytes,
-                "bytes_note": ("4*N*s: read parameters, read peer snapshot, write parameters, write the next "
-                               "snapshot (which the publish then does not copy)" if wt_main else
-                               "3*N*s: read parameters, read peer snapshot, write parameters"),
+                "bytes_note": (("%d x " % per_launch if per_launch > 1 else "") +
+                               ("4*N*s: read parameters, read peer snapshot, write parameters, write the next "
+                                "snapshot (which the publish then does not copy)" if wt_main else
+                                "3*N*s: read parameters, read peer snapshot, write parameters")),
                 "avg_launch_us": round(k_us, 2),
                 "basis": ("cold: the kernel alone over rotating buffers (> 1.2 GB between reuses, no "
                           "Infinity-Cache hits), every launch timed by its own dispatch begin/end events "
@@ -925,7 +1331,9 @@ def main():
                     "timing": ("kernel dispatch begin/end events (hipExtLaunchKernelGGL) on the averaging "
                                "kernel's own stream" if args.timing != "bracket" else
                                "HIP event pair recorded around the launch on its stream")
-                              + ", every %d-th step of the timed loop" % args.sample_every,
+                              + ", every %d-th step of a separate %d-step pass (not the timed one)"
+                              % (args.sample_every, s_steps),
+                    "sampled_pass_ms_per_step": round(1e3 * s_el / s_steps, 4),
                     "event_bracket_us": (round(float(np.nanmean(bracket_ms) * 1e3), 2)
                                          if args.timing != "dispatch" else None),
                     "note": ("inside the gossip round the peer snapshot was written just before the average and "
@@ -940,9 +1348,19 @@ def main():
                                         "source": "MI355X_MICROARCH.md: 6.29 TB/s measured for a float4 copy "
                                                   "(79 % of the 8 TB/s spec); peak above stays the spec"},
             },
-        }
+        })
+        if wt_main and args.numel == RESNET18_NUMEL and args.dtype == "f32":
+            out["roofline"]["vs_mix_ceiling"] = dict(MIX_CEILING_11M, kernel_frac_over_ceiling=round(
+                achieved / HBM_PEAK_GBS / MIX_CEILING_11M["frac"], 4),
+                note="the chip's cold ceiling for one 11.17M-element 2R:2W launch (single learner); a batched "
+                     "dispatch moves more bytes per ramp/drain, so it can exceed it")
         if pull_trials:
             out["pull_trials_gbs"] = pull_trials
+            out["pull_trials_median_gbs"] = {k: round(float(np.median(v)), 2) for k, v in pull_trials.items()}
+            out["pull_choice"] = {"chosen": pull, "rule": "highest median over %d interleaved passes, each trial >= "
+                                  "%g ms and >= 30 rounds" % (args.trial_passes, args.trial_ms)}
+        if trial_errors:
+            out["trial_errors"] = trial_errors
         if world > 1:
             pull_bytes = 256 + args.numel * esize
             p_us = pull_us[0] if pull_us and np.isfinite(pull_us[0]) else None
@@ -967,44 +1385,45 @@ def main():
                             "(barriers and the average included): a lower bound on the link rate",
                 }
         if secondary is not None:
-            s_wt, (w_el, w_avg, w_rounds, (w_ms, _)) = secondary
+            s_wt, (w_el, w_avg, w_rounds, _), (w_ms, _) = secondary
             w_us = float(np.nanmean(w_ms) * 1e3)
-            w_bytes = (4 if s_wt else 3) * args.numel * esize
+            w_bytes = (4 if s_wt else 3) * args.numel * esize * per_launch
             out["secondary_publish"] = {
                 "publish": "write-through" if s_wt else "full",
                 "value": round(w_avg * unit_bytes / w_el / 1e9, 2),
                 "ms_per_step": round(1e3 * w_el / args.steps, 4),
                 "avg_launch_us": round(w_us, 2),
                 "kernel_gbs": round(w_bytes / (w_us * 1e-6) / 1e9, 1),
-                "note": "the same rounds with the other publish form. write-through: the averaging kernel also "
-                        "writes the next snapshot (4*N*s) and the publish moves only the 256-B header; full: "
-                        "every publish copies the 2*N*s snapshot. Write-through is valid when nothing modifies "
-                        "the parameters between update_wait and the next update_send (the reference's loop, "
-                        "examples/pytorch-cifar/main.py:130-145); the adapter checks the parameters' version "
-                        "counters and storage before reusing a snapshot",
+                "note": "the same rounds with the other publish form (value from an uninstrumented pass, the kernel "
+                        "from a sampled one). write-through: the averaging kernel also writes the next snapshot "
+                        "(4*N*s) and the publish moves nothing; full: every publish copies the 2*N*s snapshot. "
+                        "Write-through is valid when nothing modifies the parameters between update_wait and the "
+                        "next update_send (the reference's loop, examples/pytorch-cifar/main.py:130-145); the "
+                        "adapter checks the parameters' version counters and storage before reusing a snapshot",
             }
         if overlap is not None:
             out["overlap"] = overlap
-        if world == 1 and not args.no_sweep:
-            progress("size sweep")
-            out["roofline"]["size_sweep"] = size_sweep(device)
-            progress("round sweep")
-            out["round_sweep"] = round_sweep(device, tmp)
+        if size_rows is not None:
+            out["roofline"]["size_sweep"] = size_rows
+        if round_rows is not None:
+            out["round_sweep"] = round_rows
         out["cpu_baseline"] = cpu
         if parity is not None:
             out["parity"] = parity
             out["parity_of_timed_transport"] = {"transport": used, "ok": bool(parity.get(used, False))}
         print(json.dumps(out), flush=True)
-    progress("done")
+    wd.enter("shutdown", 300.0)
     for conn, _ in lockstep_learners + async_learners:
         conn.close()
     if world > 1:
-        dist.barrier()
+        hbarrier()
         dist.destroy_process_group()
-    if parity is not None and not all(v for k, v in parity.items() if k != "workload"):
-        print("bench.py: parity check FAILED: %s" % {k: v for k, v in parity.items() if k != "workload"},
-              file=sys.stderr, flush=True)
-        if not parity.get(used, False):      # the number above came from an unverified transport
+    wd.idle()
+    progress("done")
+    if parity is not None:
+        failed = {k: v for k, v in parity.items() if k != "workload" and not v}
+        if failed:
+            print("bench.py: parity check FAILED: %s" % failed, file=sys.stderr, flush=True)
             sys.exit(1)
 
 

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("DPWA_HIP_LIB", os.path.join(_HERE, "libdpwa_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dpwa_hip.h")
 
 # Constants mirrored from include/dpwa_hip.h
-ABI_VERSION = 3
+ABI_VERSION = 4
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_NOMEM = 0, -1, -2, -3, -4
 F32, BF16, F64 = 0, 1, 2
 INTERP_CONSTANT, INTERP_CLOCK, INTERP_LOSS = 0, 1, 2
@@ -56,6 +56,12 @@ class Coef(ctypes.Structure):
                 ("b", ctypes.c_float), ("status", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class AverageDesc(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("peer_slot", ctypes.c_void_p), ("n", ctypes.c_int64),
+                ("clock_dev", ctypes.c_void_p), ("loss", ctypes.c_double), ("coef_dev", ctypes.c_void_p),
+                ("snap_payload", ctypes.c_void_p)]
+
+
 class Interp(ctypes.Structure):
     _fields_ = [("method", ctypes.c_int32), ("reserved", ctypes.c_int32), ("value", ctypes.c_double),
                 ("divergence_threshold", ctypes.c_double)]
@@ -79,6 +85,9 @@ SIGNATURES = {
     "dpwa_lerp_bf16_host": [_vp, _vp, _i64, _dbl, _vp],
     "dpwa_factor": [ctypes.POINTER(Interp), _vp, _vp, _dbl, _vp, _vp, _vp],
     "dpwa_average": [_i32, _vp, _vp, _i64, ctypes.POINTER(Interp), _vp, _dbl, _vp, _vp, _vp, _vp, _vp],
+    "dpwa_average_many": [_i32, _vp, _int, ctypes.POINTER(Interp), _vp, _vp, _vp],
+    "dpwa_learner_average_many": [_vp, _vp, _vp, _vp, _vp, _int, _vp],
+    "dpwa_learner_set_header_publish": [_vp, _int],
     "dpwa_learner_copy_factor": [_vp, _vp, _vp],
     "dpwa_learner_copy_fetched": [_vp, _vp, _vp],
     "dpwa_learner_create": [ctypes.POINTER(_vp), _int, _i64, _i32, ctypes.POINTER(Interp)],
@@ -147,6 +156,7 @@ SIGNATURES = {
     "dpwa_node_update_wait": [_vp, _dbl, _vp, _int, _vp, _pint],
     "dpwa_node_lerp": [_vp, _vp, _vp],
     "dpwa_node_update_wait_average": [_vp, _vp, _dbl, _vp, _int, _vp, _pint],
+    "dpwa_node_update_wait_average_many": [_vp, _vp, _vp, _vp, _int, _int, _vp, _vp],
     "dpwa_node_info": [_vp, _pint, _pint, ctypes.POINTER(_u64), _pint],
     "dpwa_sched_create": [ctypes.POINTER(_vp), _int, ctypes.POINTER(ctypes.c_uint32), _int, _dbl],
     "dpwa_sched_destroy": [_vp],

@@ -69,6 +69,28 @@ class DpwaPyTorchAdapter:
             self._versions = self._param_versions()
 
     # -- extensions -------------------------------------------------------------------
+    @staticmethod
+    def update_wait_many(adapters, losses):
+        """update_wait of several adapters whose models share a GPU (co-resident learners of
+        one process), in order, with their averages as one dispatch (same results as calling
+        update_wait on each)."""
+        adapters = list(adapters)
+        if not adapters:
+            return
+        wts = {a._write_through for a in adapters}
+        if len(wts) != 1 or any(not isinstance(a._conn, DpwaConnection) or type(a._conn) is not DpwaConnection
+                                for a in adapters):
+            for a, loss in zip(adapters, losses):     # mixed forms or wire peers: one by one
+                a.update_wait(loss)
+            return
+        wt = wts.pop()
+        res = DpwaConnection.update_wait_average_many([a._conn for a in adapters],
+                                                      [a._flat.buffer for a in adapters], list(losses),
+                                                      write_through=wt)
+        for a, (payload, _) in zip(adapters, res):
+            if wt and payload is not None:
+                a._versions = a._param_versions()
+
     @property
     def connection(self):
         return self._conn

@@ -311,9 +311,17 @@ class WireConnection(DpwaConnection):
         return PeerSnapshot(self, k, 0), DeviceFactor(self._learner)
 
     def _loss(self, loss):
-        from .learner import loss_args
-        h, d, self._learner._keep = loss_args(loss, self._learner.device)
+        # the learner's own conversion: it also sets the dtype flag the kernels read a device
+        # loss pointer with (a float32 loss tensor is read in place as float32)
+        h, d, self._learner._keep = self._learner.loss_args(loss)
         return h, d
+
+    def _bind(self, parameters):
+        learner = super()._bind(parameters)
+        # served snapshots carry the loss given to update_send (conn.py:110): a write-through
+        # average never writes the next header ahead with a placeholder loss
+        _lib.call("dpwa_learner_set_header_publish", learner.handle, 1)
+        return learner
 
     @property
     def last_fetch_peer(self):

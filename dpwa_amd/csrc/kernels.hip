@@ -286,13 +286,13 @@ struct StripeSrc {
 // DUAL also stores the result into args.snap (write-through snapshot: the next publish of
 // these parameters then needs no copy).  BLOCK lanes per workgroup (kStreamBlock).
 template <class Ops, int MODE, bool DUAL, int BLOCK, int POLICY, class Src>
-__device__ __forceinline__ void lerp_span(typename Ops::V *__restrict__ param, const Src &src, int64_t n,
-                                          const LerpArgs &args)
+__device__ __forceinline__ void lerp_span(uint32_t blk, typename Ops::V *__restrict__ param, const Src &src,
+                                          int64_t n, const LerpArgs &args)
 {
     using V = typename Ops::V;
     constexpr int SPAN = BLOCK * 16;
     const int64_t nv = n / Ops::PER;
-    const int64_t span_off = src.template span_of<SPAN>(blockIdx.x);
+    const int64_t span_off = src.template span_of<SPAN>(blk);
     const int lane_off = threadIdx.x * 16;
     const __amdgpu_buffer_rsrc_t rq = span_rsrc<SPAN>(src.span_base(span_off), span_off, nv * 16);
     const __amdgpu_buffer_rsrc_t rp = span_rsrc<SPAN>(param, span_off, nv * 16);
@@ -318,14 +318,14 @@ __device__ __forceinline__ void lerp_span(typename Ops::V *__restrict__ param, c
                 s_a = c.a;
                 s_b = c.b;
                 s_ok = c.status == DPWA_STATUS_OK;
-                if (blockIdx.x == 0) factor_commit(fa, c);
+                if (blk == 0) factor_commit(fa, c);
             }
         }
         __syncthreads();
         if (!s_ok) {          // no-op round; a write-through snapshot still gets the parameters
             if (DUAL)
                 span_store<V, LerpPolicy<POLICY>::snap_store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, p);
-            if (DUAL && blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
+            if (DUAL && blk == 0 && threadIdx.x < n - nv * Ops::PER) {
                 const int64_t j = nv * Ops::PER + threadIdx.x;
                 reinterpret_cast<typename Ops::S *>(args.snap)[j] = reinterpret_cast<typename Ops::S *>(param)[j];
             }
@@ -339,7 +339,7 @@ __device__ __forceinline__ void lerp_span(typename Ops::V *__restrict__ param, c
         span_store<V, LerpPolicy<POLICY>::store>(rp, lane_off, r);
         if (DUAL) span_store<V, LerpPolicy<POLICY>::snap_store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, r);
     }
-    if (blockIdx.x == 0 && threadIdx.x < n - nv * Ops::PER) {
+    if (blk == 0 && threadIdx.x < n - nv * Ops::PER) {
         using S = typename Ops::S;
         S *ps = reinterpret_cast<S *>(param);
         const int64_t j = nv * Ops::PER + threadIdx.x;
@@ -353,7 +353,7 @@ template <class Ops, int MODE, bool DUAL, int BLOCK = kBlock, int POLICY = 0>
 __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ param,
                                                 const typename Ops::V *__restrict__ peer, int64_t n, LerpArgs args)
 {
-    lerp_span<Ops, MODE, DUAL, BLOCK, POLICY>(param, ContigSrc{(const char *)peer}, n, args);
+    lerp_span<Ops, MODE, DUAL, BLOCK, POLICY>(blockIdx.x, param, ContigSrc{(const char *)peer}, n, args);
 }
 
 // The relay's fused second phase: the fused average reads the peer's snapshot stripe by stripe
@@ -363,7 +363,28 @@ template <class Ops, bool DUAL>
 __global__ __launch_bounds__(kStreamBlock) void k_lerp_relay(typename Ops::V *__restrict__ param, int64_t n,
                                                              LerpArgs args, StripeSrc src)
 {
-    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, 0>(param, src, n, args);
+    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, 0>(blockIdx.x, param, src, n, args);
+}
+
+// Several independent fused averages in ONE dispatch (co-resident learners of one round:
+// LocalGroup).  Entry i owns the workgroups [begin[i], begin[i+1]); each workgroup runs the
+// single-average span code for its entry, so the per-learner semantics (factor, clock commit by
+// the entry's first workgroup, ragged tail) are those of k_lerp.  One launch instead of one per
+// learner removes a ramp, a drain and a kernel boundary per extra learner.
+template <class Ops, bool DUAL>
+__global__ __launch_bounds__(kStreamBlock) void k_lerp_batch(AvgBatch batch)
+{
+    // the entry of this workgroup: a short scalar scan over the uniform begin[] table
+    int i = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxAvgBatch; ++k)
+        if (k < batch.count && blockIdx.x >= batch.begin[k]) i = k;
+    const AvgEntry &e = batch.e[i];
+    LerpArgs args{};
+    args.fused = e.fa;
+    args.snap = e.snap;
+    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, 0>(blockIdx.x - batch.begin[i], (typename Ops::V *)e.param,
+                                                      ContigSrc{(const char *)e.peer}, e.n, args);
 }
 
 // Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
@@ -512,6 +533,44 @@ hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t 
     args.fused = fa;
     args.snap = snap;
     return launch_any(dtype, COEF_FUSED, param, peer, n, args, s, timing);
+}
+
+hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hipStream_t s,
+                                 const LaunchTiming *timing)
+{
+    if (b.count < 1 || b.count > kMaxAvgBatch) return hipErrorInvalidValue;
+    AvgBatch x = b;
+    uint32_t g = 0;
+    const int per = dtype == DPWA_F32 ? OpsF32::PER : dtype == DPWA_BF16 ? OpsBF16::PER : 0;
+    if (!per) return hipErrorInvalidValue;
+    for (int i = 0; i < x.count; ++i) {
+        const AvgEntry &e = x.e[i];
+        if (e.n < 0 || !aligned16(e.param) || !aligned16(e.peer) || (dual != (e.snap != nullptr)) ||
+            !aligned16(e.snap))
+            return hipErrorInvalidValue;
+        x.begin[i] = g;
+        const int64_t gi = (e.n / per) / kStreamBlock + 1;   // as launch_blocks: last span may be empty
+        if ((int64_t)g + gi > 0x7fffffffLL) return hipErrorInvalidValue;
+        g += (uint32_t)gi;
+    }
+    for (int i = x.count; i < kMaxAvgBatch; ++i) x.begin[i] = 0xffffffffu;
+#define DPWA_BATCH_LAUNCH(OPS, DL)                                                                          \
+    do {                                                                                                    \
+        if (timing)                                                                                         \
+            hipExtLaunchKernelGGL((k_lerp_batch<OPS, DL>), dim3(g), dim3(kStreamBlock), 0, s, timing->start, \
+                                  timing->stop, 0, x);                                                      \
+        else                                                                                                \
+            hipLaunchKernelGGL((k_lerp_batch<OPS, DL>), dim3(g), dim3(kStreamBlock), 0, s, x);             \
+    } while (0)
+    if (dtype == DPWA_F32) {
+        if (dual) DPWA_BATCH_LAUNCH(OpsF32, true);
+        else DPWA_BATCH_LAUNCH(OpsF32, false);
+    } else {
+        if (dual) DPWA_BATCH_LAUNCH(OpsBF16, true);
+        else DPWA_BATCH_LAUNCH(OpsBF16, false);
+    }
+#undef DPWA_BATCH_LAUNCH
+    return hipGetLastError();
 }
 
 __global__ void k_acquire_system();

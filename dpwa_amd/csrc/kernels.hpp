@@ -53,6 +53,24 @@ struct LaunchTiming {
 hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa,
                           void *snap, hipStream_t s, const LaunchTiming *timing = nullptr);
 
+// Several fused averages (co-resident learners) in one dispatch: entry i's workgroups follow
+// entry i-1's.  Every pointer 16-B aligned; `dual` = every entry writes through (snap non-null).
+constexpr int kMaxAvgBatch = 8;
+struct AvgEntry {
+    void *param;
+    const void *peer;    // payload of the snapshot averaged with
+    void *snap;          // write-through destination, or null
+    int64_t n;
+    FusedArgs fa;
+};
+struct AvgBatch {
+    int32_t count;
+    uint32_t begin[kMaxAvgBatch];   // first workgroup of each entry (filled by the launcher)
+    AvgEntry e[kMaxAvgBatch];
+};
+hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hipStream_t s,
+                                const LaunchTiming *timing = nullptr);
+
 // Factor + clock only (one thread).
 hipError_t launch_factor(const FusedArgs &fa, hipStream_t s);
 

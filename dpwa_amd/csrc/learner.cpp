@@ -341,6 +341,7 @@ struct dpwa_learner {
     bool loss_f32 = false;              // device loss pointers point at a float32
     bool wt_valid = false;
     bool wt_header = false;             // the write-through average also wrote the next header
+    bool header_on_publish = false;     // never write the next header ahead (served to wire peers)
     const void *wt_flat = nullptr;
     hipStream_t wt_stream = nullptr;
     hipEvent_t ev_wt = nullptr;
@@ -861,6 +862,7 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
 }
 
 static int relay_materialize(dpwa_learner *l);
+static hipError_t staging_read(dpwa_learner *l, hipStream_t s);
 
 static FusedArgs fused_args(dpwa_learner *l, double loss, const double *loss_dev)
 {
@@ -889,6 +891,7 @@ int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dp
     if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
     HIP_TRY(launch_factor(fused_args(l, loss, loss_dev), s));
     HIP_TRY(hipEventRecord(l->ev_factor, s));
+    HIP_TRY(staging_read(l, s));   // a later pull into this staging buffer waits for the header read
     l->consume_stream = s;   // the header has been read on s
     l->consumed_once = true;
     l->cur = (l->cur + 1) & 3;
@@ -926,56 +929,147 @@ int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream)
     return DPWA_OK;
 }
 
-static int average_impl(dpwa_learner *l, void *flat, double loss, const double *loss_dev, hipStream_t s,
-                        bool write_through)
+// One fused average, split so that several learners' averages can share a dispatch:
+// average_prepare orders `s` after everything the kernel reads or overwrites and builds its
+// arguments; the caller launches; average_commit does the learner's bookkeeping.
+struct AvgPlan {
+    void *flat = nullptr;
+    const char *peer = nullptr;   // payload averaged with (contiguous source)
+    char *snap = nullptr;         // write-through destination
+    FusedArgs fa{};
+    bool relay = false;           // the relay's phase 2 fused into this average (k_lerp_relay)
+    bool write_through = false;
+};
+
+static int average_prepare(dpwa_learner *l, void *flat, double loss, const double *loss_dev, hipStream_t s,
+                           bool write_through, AvgPlan &p)
 {
     if (!l->have_fetch || l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_average: no fetch in flight");
-    char *snap = nullptr;
-    FusedArgs fa = fused_args(l, loss, loss_dev);
+    p = AvgPlan();
+    p.flat = flat;
+    p.write_through = write_through;
+    p.fa = fused_args(l, loss, loss_dev);
     if (write_through) {
         const int k = (int)(l->version % 2);   // slot of the next publish
         int rc = wait_slot_readers(l, k, s);
         if (rc) return rc;
-        snap = l->slots + (size_t)k * l->slot_stride + kPayloadOff;
-        if (l->cfg.method != DPWA_INTERP_LOSS) {   // peers never read this header's loss
-            fa.next_header = (dpwa_header *)(snap - kPayloadOff);
-            fa.clock_next = &l->ctl->clock[(l->cur + 2) & 3];
-            fa.next_version = l->version + 1;
-            fa.n = l->n;
-            fa.dtype = l->dtype;
+        p.snap = l->slots + (size_t)k * l->slot_stride + kPayloadOff;
+        if (l->cfg.method != DPWA_INTERP_LOSS && !l->header_on_publish) {   // peers never read this header's loss
+            p.fa.next_header = (dpwa_header *)(p.snap - kPayloadOff);
+            p.fa.clock_next = &l->ctl->clock[(l->cur + 2) & 3];
+            p.fa.next_version = l->version + 1;
+            p.fa.n = l->n;
+            p.fa.dtype = l->dtype;
         }
     }
-    if (l->relay_deferred && (((uintptr_t)flat | (uintptr_t)snap) & 15) == 0) {
+    if (l->relay_deferred && (((uintptr_t)flat | (uintptr_t)p.snap) & 15) == 0) {
         // the relay's phase 2 fused into the average: stripes read where phase 1 left them
         const RelayArgs &a = l->relay_saved;
-        fa.hdr = (const dpwa_header *)(a.slots[l->relay_saved_pick] + a.slot_off);
+        p.fa.hdr = (const dpwa_header *)(a.slots[l->relay_saved_pick] + a.slot_off);
         HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));
-        const LaunchTiming *timing = nullptr;
-        if (l->timing_armed && l->timing_used < (int)l->timing.size())
-            timing = &l->timing[l->timing_used++];
-        HIP_TRY(launch_average_relay(l->dtype, flat, l->n, fa, snap, a, l->relay_saved_pick, s, timing));
-        HIP_TRY(hipEventRecord(l->ev_relay, s));   // the next round's barrier waits for these reads
-        l->relay_pending = true;
-        l->relay_deferred = false;
+        p.relay = true;
     } else {
         int rc = relay_materialize(l);
         if (rc) return rc;
         if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));   // TxThread.fetch_wait
-        const LaunchTiming *timing = nullptr;
-        if (l->timing_armed && l->timing_used < (int)l->timing.size() && ((uintptr_t)flat & 15) == 0)
-            timing = &l->timing[l->timing_used++];
-        HIP_TRY(launch_average(l->dtype, flat, l->src + kPayloadOff, l->n, fa, snap, s, timing));
+        p.peer = l->src + kPayloadOff;
+    }
+    return DPWA_OK;
+}
+
+static const LaunchTiming *take_timing(dpwa_learner *l)
+{
+    if (l->timing_armed && l->timing_used < (int)l->timing.size()) return &l->timing[l->timing_used++];
+    return nullptr;
+}
+
+static int average_commit(dpwa_learner *l, const AvgPlan &p, hipStream_t s)
+{
+    if (p.relay) {
+        HIP_TRY(hipEventRecord(l->ev_relay, s));   // the next round's barrier waits for these reads
+        l->relay_pending = true;
+        l->relay_deferred = false;
+    } else {
         HIP_TRY(staging_read(l, s));
     }
     l->timing_armed = false;
     l->consume_stream = s;
     l->consumed_once = true;
     l->cur = (l->cur + 1) & 3;
-    l->wt_valid = write_through;
-    l->wt_header = fa.next_header != nullptr;
-    l->wt_flat = flat;
+    l->wt_valid = p.write_through;
+    l->wt_header = p.fa.next_header != nullptr;
+    l->wt_flat = p.flat;
     l->wt_stream = s;
     finish_fetch(l);
+    return DPWA_OK;
+}
+
+static int average_launch(dpwa_learner *l, const AvgPlan &p, hipStream_t s)
+{
+    if (p.relay) {
+        HIP_TRY(launch_average_relay(l->dtype, p.flat, l->n, p.fa, p.snap, l->relay_saved, l->relay_saved_pick, s,
+                                     take_timing(l)));
+    } else {
+        const LaunchTiming *timing = ((uintptr_t)p.flat & 15) == 0 ? take_timing(l) : nullptr;
+        HIP_TRY(launch_average(l->dtype, p.flat, p.peer, l->n, p.fa, p.snap, s, timing));
+    }
+    return DPWA_OK;
+}
+
+static int average_impl(dpwa_learner *l, void *flat, double loss, const double *loss_dev, hipStream_t s,
+                        bool write_through)
+{
+    AvgPlan p;
+    int rc = average_prepare(l, flat, loss, loss_dev, s, write_through, p);
+    if (rc) return rc;
+    if ((rc = average_launch(l, p, s))) return rc;
+    return average_commit(l, p, s);
+}
+
+// Can plan p join a batched dispatch (k_lerp_batch)?  Contiguous source, 16-B aligned operands.
+static bool batchable(const AvgPlan &p)
+{
+    return !p.relay && ((((uintptr_t)p.flat | (uintptr_t)p.peer | (uintptr_t)p.snap) & 15) == 0);
+}
+
+// Launches the batchable plans in groups of the same (dtype, write-through), up to
+// kMaxAvgBatch per dispatch, and every other plan on its own.  Timed like a single average:
+// the first armed learner of a dispatch lends it its timing pair.
+static int launch_plans(dpwa_learner *const *ls, const AvgPlan *plans, const int *idx, int count, hipStream_t s)
+{
+    std::vector<char> done((size_t)count, 0);
+    for (int a = 0; a < count; ++a) {
+        if (done[a]) continue;
+        const int ia = idx[a];
+        dpwa_learner *la = ls[ia];
+        const AvgPlan &pa = plans[ia];
+        done[a] = 1;
+        if (!batchable(pa)) {
+            int rc = average_launch(la, pa, s);
+            if (rc) return rc;
+            continue;
+        }
+        AvgBatch b{};
+        const LaunchTiming *timing = take_timing(la);
+        auto add = [&](dpwa_learner *l, const AvgPlan &p) {
+            AvgEntry &e = b.e[b.count++];
+            e.param = p.flat;
+            e.peer = p.peer;
+            e.snap = p.snap;
+            e.n = l->n;
+            e.fa = p.fa;
+        };
+        add(la, pa);
+        for (int c = a + 1; c < count && b.count < kMaxAvgBatch; ++c) {
+            const int ic = idx[c];
+            if (done[c] || !batchable(plans[ic]) || ls[ic]->dtype != la->dtype || plans[ic].write_through != pa.write_through)
+                continue;
+            if (!timing) timing = take_timing(ls[ic]);
+            add(ls[ic], plans[ic]);
+            done[c] = 1;
+        }
+        HIP_TRY(launch_average_batch(la->dtype, pa.snap != nullptr, b, s, timing));
+    }
     return DPWA_OK;
 }
 
@@ -992,6 +1086,76 @@ int dpwa_learner_average_through(dpwa_learner *l, void *flat, double loss, const
     if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_average_through: NULL argument");
     DeviceGuard dg(l->device);
     return average_impl(l, flat, loss, loss_dev, (hipStream_t)stream, true);
+}
+
+int dpwa_learner_average_many(dpwa_learner *const *ls, void *const *flats, const double *loss,
+                              const double *const *loss_dev, const int *write_through, int count, dpwa_stream_t stream)
+{
+    if (count < 0 || (count > 0 && (!ls || !flats || !loss || !write_through)))
+        return set_error(DPWA_ERR_ARG, "dpwa_learner_average_many: bad arguments");
+    if (count == 0) return DPWA_OK;
+    for (int i = 0; i < count; ++i) {
+        if (!ls[i] || (!flats[i] && ls[i]->n > 0))
+            return set_error(DPWA_ERR_ARG, "dpwa_learner_average_many: NULL learner or buffer at %d", i);
+        if (ls[i]->device != ls[0]->device)
+            return set_error(DPWA_ERR_ARG, "dpwa_learner_average_many: learners on devices %d and %d share one stream",
+                             ls[0]->device, ls[i]->device);
+        for (int j = 0; j < i; ++j)
+            if (ls[j] == ls[i]) return set_error(DPWA_ERR_ARG, "dpwa_learner_average_many: learner %d given twice", i);
+    }
+    DeviceGuard dg(ls[0]->device);
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<AvgPlan> plans((size_t)count);
+    std::vector<int> idx;
+    idx.reserve((size_t)count);
+    for (int i = 0; i < count; ++i) {
+        int rc = average_prepare(ls[i], flats[i], loss[i], loss_dev ? loss_dev[i] : nullptr, s, write_through[i] != 0,
+                                 plans[i]);
+        if (rc) return rc;   // nothing launched yet for this learner; earlier ones are prepared only
+        idx.push_back(i);
+    }
+    int rc = launch_plans(ls, plans.data(), idx.data(), count, s);
+    if (rc) return rc;
+    for (int i = 0; i < count; ++i)
+        if ((rc = average_commit(ls[i], plans[i], s))) return rc;
+    return DPWA_OK;
+}
+
+int dpwa_average_many(int32_t dtype, const dpwa_average_desc *descs, int count, const dpwa_interp *cfg,
+                      dpwa_stream_t stream, void *start_event, void *stop_event)
+{
+    if (count < 1 || count > kMaxAvgBatch || !descs || !cfg || dtype_size(dtype) == 0 || (!start_event) != (!stop_event))
+        return set_error(DPWA_ERR_ARG, "dpwa_average_many: bad arguments (1..%d descriptors)", kMaxAvgBatch);
+    if (cfg->method < 0 || cfg->method > 2) return set_error(DPWA_ERR_ARG, "dpwa_average_many: unknown method %d", cfg->method);
+    AvgBatch b{};
+    const bool dual = descs[0].snap_payload != nullptr;
+    for (int i = 0; i < count; ++i) {
+        const dpwa_average_desc &d = descs[i];
+        if (!d.param || !d.peer_slot || !d.clock_dev || !d.coef_dev || d.n < 0 || (d.snap_payload != nullptr) != dual ||
+            (((uintptr_t)d.param | (uintptr_t)d.peer_slot | (uintptr_t)d.snap_payload) & 15))
+            return set_error(DPWA_ERR_ARG, "dpwa_average_many: descriptor %d: NULL, unaligned or mixed write-through", i);
+        AvgEntry &e = b.e[b.count++];
+        e.param = d.param;
+        e.peer = (const char *)d.peer_slot + kPayloadOff;
+        e.snap = d.snap_payload;
+        e.n = d.n;
+        e.fa.cfg = *cfg;
+        e.fa.clock_in = d.clock_dev;
+        e.fa.clock_out = d.clock_dev + 1;
+        e.fa.hdr = (const dpwa_header *)d.peer_slot;
+        e.fa.loss_h = d.loss;
+        e.fa.coef_out = d.coef_dev;
+    }
+    LaunchTiming t{(hipEvent_t)start_event, (hipEvent_t)stop_event};
+    HIP_TRY(launch_average_batch(dtype, dual, b, (hipStream_t)stream, start_event ? &t : nullptr));
+    return DPWA_OK;
+}
+
+int dpwa_learner_set_header_publish(dpwa_learner *l, int always)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_set_header_publish: NULL learner");
+    l->header_on_publish = always != 0;
+    return DPWA_OK;
 }
 
 int dpwa_learner_read_snapshot(dpwa_learner *l, void *header_out, void *payload_out, int64_t payload_bytes,
@@ -1386,6 +1550,7 @@ int dpwa_learner_copy_fetched(dpwa_learner *l, void *dst_dev, dpwa_stream_t stre
     if (l->src_copied) HIP_TRY(hipStreamWaitEvent(s, l->ev_fetched, 0));
     if (l->payload_bytes)
         HIP_TRY(hipMemcpyAsync(dst_dev, l->src + kPayloadOff, l->payload_bytes, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(staging_read(l, s));   // a later pull into this staging buffer waits for this copy
     l->consume_stream = s;   // the staging buffer / peer slot is read on s
     l->consumed_once = true;
     return DPWA_OK;

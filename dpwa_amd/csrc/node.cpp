@@ -360,6 +360,38 @@ int dpwa_node_update_wait_average(dpwa_node *n, void *flat, double loss, const d
     return dpwa_learner_average(n->learner, flat, loss, loss_dev, stream);
 }
 
+int dpwa_node_update_wait_average_many(dpwa_node *const *nodes, void *const *flats, const double *loss,
+                                       const double *const *loss_dev, int count, int flags, dpwa_stream_t stream,
+                                       int *peers)
+{
+    if (count < 0 || (count > 0 && (!nodes || !flats || !loss || !peers)))
+        return set_error(DPWA_ERR_ARG, "dpwa_node_update_wait_average_many: bad arguments");
+    std::vector<dpwa_learner *> ls;
+    std::vector<void *> fl;
+    std::vector<double> lo;
+    std::vector<const double *> ld;
+    std::vector<int> wt;
+    const bool through = (flags & DPWA_FLAG_WRITE_THROUGH) != 0;
+    for (int i = 0; i < count; ++i) peers[i] = -1;
+    for (int i = 0; i < count; ++i) {
+        dpwa_node *n = nodes[i];
+        if (!n || !n->learner) return set_error(DPWA_ERR_STATE, "dpwa_node_update_wait_average_many: node %d not bound", i);
+        int rc = finish_fetch(n, flags, stream, &peers[i]);   // dpwa.py:130-137, node by node
+        if (rc) return rc;
+        if (peers[i] < 0) continue;
+        if (through && n->board &&
+            (rc = dpwa_board_publish_wait(n->board, learner_version(n->learner) + 1, n->publish_timeout_ms)))
+            return rc;
+        ls.push_back(n->learner);
+        fl.push_back(flats[i]);
+        lo.push_back(loss[i]);
+        ld.push_back(loss_dev ? loss_dev[i] : nullptr);
+        wt.push_back(through ? 1 : 0);
+    }
+    if (ls.empty()) return DPWA_OK;
+    return dpwa_learner_average_many(ls.data(), fl.data(), lo.data(), ld.data(), wt.data(), (int)ls.size(), stream);
+}
+
 int dpwa_node_info(const dpwa_node *n, int *fetching, int *fetch_peer, uint64_t *fetch_version, int *last_attempts)
 {
     if (!n) return set_error(DPWA_ERR_ARG, "dpwa_node_info: NULL node");

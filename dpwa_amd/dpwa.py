@@ -345,6 +345,58 @@ class DpwaConnection:
         return self._result()
 
     # ---------------------------------------------------------------- extensions
+    @staticmethod
+    def update_wait_average_many(conns, parameters, losses, write_through=False):
+        """update_wait_average of several connections of this process whose learners share a
+        GPU (co-resident learners of a LocalGroup), in the given order: each fetch is resolved
+        as the single calls would resolve it, and the averages run as ONE dispatch instead of
+        one per learner (same results; a kernel boundary and a launch ramp/drain fewer per
+        extra learner).  Returns the list of what update_wait returns, per connection."""
+        conns, parameters, losses = list(conns), list(parameters), list(losses)
+        if not (len(conns) == len(parameters) == len(losses)):
+            raise ValueError("update_wait_average_many: %d connections, %d buffers, %d losses"
+                             % (len(conns), len(parameters), len(losses)))
+        bound = [i for i, c in enumerate(conns) if c._learner is not None]
+        out = [(None, 0)] * len(conns)
+        if not bound:
+            return out
+        dev = conns[bound[0]]._learner.device
+        k = len(bound)
+        nodes, flats = (ctypes.c_void_p * k)(), (ctypes.c_void_p * k)()
+        hs, ds = (ctypes.c_double * k)(), (ctypes.c_void_p * k)()
+        keep = []
+        flags = 0
+        for j, i in enumerate(bound):
+            c = conns[i]
+            learner = c._learner
+            if learner.device != dev:
+                raise ValueError("update_wait_average_many: learners on %s and %s" % (dev, learner.device))
+            if learner.take_status():
+                c._zero_division()
+            flats[j] = learner._ptr(parameters[i])
+            h, d, learner._keep = learner.loss_args(losses[i])
+            keep.append(learner._keep)
+            hs[j] = h
+            ds[j] = d.value if d is not None else None
+            nodes[j] = c._node.value
+            flags |= c._flags
+        flags |= _lib.FLAG_WRITE_THROUGH if write_through else 0
+        peers = (ctypes.c_int * k)()
+        lib = conns[bound[0]]._lib
+        rc = lib.dpwa_node_update_wait_average_many(nodes, flats, hs, ds, k, flags,
+                                                     ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(dev.index)),
+                                                     peers)
+        for j, i in enumerate(bound):
+            conns[i].fetching = False
+        if rc:
+            raise _lib.DpwaError("dpwa_node_update_wait_average_many", rc,
+                                 lib.dpwa_last_error().decode(errors="replace"))
+        for j, i in enumerate(bound):
+            c = conns[i]
+            if peers[j] >= 0:
+                out[i] = (PeerSnapshot(c, peers[j], c._learner.version), DeviceFactor(c._learner))
+        return out
+
     @property
     def clock(self):
         """The learner's clock (dpwa.py:59); reading it synchronises with the device."""

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DPWA_ABI_VERSION 3
+#define DPWA_ABI_VERSION 4
 
 #define DPWA_OK 0
 #define DPWA_ERR_ARG (-1)     /* bad argument (API misuse)                          */
@@ -119,6 +119,23 @@ int dpwa_average(int32_t dtype, void *param, const void *peer_slot, int64_t n, c
                  double *clock_dev, double loss, dpwa_coef *coef_dev, void *snap_payload, dpwa_stream_t stream,
                  void *start_event, void *stop_event);
 
+/* dpwa_average over several independent (param, peer slot) pairs in ONE dispatch -- the averages
+ * of co-resident learners of one round (pytorch.py:66-68 once per learner).  Each descriptor is
+ * one dpwa_average call: its own clock_dev (reads [0], writes [1]), coefficient block and loss;
+ * all share `cfg` and `dtype`, and either all or none write through (snap_payload).  Every
+ * pointer 16-B aligned; 1..8 descriptors.  Events as dpwa_average (the whole dispatch). */
+typedef struct dpwa_average_desc {
+    void *param;
+    const void *peer_slot;   /* [dpwa_header | pad | payload] */
+    int64_t n;
+    double *clock_dev;
+    double loss;
+    dpwa_coef *coef_dev;
+    void *snap_payload;      /* NULL, or n elements: the write-through destination */
+} dpwa_average_desc;
+int dpwa_average_many(int32_t dtype, const dpwa_average_desc *descs, int count, const dpwa_interp *cfg,
+                      dpwa_stream_t stream, void *start_event, void *stop_event);
+
 /* Factor + clock on the device (dpwa.py:139-155 + interpolation.py): reads *clock_dev and the
  * peer's header, writes *coef_dev and, unless the status is an error, *clock_dev = new_clock.
  * `loss` is used when loss_dev is NULL, else *loss_dev (a device float64). */
@@ -187,6 +204,17 @@ int dpwa_learner_average(dpwa_learner *l, void *flat, double loss, const double 
  * publish (4*n*s bytes instead of 3*n*s here, and that publish then moves no payload). */
 int dpwa_learner_average_through(dpwa_learner *l, void *flat, double loss, const double *loss_dev,
                                  dpwa_stream_t stream);
+/* The averages of `count` learners of one device (each with a fetch in flight) as few
+ * dispatches as possible: every learner's dpwa_learner_average(_through) (write_through[i]),
+ * same results and bookkeeping, but compatible ones (same dtype and form, 16-B aligned,
+ * contiguous source) share one launch of up to 8.  loss_dev may be NULL (all host losses). */
+int dpwa_learner_average_many(dpwa_learner *const *learners, void *const *flats, const double *loss,
+                              const double *const *loss_dev, const int *write_through, int count,
+                              dpwa_stream_t stream);
+/* always != 0: a write-through average never writes the next publish's header ahead; that
+ * publish then writes it with the loss given to it (a snapshot served over the wire bridge
+ * carries the reference's {'clock', 'loss'} state, conn.py:110). */
+int dpwa_learner_set_header_publish(dpwa_learner *l, int always);
 /* Publish that reuses a write-through snapshot when the last average wrote `flat` through
  * (the caller asserts `flat` is unchanged since): header only; otherwise a full publish. */
 int dpwa_learner_publish_reuse(dpwa_learner *l, const void *flat, double loss, const double *loss_dev,
@@ -402,6 +430,12 @@ int dpwa_node_update_wait(dpwa_node *n, double loss, const double *loss_dev, int
 int dpwa_node_lerp(dpwa_node *n, void *flat, dpwa_stream_t stream);
 int dpwa_node_update_wait_average(dpwa_node *n, void *flat, double loss, const double *loss_dev,
                                   int flags, dpwa_stream_t stream, int *peer);
+/* update_wait_average of `count` nodes of this process whose learners share a device, in node
+ * order (each node's fetch is resolved in turn, as `count` calls would), with their averages
+ * enqueued as one batched dispatch (dpwa_learner_average_many).  peers[i] as *peer above. */
+int dpwa_node_update_wait_average_many(dpwa_node *const *nodes, void *const *flats, const double *loss,
+                                       const double *const *loss_dev, int count, int flags,
+                                       dpwa_stream_t stream, int *peers);
 /* State of the current/last round: fetching flag, fetched peer (-1: none), its publish
  * number, and the picks the last fetch took. */
 int dpwa_node_info(const dpwa_node *n, int *fetching, int *fetch_peer, uint64_t *fetch_version,
