@@ -545,7 +545,7 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
     if (!per) return hipErrorInvalidValue;
     for (int i = 0; i < x.count; ++i) {
         const AvgEntry &e = x.e[i];
-        if (e.n < 0 || !aligned16(e.param) || !aligned16(e.peer) || (dual != (e.snap != nullptr)) ||
+        if (e.n < 0 || !aligned16(e.param) || !aligned16(e.peer) || (!dual && e.snap) || (dual && !e.snap && e.n > 0) ||
             !aligned16(e.snap))
             return hipErrorInvalidValue;
         x.begin[i] = g;

@@ -1068,7 +1068,7 @@ static int launch_plans(dpwa_learner *const *ls, const AvgPlan *plans, const int
             add(ls[ic], plans[ic]);
             done[c] = 1;
         }
-        HIP_TRY(launch_average_batch(la->dtype, pa.snap != nullptr, b, s, timing));
+        HIP_TRY(launch_average_batch(la->dtype, pa.write_through, b, s, timing));
     }
     return DPWA_OK;
 }
@@ -1128,10 +1128,12 @@ int dpwa_average_many(int32_t dtype, const dpwa_average_desc *descs, int count, 
         return set_error(DPWA_ERR_ARG, "dpwa_average_many: bad arguments (1..%d descriptors)", kMaxAvgBatch);
     if (cfg->method < 0 || cfg->method > 2) return set_error(DPWA_ERR_ARG, "dpwa_average_many: unknown method %d", cfg->method);
     AvgBatch b{};
-    const bool dual = descs[0].snap_payload != nullptr;
+    bool dual = false;   // an empty entry may pass no buffers at all
+    for (int i = 0; i < count; ++i) dual = dual || descs[i].snap_payload != nullptr;
     for (int i = 0; i < count; ++i) {
         const dpwa_average_desc &d = descs[i];
-        if (!d.param || !d.peer_slot || !d.clock_dev || !d.coef_dev || d.n < 0 || (d.snap_payload != nullptr) != dual ||
+        if ((!d.param && d.n > 0) || !d.peer_slot || !d.clock_dev || !d.coef_dev || d.n < 0 ||
+            (d.snap_payload == nullptr && d.n > 0 && dual) ||
             (((uintptr_t)d.param | (uintptr_t)d.peer_slot | (uintptr_t)d.snap_payload) & 15))
             return set_error(DPWA_ERR_ARG, "dpwa_average_many: descriptor %d: NULL, unaligned or mixed write-through", i);
         AvgEntry &e = b.e[b.count++];
