@@ -65,6 +65,15 @@ MIX_CEILING_11M = {"mix": "2R:2W", "frac": 0.759, "source": "profiles/r02_stream
 
 
 _T0 = time.perf_counter()
+_RESULT_FD = 1       # where the one result line goes (main() moves everything else off stdout)
+
+
+def emit(line):
+    """Writes the result line to the real stdout (a dup of fd 1 taken at start-up: libraries'
+    banners -- gloo's "[Gloo] Rank k is connected", RCCL's -- were moved to stderr)."""
+    data = (line + "\n").encode()
+    while data:
+        data = data[os.write(_RESULT_FD, data):]
 
 
 def progress(msg):
@@ -176,16 +185,20 @@ def self_launch(args, argv):
     timer.daemon = True
     timer.start()
     got = False
-    for line in p.stdout:
-        sys.stdout.write(line)
-        sys.stdout.flush()
-        got = got or (line.lstrip().startswith("{") and '"metric"' in line)
+    for line in p.stdout:   # the result line to stdout, anything else the ranks print to stderr
+        if line.lstrip().startswith("{") and '"metric"' in line:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            got = True
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
     rc = p.wait()
     timer.cancel()
     if not got:
         out = base_line(args, args.gpus)
         out["error"] = "torch.distributed.run exited with %d without a result line" % rc
-        print(json.dumps(out), flush=True)
+        emit(json.dumps(out))
         rc = rc or 1
     return rc
 
@@ -234,8 +247,7 @@ class Watchdog:
                 if transport is not None:
                     parity[transport] = False
                 out["parity"] = parity
-                sys.stdout.write(json.dumps(out) + "\n")
-                sys.stdout.flush()
+                emit(json.dumps(out))
             faulthandler.dump_traceback(all_threads=True)
             sys.stderr.flush()
             os._exit(3)
@@ -829,6 +841,12 @@ def main(argv=None):
         # no launcher: start one as a child process before anything touches a GPU
         sys.exit(self_launch(args, argv))
     world = world or 1
+    # stdout carries exactly one line: keep a dup of it for emit() and send everything else that
+    # writes to fd 1 (print, C++ libraries) to stderr
+    global _RESULT_FD
+    sys.stdout.flush()
+    _RESULT_FD = os.dup(1)
+    os.dup2(2, 1)
     # a rank stopped from outside (the launcher after another rank failed, a time limit) prints
     # where every thread was before it goes
     import faulthandler
@@ -1136,7 +1154,7 @@ def main(argv=None):
                 out["error"] = "no transport passed the parity check and its trials"
                 out["parity"] = parity
                 out["trial_errors"] = trial_errors
-                print(json.dumps(out), flush=True)
+                emit(json.dumps(out))
             sys.exit(1)
         pull = max(medians, key=medians.get)
         if pull.startswith("async/"):
@@ -1411,7 +1429,7 @@ def main(argv=None):
         if parity is not None:
             out["parity"] = parity
             out["parity_of_timed_transport"] = {"transport": used, "ok": bool(parity.get(used, False))}
-        print(json.dumps(out), flush=True)
+        emit(json.dumps(out))
     wd.enter("shutdown", 300.0)
     for conn, _ in lockstep_learners + async_learners:
         conn.close()

@@ -30,6 +30,8 @@ REPLY_PAYLOAD, REPLY_EMPTY, REPLY_TIMEOUT, REPLY_ERROR = 3, 4, 5, 6
 PEER_READY, PEER_NO_STATE, PEER_DOWN, PEER_SLOW, PEER_DEAD = 0, 1, 2, 3, 4
 NODE_PEER_UNSET, NODE_PEER_LOCAL, NODE_PEER_REMOTE = 0, 1, 2
 PULL_COPY_ENGINE, PULL_KERNEL = 0, 1
+FETCH_ZERO_COPY, FETCH_PUBLISHED, FETCH_RESCUE = 1, 2, 4
+FETCH_LANDED, FETCH_IN_FLIGHT, FETCH_TIMED_OUT = 0, 1, 2
 FLAG_EAGER, FLAG_ZERO_COPY, FLAG_REUSE_SNAPSHOT, FLAG_WRITE_THROUGH, FLAG_PICK_ONLY = 1, 2, 4, 8, 16
 
 
@@ -88,6 +90,9 @@ SIGNATURES = {
     "dpwa_average_many": [_i32, _vp, _int, ctypes.POINTER(Interp), _vp, _vp, _vp],
     "dpwa_learner_average_many": [_vp, _vp, _vp, _vp, _vp, _int, _vp],
     "dpwa_learner_set_header_publish": [_vp, _int],
+    "dpwa_learner_fetch_state": [_vp, _i64, _pint],
+    "dpwa_learner_rescue_free": [_vp, _pint],
+    "dpwa_learner_fetch_stream": [_vp, ctypes.POINTER(_vp)],
     "dpwa_learner_copy_factor": [_vp, _vp, _vp],
     "dpwa_learner_copy_fetched": [_vp, _vp, _vp],
     "dpwa_learner_create": [ctypes.POINTER(_vp), _int, _i64, _i32, ctypes.POINTER(Interp)],
@@ -139,6 +144,7 @@ SIGNATURES = {
     "dpwa_node_set_peer": [_vp, _int, _int, _vp],
     "dpwa_node_set_fault": [_vp, _int, _int],
     "dpwa_node_set_board": [_vp, _vp, ctypes.POINTER(_i32), _int],
+    "dpwa_node_set_timeout": [_vp, _int],
     "dpwa_board_open": [ctypes.POINTER(_vp), ctypes.c_char_p, _int, _int, _int],
     "dpwa_board_unlink": [ctypes.c_char_p],
     "dpwa_board_close": [_vp],

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -329,8 +330,16 @@ struct dpwa_learner {
     // the average that last read its buffer (ev_stage_done), so a pull starts at update_send
     // instead of after the caller's queued work, and a peer's read mark is released sooner.
     char *staging_alt = nullptr;        // second staging buffer, allocated at the first such fetch
-    hipEvent_t ev_stage_done[2] = {nullptr, nullptr};
-    bool stage_read[2] = {false, false};
+    // [2]: the rescue buffer (a fetch re-selected after a timed-out pull, conn.py:304-309),
+    // pulled on its own stream so a stalled pull ahead of it cannot hold it up
+    hipEvent_t ev_stage_done[3] = {nullptr, nullptr, nullptr};
+    bool stage_read[3] = {false, false, false};
+    char *rescue_buf = nullptr;
+    hipStream_t rescue_stream = nullptr;
+    hipEvent_t ev_rescue = nullptr;     // the last rescue pull landed
+    bool rescue_used = false;
+    int64_t fetch_issue_ns = 0;         // host time the fetch in flight was issued (its timeout clock)
+    hipStream_t fetch_stream = nullptr; // stream the fetch in flight moves its bytes on
     int stage_next = 0;
     int src_stage = -1;                 // staging buffer (0 / 1) l->src points into, -1: none
     hipEvent_t ev_factor = nullptr;     // last factor computation done
@@ -388,6 +397,12 @@ struct dpwa_learner {
     int32_t *host_status = nullptr;     // pinned mirror of coef.status for non-blocking polls
     int32_t *host_status_dev = nullptr; // its device-side address
 };
+
+static int64_t now_ns()
+{
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 static bool is_live(dpwa_learner *l)
 {
@@ -549,6 +564,9 @@ int dpwa_learner_destroy(dpwa_learner *l)
     for (auto ev : l->ev_stage_done)
         if (ev) (void)hipEventDestroy(ev);
     if (l->staging_alt) (void)hipFree(l->staging_alt);
+    if (l->rescue_buf) (void)hipFree(l->rescue_buf);
+    if (l->rescue_stream) (void)hipStreamDestroy(l->rescue_stream);
+    if (l->ev_rescue) (void)hipEventDestroy(l->ev_rescue);
     if (l->ev_factor) (void)hipEventDestroy(l->ev_factor);
     if (l->ev_wt) (void)hipEventDestroy(l->ev_wt);
     if (l->ev_read) (void)hipEventDestroy(l->ev_read);
@@ -804,7 +822,36 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
         auto &rv = ep.local->readers[k];
         if (std::find(rv.begin(), rv.end(), l) == rv.end()) rv.push_back(l);
     }
-    if (zero_copy && ep.kind == 1 && ep.device == l->device) {
+    l->fetch_issue_ns = now_ns();
+    l->fetch_stream = l->side;
+    if (flags & DPWA_FETCH_RESCUE) {
+        // re-selected after a timed-out pull: its own stream and buffer, ordered after the
+        // publish of the snapshot (above, local peers) and after the last reader of the buffer
+        if (!l->rescue_buf) {
+            HIP_TRY(hipMalloc(&l->rescue_buf, l->slot_stride));
+            HIP_TRY(hipStreamCreateWithFlags(&l->rescue_stream, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&l->ev_rescue, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&l->ev_stage_done[2], hipEventDisableTiming));
+        }
+        if (!(flags & DPWA_FETCH_PUBLISHED)) {
+            HIP_TRY(hipEventRecord(l->ev_issue, s));
+            HIP_TRY(hipStreamWaitEvent(l->rescue_stream, l->ev_issue, 0));
+        }
+        if (l->stage_read[2]) HIP_TRY(hipStreamWaitEvent(l->rescue_stream, l->ev_stage_done[2], 0));
+        const size_t nbytes = kPayloadOff + round_up(l->payload_bytes, 16);
+        if (l->pull_mode == DPWA_PULL_KERNEL)
+            HIP_TRY(launch_pull(l->rescue_buf, peer_slot, (int64_t)nbytes, l->pull_blocks,
+                                ep.kind == 2 || ep.device != l->device, l->rescue_stream));
+        else
+            HIP_TRY(hipMemcpyAsync(l->rescue_buf, peer_slot, nbytes, hipMemcpyDefault, l->rescue_stream));
+        HIP_TRY(hipEventRecord(l->ev_rescue, l->rescue_stream));
+        HIP_TRY(hipEventRecord(l->ev_fetched, l->rescue_stream));
+        l->rescue_used = true;
+        l->fetch_stream = l->rescue_stream;
+        l->src = l->rescue_buf;
+        l->src_copied = true;
+        l->src_stage = 2;
+    } else if (zero_copy && ep.kind == 1 && ep.device == l->device) {
         l->src = peer_slot;             // read in place; stream order covers the rest
         l->src_copied = false;
         l->src_stage = -1;
@@ -1555,6 +1602,39 @@ int dpwa_learner_copy_fetched(dpwa_learner *l, void *dst_dev, dpwa_stream_t stre
     HIP_TRY(staging_read(l, s));   // a later pull into this staging buffer waits for this copy
     l->consume_stream = s;   // the staging buffer / peer slot is read on s
     l->consumed_once = true;
+    return DPWA_OK;
+}
+
+int dpwa_learner_fetch_state(dpwa_learner *l, int64_t timeout_ms, int *state)
+{
+    if (!l || !state) return set_error(DPWA_ERR_ARG, "dpwa_learner_fetch_state: NULL argument");
+    *state = DPWA_FETCH_LANDED;
+    if (!l->have_fetch || !l->src_copied || l->relay_deferred) return DPWA_OK;
+    DeviceGuard dg(l->device);
+    const hipError_t e = hipEventQuery(l->ev_fetched);
+    if (e == hipSuccess) return DPWA_OK;
+    if (e != hipErrorNotReady) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(e));
+    const bool late = timeout_ms >= 0 && now_ns() - l->fetch_issue_ns >= timeout_ms * 1000000LL;
+    *state = late ? DPWA_FETCH_TIMED_OUT : DPWA_FETCH_IN_FLIGHT;
+    return DPWA_OK;
+}
+
+int dpwa_learner_rescue_free(dpwa_learner *l, int *free_out)
+{
+    if (!l || !free_out) return set_error(DPWA_ERR_ARG, "dpwa_learner_rescue_free: NULL argument");
+    *free_out = 1;
+    if (!l->rescue_used) return DPWA_OK;
+    DeviceGuard dg(l->device);
+    const hipError_t e = hipEventQuery(l->ev_rescue);
+    if (e != hipSuccess && e != hipErrorNotReady) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(e));
+    *free_out = e == hipSuccess ? 1 : 0;
+    return DPWA_OK;
+}
+
+int dpwa_learner_fetch_stream(dpwa_learner *l, dpwa_stream_t *stream)
+{
+    if (!l || !stream) return set_error(DPWA_ERR_ARG, "dpwa_learner_fetch_stream: NULL argument");
+    *stream = l->fetch_stream ? l->fetch_stream : l->side;
     return DPWA_OK;
 }
 

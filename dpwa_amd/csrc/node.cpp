@@ -8,8 +8,10 @@
 //   update_wait          dpwa/dpwa.py:125-156  (factor only; the lerp follows separately)
 //   update_wait_average  dpwa/dpwa.py:125-156 + dpwa/adapters/pytorch.py:60-68 in one kernel
 // Built only on the public C ABI of the learner and the scheduler.
+#include <chrono>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "common.hpp"
@@ -44,6 +46,10 @@ struct dpwa_node {
     dpwa_board *board = nullptr;
     std::vector<int32_t> board_rank;
     int publish_timeout_ms = -1;
+    // fetch timeout (conn.py:249, 304-309): the reply of a judged pull is reported when
+    // update_wait polls it (reply_pending), as data or as a timeout
+    int timeout_ms = -1;
+    bool reply_pending = false;
 };
 
 using namespace dpwa;
@@ -152,108 +158,191 @@ static int32_t peer_status(const dpwa_node *n, size_t k)
     return DPWA_PEER_READY;
 }
 
-// Free-running rounds: TxThread's loop (conn.py:277-315, as dpwa_sched_fetch runs it) with
-// the board standing in for the peers' RxThreads.  A READY peer's snapshot is acquired
-// *before* the outcome is reported, so a peer that closed between its status read and the
-// acquire counts as gone -- refused when not yet connected (conn.py:253-256), an error when
-// it was (conn.py:311-313) -- and never as a reply with data.
-static int board_fetch(dpwa_node *n, int flags, int *peer_out, uint64_t *version_out, int *attempts_out)
+static int64_t now_ms()
 {
-    *peer_out = -1;
-    *version_out = 0;
-    int attempts = 0;
-    while (attempts < kMaxFetchAttempts) {
-        int peer, connected, done = 0, data = 0;
-        int rc = dpwa_sched_pick(n->sched, &peer, &connected);
-        if (rc) return rc;
-        if (peer < 0) break;
-        attempts++;
-        int32_t st = n->status[peer];
-        uint64_t v = 0;
-        if (st == DPWA_PEER_READY && n->peers[peer].kind == PEER_REMOTE) {
-            if (flags & DPWA_FLAG_PICK_ONLY)
-                return set_error(DPWA_ERR_STATE, "the relay transport needs lock-step rounds, not a board");
-            if ((rc = dpwa_board_acquire(n->board, n->board_rank[peer], &v))) return rc;
-            if (v == 0) st = DPWA_PEER_DOWN;      // closed since its status was read
-        }
-        if (!connected) {
-            int c = DPWA_CONNECT_OK;
-            if (st == DPWA_PEER_DOWN) c = DPWA_CONNECT_REFUSED;
-            else if (st == DPWA_PEER_DEAD) c = DPWA_CONNECT_ERROR;
-            if ((rc = dpwa_sched_report(n->sched, peer, c, &done, &data))) return rc;
-            if (done) break;
-        }
-        int r;
-        switch (st) {
-        case DPWA_PEER_READY: r = DPWA_REPLY_PAYLOAD; break;
-        case DPWA_PEER_NO_STATE: r = DPWA_REPLY_EMPTY; break;
-        case DPWA_PEER_SLOW: r = DPWA_REPLY_TIMEOUT; break;
-        default: r = DPWA_REPLY_ERROR; break;
-        }
-        if ((rc = dpwa_sched_report(n->sched, peer, r, &done, &data))) return rc;
-        if (data) {
-            *peer_out = peer;
-            *version_out = v;
-            break;
-        }
-        if (done) break;
-    }
-    *attempts_out = attempts;
-    return DPWA_OK;
+    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
 }
 
-static int start_fetch(dpwa_node *n, int flags, dpwa_stream_t stream)
+// Moves peer `peer`'s snapshot towards this node's learner (or, PICK_ONLY, just records the
+// pick for a transport that moves the bytes itself).  board_version: the version the board
+// handed out (free-running), else unused.  rescue: into the rescue buffer on its own stream.
+static int issue_pull(dpwa_node *n, int peer, uint64_t board_version, int flags, dpwa_stream_t stream, bool rescue)
 {
-    int zero_copy = (flags & DPWA_FLAG_ZERO_COPY) ? 1 : 0;
-    n->fetch_started = true;
-    n->fetch_peer = -1;
-    for (size_t k = 0; k < n->peers.size(); ++k) n->status[k] = peer_status(n, k);
-    int peer = -1, attempts = 0;
-    int rc;
-    if (n->board) {
-        // free-running: the newest complete publish, held against rewrite until our pull lands
-        uint64_t version = 0;
-        if ((rc = board_fetch(n, flags, &peer, &version, &attempts))) return rc;
-        n->last_attempts = attempts;
-        if (peer < 0) return DPWA_OK;
-        const int r = n->board_rank[peer];
-        // a completed publish (the board advertised it): the pull needs no ordering after `stream`
-        if ((rc = dpwa_learner_fetch(n->learner, peer, version, DPWA_FETCH_PUBLISHED, stream))) {
-            dpwa_board_release(n->board, r, nullptr, 1);
-            return rc;
-        }
-        dpwa_stream_t side = nullptr;
-        if ((rc = dpwa_learner_side_stream(n->learner, &side)) ||
-            (rc = dpwa_board_release(n->board, r, side, 0)))
-            return rc;
-        n->fetch_peer = peer;
-        n->fetch_version = version;
-        return DPWA_OK;
-    }
-    if ((rc = dpwa_sched_fetch(n->sched, n->status.data(), kMaxFetchAttempts, &peer, &attempts))) return rc;
-    n->last_attempts = attempts;
-    if (peer < 0) return DPWA_OK;
     PeerRef &p = n->peers[peer];
+    const bool via_board = n->board && p.kind == PEER_REMOTE;
     uint64_t version;
-    if (p.kind == PEER_LOCAL) {
+    int fflags;
+    int rc;
+    if (via_board) {
+        // a completed publish (the board advertised it): the pull needs no ordering after `stream`
+        version = board_version;
+        fflags = DPWA_FETCH_PUBLISHED;
+    } else if (p.kind == PEER_LOCAL) {
         dpwa_learner *pl = p.node->learner;
         if (n->attached_to[peer] != pl) {
             if ((rc = dpwa_learner_attach_local(n->learner, peer, pl))) return rc;
             n->attached_to[peer] = pl;
         }
         version = learner_version(pl);
+        fflags = (flags & DPWA_FLAG_ZERO_COPY) ? DPWA_FETCH_ZERO_COPY : 0;
     } else {
         version = learner_version(n->learner);   // lock-step: every node publishes once per round
-        zero_copy = 0;
+        fflags = 0;
     }
     if (flags & DPWA_FLAG_PICK_ONLY) {   // the transport moves the bytes (relay)
         n->fetch_peer = peer;
         n->fetch_version = version;
         return DPWA_OK;
     }
-    if ((rc = dpwa_learner_fetch(n->learner, peer, version, zero_copy, stream))) return rc;
+    if (rescue) fflags = (fflags & DPWA_FETCH_PUBLISHED) | DPWA_FETCH_RESCUE;
+    if ((rc = dpwa_learner_fetch(n->learner, peer, version, fflags, stream))) {
+        if (via_board) dpwa_board_release(n->board, n->board_rank[peer], nullptr, 1);
+        return rc;
+    }
+    if (via_board) {   // our read mark is cleared once the pull has landed
+        dpwa_stream_t fs = nullptr;
+        if ((rc = dpwa_learner_fetch_stream(n->learner, &fs)) ||
+            (rc = dpwa_board_release(n->board, n->board_rank[peer], fs, 0)))
+            return rc;
+    }
     n->fetch_peer = peer;
     n->fetch_version = version;
+    return DPWA_OK;
+}
+
+// Host poll of a rescue pull (the abnormal path only): until it lands or timeout_ms after it was
+// issued, as the reference's receive blocks up to its socket timeout.
+static int wait_pull(dpwa_node *n, int *state)
+{
+    for (;;) {
+        int rc = dpwa_learner_fetch_state(n->learner, n->timeout_ms, state);
+        if (rc || *state != DPWA_FETCH_IN_FLIGHT) return rc;
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+// TxThread.run's loop for one queue item (conn.py:277-315): pick (conn.py:224-240), lazy
+// connect (conn.py:245-260), request, reply.  The reply of a judged pull (a copying pull from a
+// local peer or through the board, with a timeout set) is not reported here but when update_wait
+// polls it (judge_pending); after a timeout the loop runs again with rescue = true, each
+// re-selected pull going to the rescue buffer and being polled to its deadline on the host.
+// Free-running rounds read REMOTE peers through the board: a READY peer's snapshot is acquired
+// *before* the outcome is reported, so a peer that closed between its status read and the acquire
+// counts as gone -- refused when not yet connected (conn.py:253-256), an error when it was
+// (conn.py:311-313) -- and never as a reply with data.
+static int fetch_loop(dpwa_node *n, int flags, dpwa_stream_t stream, bool rescue)
+{
+    int attempts = 0;
+    int rc = DPWA_OK;
+    while (attempts < kMaxFetchAttempts) {
+        int peer, connected, done = 0, data = 0;
+        if ((rc = dpwa_sched_pick(n->sched, &peer, &connected))) break;
+        if (peer < 0) break;
+        attempts++;
+        const PeerRef &p = n->peers[peer];
+        const bool via_board = n->board && p.kind == PEER_REMOTE;
+        int32_t st = n->status[peer];
+        uint64_t v = 0;
+        if (st == DPWA_PEER_READY && via_board) {
+            if (flags & DPWA_FLAG_PICK_ONLY) {
+                rc = set_error(DPWA_ERR_STATE, "the relay transport needs lock-step rounds, not a board");
+                break;
+            }
+            if ((rc = dpwa_board_acquire(n->board, n->board_rank[peer], &v))) break;
+            if (v == 0) st = DPWA_PEER_DOWN;      // closed since its status was read
+        }
+        if (!connected) {
+            int c = DPWA_CONNECT_OK;
+            if (st == DPWA_PEER_DOWN) c = DPWA_CONNECT_REFUSED;
+            else if (st == DPWA_PEER_DEAD) c = DPWA_CONNECT_ERROR;
+            if ((rc = dpwa_sched_report(n->sched, peer, c, &done, &data))) break;
+            if (done) break;
+        }
+        if (st == DPWA_PEER_READY) {
+            const bool judged = n->timeout_ms >= 0 && !(flags & DPWA_FLAG_PICK_ONLY) &&
+                                (p.kind == PEER_LOCAL || via_board);
+            int state = DPWA_FETCH_LANDED;
+            if (rescue && judged) {
+                // the rescue buffer must be free: its last pull landed (else our own transport is
+                // stalled: wait up to the timeout, then this request times out and the round ends)
+                int free_ = 1;
+                const int64_t t0 = now_ms();
+                while ((rc = dpwa_learner_rescue_free(n->learner, &free_)) == DPWA_OK && !free_ &&
+                       now_ms() - t0 < n->timeout_ms)
+                    std::this_thread::sleep_for(std::chrono::microseconds(20));
+                if (rc) break;
+                if (!free_) {
+                    if (via_board) dpwa_board_release(n->board, n->board_rank[peer], nullptr, 1);
+                    rc = dpwa_sched_report(n->sched, peer, DPWA_REPLY_TIMEOUT, &done, &data);
+                    break;
+                }
+            }
+            if ((rc = issue_pull(n, peer, v, flags, stream, rescue && judged))) break;
+            if (judged && !rescue) {
+                n->reply_pending = true;         // judged when update_wait polls it
+                break;
+            }
+            if (judged && (rc = wait_pull(n, &state))) break;
+            if (state == DPWA_FETCH_TIMED_OUT) {
+                dpwa_learner_cancel(n->learner);
+                n->fetch_peer = -1;
+                if ((rc = dpwa_sched_report(n->sched, peer, DPWA_REPLY_TIMEOUT, &done, &data))) break;
+                continue;
+            }
+            if ((rc = dpwa_sched_report(n->sched, peer, DPWA_REPLY_PAYLOAD, &done, &data))) break;
+            break;
+        }
+        int r;
+        switch (st) {
+        case DPWA_PEER_NO_STATE: r = DPWA_REPLY_EMPTY; break;
+        case DPWA_PEER_SLOW: r = DPWA_REPLY_TIMEOUT; break;
+        default: r = DPWA_REPLY_ERROR; break;   // DOWN while connected (reset) or DEAD
+        }
+        if ((rc = dpwa_sched_report(n->sched, peer, r, &done, &data))) break;
+        if (done) break;
+    }
+    n->last_attempts += attempts;
+    return rc;
+}
+
+static void refresh_status(dpwa_node *n)
+{
+    for (size_t k = 0; k < n->peers.size(); ++k) n->status[k] = peer_status(n, k);
+}
+
+static int start_fetch(dpwa_node *n, int flags, dpwa_stream_t stream)
+{
+    n->fetch_started = true;
+    n->fetch_peer = -1;
+    n->reply_pending = false;
+    n->last_attempts = 0;
+    refresh_status(n);
+    return fetch_loop(n, flags, stream, false);
+}
+
+// update_wait's verdict on a judged pull (conn.py:298-309): landed, or still within its
+// timeout (then the device waits for it) -> the reply with data; else a socket timeout and the
+// loop picks again.
+static int judge_pending(dpwa_node *n, int flags, dpwa_stream_t stream)
+{
+    n->reply_pending = false;
+    int state = DPWA_FETCH_LANDED, done = 0, data = 0;
+    int rc = dpwa_learner_fetch_state(n->learner, n->timeout_ms, &state);
+    if (rc) return rc;
+    const int peer = n->fetch_peer;
+    if (state != DPWA_FETCH_TIMED_OUT) return dpwa_sched_report(n->sched, peer, DPWA_REPLY_PAYLOAD, &done, &data);
+    dpwa_learner_cancel(n->learner);          // the stalled pull still lands, into a buffer nobody reads
+    n->fetch_peer = -1;
+    if ((rc = dpwa_sched_report(n->sched, peer, DPWA_REPLY_TIMEOUT, &done, &data))) return rc;
+    refresh_status(n);
+    return fetch_loop(n, flags, stream, true);
+}
+
+int dpwa_node_set_timeout(dpwa_node *n, int timeout_ms)
+{
+    if (!n) return set_error(DPWA_ERR_ARG, "dpwa_node_set_timeout: NULL node");
+    n->timeout_ms = timeout_ms < 0 ? -1 : timeout_ms;
     return DPWA_OK;
 }
 
@@ -264,6 +353,13 @@ int dpwa_node_publish(dpwa_node *n, const void *flat, double loss, const double 
     if (n->awaiting_lerp) {   // update_wait() was not followed by a lerp: abandon that fetch
         dpwa_learner_cancel(n->learner);
         n->awaiting_lerp = false;
+    }
+    if (n->reply_pending) {   // update_wait never came: the reply arrived meanwhile (TxThread ran on)
+        int done = 0, data = 0;
+        n->reply_pending = false;
+        int rc = dpwa_sched_report(n->sched, n->fetch_peer, DPWA_REPLY_PAYLOAD, &done, &data);
+        if (rc) return rc;
+        dpwa_learner_cancel(n->learner);
     }
     n->fetch_started = false;
     n->fetch_peer = -1;
@@ -316,6 +412,10 @@ static int finish_fetch(dpwa_node *n, int flags, dpwa_stream_t stream, int *peer
     n->fetching = false;
     if (!n->fetch_started) {
         int rc = start_fetch(n, flags, stream);
+        if (rc) return rc;
+    }
+    if (n->reply_pending) {
+        int rc = judge_pending(n, flags, stream);
         if (rc) return rc;
     }
     *peer = n->fetch_peer;

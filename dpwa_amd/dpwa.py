@@ -231,6 +231,8 @@ class DpwaConnection:
             arr = (ctypes.c_uint32 * max(1, len(key)))(*key)
             _lib.call("dpwa_node_create", ctypes.byref(self._node), len(self.peers), arr, len(key),
                       float(self.fetch_probability), ctypes.byref(cfg))
+        # the YAML's socket timeout (conn.py:249) judges the device path's pulls (dpwa_node_set_timeout)
+        _lib.call("dpwa_node_set_timeout", self._node, int(self.timeout_ms) if self.timeout_ms is not None else -1)
         sched = ctypes.c_void_p()
         _lib.call("dpwa_node_handles", self._node, None, ctypes.byref(sched))
         self._sched = Scheduler(len(self.peers), handle=sched.value)

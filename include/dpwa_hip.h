@@ -190,8 +190,24 @@ int dpwa_learner_attach_fds(dpwa_learner *l, int peer_id, const void *handle, in
  * caller's lock-step barrier or the board's read marks. */
 #define DPWA_FETCH_ZERO_COPY 1
 #define DPWA_FETCH_PUBLISHED 2
+/* DPWA_FETCH_RESCUE: the fetch re-selected after a timed-out pull (conn.py:304-309 reconnects and
+ * picks again): it copies into a separate rescue buffer on a separate stream, so the stalled pull
+ * ahead of it on the side stream cannot hold it up. */
+#define DPWA_FETCH_RESCUE 4
 int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int flags,
                        dpwa_stream_t stream);
+/* The fetch timeout of the device path (the reference's socket timeout, conn.py:249 with
+ * timeout_ms from the YAML, and its handling at conn.py:304-309).  fetch_state polls the copying
+ * fetch in flight without blocking: DPWA_FETCH_LANDED (landed, or nothing to wait for),
+ * DPWA_FETCH_IN_FLIGHT, or DPWA_FETCH_TIMED_OUT (still in flight timeout_ms after it was issued).
+ * rescue_free: *free_out = 1 when the rescue buffer's last pull has landed.  fetch_stream: the
+ * stream the fetch in flight moves its bytes on (side or rescue stream). */
+#define DPWA_FETCH_LANDED 0
+#define DPWA_FETCH_IN_FLIGHT 1
+#define DPWA_FETCH_TIMED_OUT 2
+int dpwa_learner_fetch_state(dpwa_learner *l, int64_t timeout_ms, int *state);
+int dpwa_learner_rescue_free(dpwa_learner *l, int *free_out);
+int dpwa_learner_fetch_stream(dpwa_learner *l, dpwa_stream_t *stream);
 
 /* update_wait's averaging (dpwa.py:133-155 + pytorch.py:64-68) as ONE kernel: make `stream`
  * wait for the fetch, then every workgroup evaluates the factor (fp64, from the device clock
@@ -409,6 +425,16 @@ int dpwa_node_set_fault(dpwa_node *n, int peer, int status);
  * board NULL returns the node to lock-step.  The node does not own the board. */
 typedef struct dpwa_board dpwa_board;
 int dpwa_node_set_board(dpwa_node *n, dpwa_board *board, const int32_t *peer_ranks, int publish_timeout_ms);
+/* The YAML's timeout_ms (DpwaConfiguration.get_timeoutms, dpwa.py:90 -> conn.py:249) on the
+ * device path (< 0 disables).  A copying pull from a local peer or through the gossip board is
+ * judged when update_wait polls it (never a host wait in the normal path): landed, or issued
+ * less than timeout_ms ago -> the reply with data (score +10, conn.py:301-302; a pull still in
+ * flight is then waited for on the device); still in flight after timeout_ms -> a socket timeout
+ * (score -100, reconnect, conn.py:304-309) and the loop picks again, the re-selected pull going
+ * to the rescue buffer (DPWA_FETCH_RESCUE) and being polled on the host up to timeout_ms like
+ * the reference's blocking receive.  Lock-step (DistGroup) pulls wait for the round's barrier,
+ * i.e. for the slowest learner, not for the peer, and are not judged. */
+int dpwa_node_set_timeout(dpwa_node *n, int timeout_ms);
 
 /* update_send (dpwa.py:104-123): publish, then the Bernoulli gate; with DPWA_FLAG_EAGER a
  * granted fetch starts now (peer choice + pull on the side stream), else at update_wait.

@@ -1,0 +1,145 @@
+"""The device path's fetch timeout (the reference's socket timeout: conn.py:249 sets it from the
+YAML's timeout_ms; conn.py:304-309 handles it: score -100, disconnect, pick again).
+
+A pull is held back on the learner's side stream by a long spin kernel queued ahead of it, and
+update_wait polls it after the deadline: the round must score that peer -100, pick again, pull
+the re-selected peer into the rescue buffer and average with it -- peers, scores, clocks and
+parameters against the oracle policy with that request scripted as a timeout.  A pull that is
+merely slower than the host (the normal case) is never judged a timeout."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from dpwa_amd import DpwaConnection, _lib
+from dpwa_amd.group import LocalGroup
+from oracle import lerp as olerp
+from oracle.policy import OracleLearner
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+HOLD_CYCLES = 1_500_000_000      # ~0.6 s of spinning on the side stream (torch.cuda._sleep)
+
+
+def write_cfg(path, names, timeout_ms, interp="clock"):
+    lines = ["- nodes:"] + ["  - {name: %s, host: localhost, port: %d}" % (n, 47000 + i) for i, n in enumerate(names)]
+    lines += ["- fetch_probability: 1", "- timeout_ms: %d" % timeout_ms, "- interpolation: %s" % interp,
+              "- divergence_threshold: 0", "- constant: { value: 0.5 }", "- clock: 0", "- loss: 0"]
+    path.write_text("\n".join(lines) + "\n")
+
+
+def side_stream(conn):
+    s = ctypes.c_void_p()
+    _lib.call("dpwa_learner_side_stream", conn._learner.handle, ctypes.byref(s))
+    return torch.cuda.ExternalStream(s.value, device=DEV)
+
+
+def expected(names, init, send, wait, seeds, timeouts):
+    """The oracle's rounds; timeouts = {(round, learner): k}: learner's k-th request of that
+    round (1-based) times out."""
+    G, T = len(names), len(send)
+    idx = {nm: i for i, nm in enumerate(names)}
+    L = [OracleLearner(names[g], [x for x in names if x != names[g]], 1.0, "clock", None, 0.0, seeds[g])
+         for g in range(G)]
+    params = init.copy()
+    out = []
+    for r in range(T):
+        states = [L[g].update_send(send[r][g]) for g in range(G)]
+        snaps = [params[g].copy() for g in range(G)]
+        row = []
+        for g in range(G):
+            n_req = [0]
+
+            def request(peer, g=g, r=r, n_req=n_req):
+                n_req[0] += 1
+                if timeouts.get((r, g)) == n_req[0]:
+                    return "timeout", None, None
+                return "payload", states[idx[peer]], snaps[idx[peer]]
+
+            state, payload, attempts = L[g].fetch(lambda p: "ok", request)
+            averaged, factor = L[g].update_wait(wait[r][g], state, payload is not None)
+            if averaged:
+                params[g] = olerp.lerp_f32(params[g], payload, factor)
+            row.append((attempts[-1]["peer"] if payload is not None else "", [a["peer"] for a in attempts]))
+        out.append((params.copy(), [L[g].clock for g in range(G)],
+                    [L[g].scores([x for x in names if x != names[g]]) for g in range(G)], row))
+    return out
+
+
+@pytest.mark.parametrize("pull", ["copy", "kernel:256"])
+@pytest.mark.parametrize("G", [2, 3])
+def test_held_pull_times_out_and_the_loop_picks_again(tmp_path, pull, G):
+    names = ["t%d" % g for g in range(G)]
+    cfg = tmp_path / "to.yaml"
+    write_cfg(cfg, names, timeout_ms=100)
+    rng = np.random.default_rng(3)
+    n, T = 100_003, 4
+    init = rng.standard_normal((G, n)).astype(np.float32)
+    send = [[1.0 + 0.5 * g + r for g in range(G)] for r in range(T)]
+    wait = [[1.0 + 0.25 * g + r for g in range(G)] for r in range(T)]
+    seeds = [60 + g for g in range(G)]
+    held = {(1, 0)}                                      # learner 0's first pull of round 1 is held
+    exp = expected(names, init, send, wait, seeds, {(1, 0): 1})
+    group = LocalGroup(prefetch=True, zero_copy=False)   # copying pulls, started at the last publish
+    conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group, pull=pull) for g in range(G)]
+    flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
+    import time
+    for r in range(T):
+        for g in range(G):
+            if (r, g) in held:
+                with torch.cuda.stream(side_stream(conns[g])):
+                    torch.cuda._sleep(HOLD_CYCLES)       # the next pull of learner g queues behind this
+        for g in range(G):
+            conns[g].update_send(flats[g], send[r][g])
+        if any(h[0] == r for h in held):
+            time.sleep(0.3)                              # past the 100 ms deadline
+        got = [conns[g].update_wait_average(flats[g], wait[r][g]) for g in range(G)]
+        torch.cuda.synchronize()                         # (the held pull has landed before the next round)
+        params, clocks, scores, row = exp[r]
+        for g in range(G):
+            assert (got[g][0].peer if got[g][0] is not None else "") == row[g][0], (r, g)
+            assert conns[g].last_fetch_attempts == len(row[g][1]), (r, g)
+            assert conns[g].clock == clocks[g], (r, g)
+            assert olerp.bits_equal(flats[g].cpu().numpy(), params[g]), (r, g)
+            want = dict(zip([x for x in names if x != names[g]], scores[g]))
+            assert conns[g].flow_control_scores() == want, (r, g)
+    assert len(exp[1][3][0][1]) == 2                     # the oracle's round: a timeout, then data
+    for c in conns:
+        c.close()
+
+
+def test_slow_but_in_time_pull_is_data(tmp_path):
+    """A pull held for less than the timeout is awaited on the device, not judged: the rounds
+    are the oracle's rounds with no timeout."""
+    G = 3
+    names = ["s%d" % g for g in range(G)]
+    cfg = tmp_path / "slow.yaml"
+    write_cfg(cfg, names, timeout_ms=5000)
+    rng = np.random.default_rng(4)
+    n, T = 50_001, 3
+    init = rng.standard_normal((G, n)).astype(np.float32)
+    send = [[1.0 + g + r for g in range(G)] for r in range(T)]
+    wait = [[2.0 + g + r for g in range(G)] for r in range(T)]
+    seeds = [80 + g for g in range(G)]
+    exp = expected(names, init, send, wait, seeds, {})
+    group = LocalGroup(prefetch=True, zero_copy=False)
+    conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group) for g in range(G)]
+    flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
+    for r in range(T):
+        if r > 0:
+            for g in range(G):
+                with torch.cuda.stream(side_stream(conns[g])):
+                    torch.cuda._sleep(50_000_000)        # ~20 ms: slower than the host, inside the timeout
+        for g in range(G):
+            conns[g].update_send(flats[g], send[r][g])
+        for g in range(G):
+            conns[g].update_wait_average(flats[g], wait[r][g])
+        params, clocks, scores, _ = exp[r]
+        for g in range(G):
+            assert olerp.bits_equal(flats[g].cpu().numpy(), params[g]), (r, g)
+            assert conns[g].clock == clocks[g]
+            assert conns[g].flow_control_scores() == dict(zip([x for x in names if x != names[g]], scores[g]))
+    for c in conns:
+        c.close()
