@@ -14,8 +14,10 @@ def _rank(rank, world, q_addr, addrs, results, chunks):
         os.write(fd, b"rank%d-chunk%d" % (rank, c))
         fds.append(fd)
     server = _FdServer(fds, world - 1)
-    q_addr.put((rank, server.address))
+    q_addr.put((rank, (server.address, os.getpid())))
     peers = addrs.get()                       # every rank's address, once all have served
+    server.allow(pid for r, (_, pid) in peers.items() if r != rank)
+    peers = {r: a for r, (a, _) in peers.items()}
     got = {}
     for r in range(world):
         if r == rank:
@@ -48,3 +50,35 @@ def test_fds_reach_every_peer():
     for rank, got in out.items():
         for r, contents in got.items():
             assert contents == ["rank%d-chunk%d" % (r, c) for c in range(chunks)], (rank, r)
+
+
+def _intruder(address, q):
+    from dpwa_amd.group import _fetch_fds
+    try:
+        _fetch_fds(address, 2)
+        q.put("got fds")
+    except Exception as e:   # noqa: BLE001
+        q.put("refused: %s" % type(e).__name__)
+
+
+def test_fds_are_served_only_to_the_ranks():
+    """A process that is not one of the job's ranks (another pid) connects first: it gets no
+    fds, and the rank that connects after it is still served (advisor finding on _FdServer)."""
+    from dpwa_amd.group import _FdServer, _fetch_fds
+    fds = [os.memfd_create("c%d" % c) for c in range(2)]
+    for c, fd in enumerate(fds):
+        os.write(fd, b"chunk%d" % c)
+    server = _FdServer(fds, 1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_intruder, args=(server.address, q))
+    p.start()
+    server.allow([os.getpid()])             # this process stands for the peer rank
+    assert q.get(timeout=60).startswith("refused")
+    p.join(30)
+    got = _fetch_fds(server.address, 2)
+    assert [os.pread(fd, 16, 0) for fd in got] == [b"chunk0", b"chunk1"]
+    for fd in got:
+        os.close(fd)
+    server.finish()
+    assert server.rejected == 1
