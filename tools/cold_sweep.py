@@ -5,6 +5,7 @@ PMC pass of this command sees only cold launches of that kernel.
 
   python tools/cold_sweep.py                                  # configs[1]: 11.17M fp32, both publish forms
   python tools/cold_sweep.py --sizes 11173962:f32 --publish write-through
+  python tools/cold_sweep.py --publish write-through --learners 2     # the batched dispatch of N=1
   rocprofv3 --kernel-trace --stats -d gpurun_out/cold -o c -- python3 tools/cold_sweep.py --all
 """
 import argparse
@@ -27,6 +28,9 @@ def main():
     ap.add_argument("--all", action="store_true", help="every north_star size (bench.SWEEP)")
     ap.add_argument("--publish", choices=["full", "write-through", "both"], default="both")
     ap.add_argument("--launches", type=int, default=64)
+    ap.add_argument("--learners", type=int, default=1,
+                    help="averages per dispatch: 1 = dpwa_average (k_lerp), > 1 = dpwa_average_many (k_lerp_batch, "
+                         "the N=1 loop's kernel)")
     args = ap.parse_args()
     sizes = [(n, d) for n, d in bench.SWEEP] if args.all else \
         [(int(x.split(":")[0]), x.split(":")[1]) for x in args.sizes.split(",")]
@@ -37,8 +41,8 @@ def main():
         dtype = torch.float32 if dt == "f32" else torch.bfloat16
         esize = 4 if dt == "f32" else 2
         for wt in forms:
-            c = bench.cold_kernel(numel, dtype, dev, wt, args.launches)
-            nbytes = (4 if wt else 3) * numel * esize
+            c = bench.cold_kernel(numel, dtype, dev, wt, args.launches, learners=args.learners)
+            nbytes = args.learners * (4 if wt else 3) * numel * esize
             gbs = nbytes / (c["avg_launch_us"] * 1e-6) / 1e9
             print(json.dumps(dict(numel=numel, dtype=dt, publish="write-through" if wt else "full",
                                   bytes_per_launch=nbytes, achieved=round(gbs, 1),

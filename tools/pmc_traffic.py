@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--publish", choices=["full", "write-through"], default="full",
                     help="write-through: the kernel also writes the next snapshot (4*N*s algorithmic bytes)")
+    ap.add_argument("--learners", type=int, default=1, help="averages per dispatch (k_lerp_batch)")
     ap.add_argument("--basis", choices=["cold", "in-loop"], default="cold",
                     help="what the profiled command ran: tools/cold_sweep.py (cold) or bench.py's loop")
     ap.add_argument("--out", required=True)
@@ -62,13 +63,14 @@ def main():
     read_bytes = 2 * f_kib * 1024      # gfx950 FETCH_SIZE = 1/2 of 16-B/lane streaming reads
     write_bytes = w_kib * 1024
     esize = 4 if args.dtype == "f32" else 2
-    algo = (4 if args.publish == "write-through" else 3) * args.numel * esize
+    algo = args.learners * (4 if args.publish == "write-through" else 3) * args.numel * esize
     out = {
         "kernel": sorted(set(names.values()))[0],
         "numel": args.numel,
         "dtype": args.dtype,
         "gpus": args.gpus,
         "publish": args.publish,
+        "learners_per_launch": args.learners,
         "basis": args.basis,
         "dispatches": {"fetch_pass": len(fetch), "write_pass": len(write)},
         "FETCH_SIZE_KiB_median": f_kib,
