@@ -267,6 +267,17 @@ def injected(transport, rank, where):
     return False
 
 
+class _NoCtxType:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NoCtx = _NoCtxType()
+
+
 def write_config(path, names, interp, fetch_probability=1.0, divergence_threshold=0.0):
     """The reference's YAML node config (dpwa/conn.py:246-262, dpwa/dpwa.py:60-90)."""
     lines = ["- nodes:"] + ["  - {name: %s, host: 127.0.0.1, port: %d}" % (n, 45000 + i)
@@ -943,13 +954,21 @@ def main(argv=None):
         lib = _lib.load()
         timed_learners = []
 
+        conns_ = [c for c, _ in learners]
+        flats_ = [f for _, f in learners]
+        one_stream = all(st is stream for st in streams)
+        const_loss = [1.0] * len(learners) if args.loss_schedule == "constant" else None
+
         def step(k, timed):
             done = 0
-            losses = [loss_of(i) for i in range(len(learners))]
+            losses = const_loss or [loss_of(i) for i in range(len(learners))]
             loss_t[0] += 1
             for i, (conn, flat) in enumerate(learners):
-                with torch.cuda.stream(streams[i]):
+                if one_stream:      # (a stream context costs microseconds of host time per round)
                     conn.update_send(flat, losses[i], reuse_snapshot=write_through)
+                else:
+                    with torch.cuda.stream(streams[i]):
+                        conn.update_send(flat, losses[i], reuse_snapshot=write_through)
             sample = timed and sample_every and k % sample_every == 0
             if batched:
                 if sample:
@@ -958,15 +977,14 @@ def main(argv=None):
                         a.record(stream)
                     if args.timing != "bracket" and timed_learners:
                         lib.dpwa_learner_arm_timing(timed_learners[0]._learner.handle)
-                res = DpwaConnection.update_wait_average_many([c for c, _ in learners], [f for _, f in learners],
-                                                              losses, write_through=write_through)
+                res = DpwaConnection.update_wait_average_many(conns_, flats_, losses, write_through=write_through)
                 if sample and args.timing != "dispatch":
                     b.record(stream)
                     lerp_events.append((a, b))
                 return sum(p is not None for p, _ in res)
             for i, (conn, flat) in enumerate(learners):
                 st = streams[i]
-                with torch.cuda.stream(st):
+                with (_NoCtx if one_stream else torch.cuda.stream(st)):
                     # the adapter's update_wait: fused device factor + lerp (one kernel)
                     if sample:
                         a, b = events[len(lerp_events)]

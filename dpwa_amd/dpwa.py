@@ -28,6 +28,7 @@ from .sched import Scheduler, seed_key
 
 LOGGER = logging.getLogger(__name__)
 RELAY_PULLS = ("relay", "relay-avg")   # DistGroup's multi-link transports (dpwa_amd/group.py)
+_MANY_CALLS = {}    # update_wait_average_many: argument arrays per set of nodes
 
 
 class Struct:
@@ -354,25 +355,34 @@ class DpwaConnection:
         as the single calls would resolve it, and the averages run as ONE dispatch instead of
         one per learner (same results; a kernel boundary and a launch ramp/drain fewer per
         extra learner).  Returns the list of what update_wait returns, per connection."""
-        conns, parameters, losses = list(conns), list(parameters), list(losses)
         if not (len(conns) == len(parameters) == len(losses)):
             raise ValueError("update_wait_average_many: %d connections, %d buffers, %d losses"
                              % (len(conns), len(parameters), len(losses)))
-        bound = [i for i, c in enumerate(conns) if c._learner is not None]
-        out = [(None, 0)] * len(conns)
-        if not bound:
-            return out
-        dev = conns[bound[0]]._learner.device
-        k = len(bound)
-        nodes, flats = (ctypes.c_void_p * k)(), (ctypes.c_void_p * k)()
-        hs, ds = (ctypes.c_double * k)(), (ctypes.c_void_p * k)()
+        # the ctypes argument arrays of this set of connections, reused across rounds (the call
+        # is on the per-round path: its host cost must stay well under the dispatch it replaces)
+        key = tuple((c._node.value, c._learner.device.index) if c._learner is not None else None for c in conns)
+        calls = _MANY_CALLS
+        cache = calls.get(key)
+        if cache is None:
+            bound = [i for i, c in enumerate(conns) if c._learner is not None]
+            if not bound:
+                return [(None, 0)] * len(conns)
+            dev = conns[bound[0]]._learner.device
+            if any(conns[i]._learner.device != dev for i in bound):
+                raise ValueError("update_wait_average_many: the learners are on different devices")
+            k = len(bound)
+            nodes = (ctypes.c_void_p * k)(*[conns[i]._node.value for i in bound])
+            cache = (bound, dev.index, nodes, (ctypes.c_void_p * k)(), (ctypes.c_double * k)(),
+                     (ctypes.c_void_p * k)(), (ctypes.c_int * k)(), conns[bound[0]]._lib)
+            if len(calls) > 64:
+                calls.clear()
+            calls[key] = cache
+        bound, dev_index, nodes, flats, hs, ds, peers, lib = cache
+        flags = _lib.FLAG_WRITE_THROUGH if write_through else 0
         keep = []
-        flags = 0
         for j, i in enumerate(bound):
             c = conns[i]
             learner = c._learner
-            if learner.device != dev:
-                raise ValueError("update_wait_average_many: learners on %s and %s" % (dev, learner.device))
             if learner.take_status():
                 c._zero_division()
             flats[j] = learner._ptr(parameters[i])
@@ -380,22 +390,18 @@ class DpwaConnection:
             keep.append(learner._keep)
             hs[j] = h
             ds[j] = d.value if d is not None else None
-            nodes[j] = c._node.value
             flags |= c._flags
-        flags |= _lib.FLAG_WRITE_THROUGH if write_through else 0
-        peers = (ctypes.c_int * k)()
-        lib = conns[bound[0]]._lib
-        rc = lib.dpwa_node_update_wait_average_many(nodes, flats, hs, ds, k, flags,
-                                                     ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(dev.index)),
-                                                     peers)
-        for j, i in enumerate(bound):
+        rc = lib.dpwa_node_update_wait_average_many(nodes, flats, hs, ds, len(bound), flags,
+                                                     torch._C._cuda_getCurrentRawStream(dev_index), peers)
+        for i in bound:
             conns[i].fetching = False
         if rc:
             raise _lib.DpwaError("dpwa_node_update_wait_average_many", rc,
                                  lib.dpwa_last_error().decode(errors="replace"))
+        out = [(None, 0)] * len(conns)
         for j, i in enumerate(bound):
-            c = conns[i]
             if peers[j] >= 0:
+                c = conns[i]
                 out[i] = (PeerSnapshot(c, peers[j], c._learner.version), DeviceFactor(c._learner))
         return out
 
