@@ -2,7 +2,8 @@
 """Host-side cost of one gossip round through the drop-in API (the part of a round a
 host-bound training loop pays on the CPU): two learners in one process, a ResNet-18-shaped
 parameter list (62 tensors) scaled down so the GPU work is negligible, timed per call with
-time.perf_counter over many rounds.  Prints one JSON line (microseconds per call)."""
+time.perf_counter over many rounds.  Prints one JSON line (microseconds per call and learner;
+connection_batched: both learners' update_wait in one update_wait_average_many call)."""
 import json
 import os
 import sys
@@ -30,7 +31,7 @@ def main(rounds=2000):
                 self.register_parameter("p%d" % i, torch.nn.Parameter(torch.zeros(min(64, int(torch.tensor(s).prod())))))
 
     out = {}
-    for mode in ("adapter", "connection"):
+    for mode in ("adapter", "connection", "connection_batched"):
         group = LocalGroup()
         if mode == "adapter":
             nets = [Net().to(dev), Net().to(dev)]
@@ -43,6 +44,8 @@ def main(rounds=2000):
             conns = [DpwaConnection(nm, cfg, seed=i, group=group) for i, nm in enumerate("ab")]
             send = [lambda l, c=c, f=f: c.update_send(f, l, reuse_snapshot=True) for c, f in zip(conns, flats)]
             wait = [lambda l, c=c, f=f: c.update_wait_average(f, l, write_through=True) for c, f in zip(conns, flats)]
+            if mode == "connection_batched":     # both averages in one call (and one dispatch)
+                wait = [lambda l: DpwaConnection.update_wait_average_many(conns, flats, [l, l], write_through=True)]
         for loss_kind in ("float", "tensor"):
             loss = 1.0 if loss_kind == "float" else torch.tensor(1.0, device=dev)
             for _ in range(50):
@@ -66,7 +69,8 @@ def main(rounds=2000):
                     torch.cuda.synchronize()      # keep the GPU queue short
             torch.cuda.synchronize()
             out["%s/%s_loss" % (mode, loss_kind)] = {"update_send_us": round(1e6 * ts / (2 * rounds), 2),
-                                                     "update_wait_us": round(1e6 * tw / (2 * rounds), 2)}
+                                                     "update_wait_us": round(1e6 * tw / (2 * rounds), 2),
+                                                     "round_us_both_learners": round(1e6 * (ts + tw) / rounds, 2)}
         for c in conns:
             c.close()
     print(json.dumps(out))
