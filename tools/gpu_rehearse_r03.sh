@@ -15,14 +15,15 @@ export TMPDIR=/tmp
 B="--gpus $N --dist-backend gloo --steps 20 --warmup 5 --no-cpu-baseline --compute-us 0"
 t0=$(date +%s)
 timeout -k 10 500 python -u bench.py $B > gpurun_out/rh_${TAG}_clean.json 2> gpurun_out/rh_${TAG}_clean.err
-echo "clean rc=$? $(( $(date +%s) - t0 ))s"; tail -c 600 gpurun_out/rh_${TAG}_clean.json; echo
+echo "clean rc=$? $(( $(date +%s) - t0 ))s, stdout lines: $(wc -l < gpurun_out/rh_${TAG}_clean.json)"
+python3 -c "import json;d=json.load(open('gpurun_out/rh_${TAG}_clean.json'));print(d['value'], d.get('pull_choice'), {k:v for k,v in d['parity'].items() if k!='workload'})"
 [ "${3:-all}" = "clean" ] && exit 0
 t0=$(date +%s)
 DPWA_BENCH_INJECT="lockstep/relay:32@1:end" timeout -k 10 500 python -u bench.py $B --no-secondary \
     > gpurun_out/rh_${TAG}_inject_end.json 2> gpurun_out/rh_${TAG}_inject_end.err
-echo "inject-end rc=$? $(( $(date +%s) - t0 ))s"; python -c "import json;d=json.load(open('gpurun_out/rh_${TAG}_inject_end.json'));print(d.get('parity'), d.get('value'))"
+echo "inject-end rc=$? $(( $(date +%s) - t0 ))s, stdout lines: $(wc -l < gpurun_out/rh_${TAG}_inject_end.json)"; python -c "import json;d=json.load(open('gpurun_out/rh_${TAG}_inject_end.json'));print(d.get('parity'), d.get('value'))"
 t0=$(date +%s)
 DPWA_BENCH_INJECT="lockstep/relay:32@1:start" timeout -k 10 400 python -u bench.py $B --no-secondary --phase-scale 0.25 \
     > gpurun_out/rh_${TAG}_inject_start.json 2> gpurun_out/rh_${TAG}_inject_start.err
-echo "inject-start rc=$? $(( $(date +%s) - t0 ))s"; cat gpurun_out/rh_${TAG}_inject_start.json
+echo "inject-start rc=$? $(( $(date +%s) - t0 ))s, stdout lines: $(wc -l < gpurun_out/rh_${TAG}_inject_start.json)"; cat gpurun_out/rh_${TAG}_inject_start.json
 exit 0
