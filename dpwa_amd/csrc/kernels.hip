@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 
 #include "kernels.hpp"
 
@@ -374,17 +376,27 @@ __global__ __launch_bounds__(kStreamBlock) void k_lerp_relay(typename Ops::V *__
 template <class Ops, bool DUAL>
 __global__ __launch_bounds__(kStreamBlock) void k_lerp_batch(AvgBatch batch)
 {
-    // the entry of this workgroup: a short scalar scan over the uniform begin[] table
     int i = 0;
+    uint32_t blk;
+    if (batch.interleave) {
+        // entries of equal size, their spans dealt round-robin: a span is read one round after
+        // the span at the same position was written by the previous round's dispatch, whichever
+        // entry wrote it, so every re-read is equally recent (Infinity Cache residency)
+        i = (int)(blockIdx.x % (uint32_t)batch.count);
+        blk = blockIdx.x / (uint32_t)batch.count;
+    } else {
+        // the entry of this workgroup: a short scalar scan over the uniform begin[] table
 #pragma unroll
-    for (int k = 1; k < kMaxAvgBatch; ++k)
-        if (k < batch.count && blockIdx.x >= batch.begin[k]) i = k;
+        for (int k = 1; k < kMaxAvgBatch; ++k)
+            if (k < batch.count && blockIdx.x >= batch.begin[k]) i = k;
+        blk = blockIdx.x - batch.begin[i];
+    }
     const AvgEntry &e = batch.e[i];
     LerpArgs args{};
     args.fused = e.fa;
     args.snap = e.snap;
-    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, 0>(blockIdx.x - batch.begin[i], (typename Ops::V *)e.param,
-                                                      ContigSrc{(const char *)e.peer}, e.n, args);
+    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, 0>(blk, (typename Ops::V *)e.param, ContigSrc{(const char *)e.peer},
+                                                      e.n, args);
 }
 
 // Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
@@ -535,6 +547,15 @@ hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t 
     return launch_any(dtype, COEF_FUSED, param, peer, n, args, s, timing);
 }
 
+static bool batch_interleave()
+{
+    static const bool on = [] {
+        const char *e = getenv("DPWA_BATCH_ORDER");
+        return !(e && strcmp(e, "contiguous") == 0);
+    }();
+    return on;
+}
+
 hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hipStream_t s,
                                  const LaunchTiming *timing)
 {
@@ -554,6 +575,11 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
         g += (uint32_t)gi;
     }
     for (int i = x.count; i < kMaxAvgBatch; ++i) x.begin[i] = 0xffffffffu;
+    // equal sizes: spans dealt round-robin over the entries (DPWA_BATCH_ORDER=contiguous: one
+    // entry after the other)
+    bool same = true;
+    for (int i = 1; i < x.count; ++i) same = same && x.e[i].n == x.e[0].n;
+    x.interleave = same && x.count > 1 && batch_interleave() ? 1 : 0;
 #define DPWA_BATCH_LAUNCH(OPS, DL)                                                                          \
     do {                                                                                                    \
         if (timing)                                                                                         \

@@ -65,6 +65,7 @@ struct AvgEntry {
 };
 struct AvgBatch {
     int32_t count;
+    int32_t interleave;             // spans dealt round-robin over equal-size entries (launcher)
     uint32_t begin[kMaxAvgBatch];   // first workgroup of each entry (filled by the launcher)
     AvgEntry e[kMaxAvgBatch];
 };
