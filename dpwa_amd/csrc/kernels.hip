@@ -547,13 +547,24 @@ hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t 
     return launch_any(dtype, COEF_FUSED, param, peer, n, args, s, timing);
 }
 
-static bool batch_interleave()
+// Span order of a batched dispatch of equal-size entries.  Dealt round-robin, every span is
+// re-read by the next round's dispatch one round after it was written, which keeps the re-reads
+// in the 256 MiB Infinity Cache while a round writes less than that; one entry after the other,
+// half the re-reads come 1.5 rounds after their write.  Measured (profiles/r03_batch_order_ab.log,
+// three interleaved pairs): round-robin +2.8 % at 11.17M fp32 (179 MB written per round), -4 %
+// at 100M fp32 (1.6 GB: twice the concurrent streams, no cache to win).  DPWA_BATCH_ORDER=
+// interleaved / contiguous forces one.
+constexpr size_t kInfinityCacheBytes = (size_t)256 << 20;
+
+static int batch_order()
 {
-    static const bool on = [] {
+    static const int forced = [] {
         const char *e = getenv("DPWA_BATCH_ORDER");
-        return !(e && strcmp(e, "contiguous") == 0);
+        if (e && strcmp(e, "contiguous") == 0) return 0;
+        if (e && strcmp(e, "interleaved") == 0) return 1;
+        return -1;
     }();
-    return on;
+    return forced;
 }
 
 hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hipStream_t s,
@@ -575,11 +586,15 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
         g += (uint32_t)gi;
     }
     for (int i = x.count; i < kMaxAvgBatch; ++i) x.begin[i] = 0xffffffffu;
-    // equal sizes: spans dealt round-robin over the entries (DPWA_BATCH_ORDER=contiguous: one
-    // entry after the other)
+    // span order: see batch_order()
     bool same = true;
-    for (int i = 1; i < x.count; ++i) same = same && x.e[i].n == x.e[0].n;
-    x.interleave = same && x.count > 1 && batch_interleave() ? 1 : 0;
+    size_t written = 0;
+    for (int i = 0; i < x.count; ++i) {
+        same = same && x.e[i].n == x.e[0].n;
+        written += (size_t)x.e[i].n * (size_t)(per == OpsF32::PER ? 4 : 2) * (dual ? 2 : 1);
+    }
+    const int order = batch_order();
+    x.interleave = same && x.count > 1 && (order == 1 || (order < 0 && written <= kInfinityCacheBytes)) ? 1 : 0;
 #define DPWA_BATCH_LAUNCH(OPS, DL)                                                                          \
     do {                                                                                                    \
         if (timing)                                                                                         \
