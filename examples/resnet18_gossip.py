@@ -68,6 +68,8 @@ def main(argv=None):
     ap.add_argument("--pull", default=None,
                     help="under torchrun: copy | kernel[:blocks] | relay[:blocks] | relay-avg[:blocks] "
                          "(the relays need --gossip lockstep)")
+    ap.add_argument("--no-batch-wait", dest="batch_wait", action="store_false",
+                    help="co-resident learners: one update_wait per adapter instead of update_wait_many")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -111,8 +113,11 @@ def main(argv=None):
             for i in range(len(mine)):
                 losses[i] = train_step(i)
             if gossip:
-                for i, a in enumerate(adapters):
-                    a.update_wait(losses[i])
+                if len(adapters) > 1 and args.batch_wait:    # co-resident: one averaging dispatch
+                    DpwaPyTorchAdapter.update_wait_many(adapters, losses)
+                else:
+                    for i, a in enumerate(adapters):
+                        a.update_wait(losses[i])
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
@@ -141,6 +146,7 @@ def main(argv=None):
             "train_steps_per_s_per_learner_plain": round(args.steps / t_plain, 1),
             "train_steps_per_s_per_learner_gossip": round(args.steps / t_gossip, 1),
             "gossip_overhead_pct": round(100 * (t_gossip - t_plain) / t_plain, 2),
+            "batched_wait": bool(args.batch_wait and len(adapters) > 1),
             "final_clock": adapters[0].connection.clock,
         }))
     for a in adapters:
