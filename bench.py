@@ -705,7 +705,9 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
     esize = 4 if dtype == torch.float32 else 2
     nbuf = 3 if write_through else 2
     per_set = learners * nbuf * numel * esize
-    sets = max(2, int(np.ceil(1.2e9 / per_set)))
+    # > 1.2 GB of other traffic between two uses of a buffer; a set that large by itself is its
+    # own rotation (7B bf16: 42 GB per learner, HBM holds the learners' slots too)
+    sets = 1 if per_set >= 1.2e9 else max(2, int(np.ceil(1.2e9 / per_set)))
     launches = max(2 * sets, min(launches, int(np.ceil(64 * 134e6 / (3 * learners * numel * esize)))))
     hdr = _lib.SLOT_PAYLOAD_OFFSET // esize
     bufs = []       # per set: [(param, slot, snap)] * learners
