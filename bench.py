@@ -950,6 +950,7 @@ def main(argv=None):
         step is timed by its own dispatch events (and/or bracketed by an event pair on its
         stream) -- the in-loop kernel figure, from a separate pass."""
         lerp_events = []
+        sampled = []        # batched: per timed dispatch (learner whose pair timed it, averages in it)
         n_slots = (steps // sample_every + 1) * len(learners) if sample_every else 0
         events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(n_slots)]
@@ -974,16 +975,20 @@ def main(argv=None):
             sample = timed and sample_every and k % sample_every == 0
             if batched:
                 if sample:
-                    a, b = events[len(lerp_events)]
+                    a, b = events[len(sampled)]
                     if args.timing != "dispatch":
                         a.record(stream)
-                    if args.timing != "bracket" and timed_learners:
-                        lib.dpwa_learner_arm_timing(timed_learners[0]._learner.handle)
+                    if args.timing != "bracket":      # the dispatch takes its first armed learner's pair
+                        for c in timed_learners:
+                            lib.dpwa_learner_arm_timing(c._learner.handle)
                 res = DpwaConnection.update_wait_average_many(conns_, flats_, losses, write_through=write_through)
-                if sample and args.timing != "dispatch":
-                    b.record(stream)
-                    lerp_events.append((a, b))
-                return sum(p is not None for p, _ in res)
+                got = [p is not None for p, _ in res]
+                if sample and any(got):
+                    sampled.append((got.index(True), sum(got)))     # (pair owner, averages in the dispatch)
+                    if args.timing != "dispatch":
+                        b.record(stream)
+                        lerp_events.append((a, b))
+                return sum(got)
             for i, (conn, flat) in enumerate(learners):
                 st = streams[i]
                 with (_NoCtx if one_stream else torch.cuda.stream(st)):
@@ -1022,16 +1027,30 @@ def main(argv=None):
             hbarrier()
         elapsed = time.perf_counter() - t0
         bracket_ms = np.array([a.elapsed_time(b) for a, b in lerp_events]) if lerp_events else np.array([np.nan])
-        kern_us = []
+        kern_us, per_learner = [], []
         for conn in timed_learners:
             buf = (ctypes.c_float * max(1, len(events)))()
             cnt = ctypes.c_int()
             _lib.call("dpwa_learner_read_average_times", conn._learner.handle, buf, len(events), ctypes.byref(cnt))
+            per_learner.append(list(buf[:cnt.value]))
             kern_us += list(buf[:cnt.value])
             _lib.call("dpwa_learner_time_averages", conn._learner.handle, 0)
+        n_avg = np.ones(len(kern_us))       # averages per timed dispatch
+        if batched and sampled and args.timing != "bracket":
+            # each timed dispatch from its pair owner's list, in the order the dispatches ran
+            kern_us, n_avg = [], []
+            nxt = [0] * len(per_learner)
+            for owner, n in sampled:
+                if nxt[owner] < len(per_learner[owner]):
+                    kern_us.append(per_learner[owner][nxt[owner]])
+                    n_avg.append(n)
+                    nxt[owner] += 1
+            n_avg = np.array(n_avg, dtype=float)
         if args.timing == "bracket":
             kern_us = list(bracket_ms * 1e3)
-        lerp_ms = (np.array(kern_us) / 1e3 if kern_us else np.array([np.nan]), bracket_ms)
+            n_avg = np.array([n for _, n in sampled], dtype=float) if batched else np.ones(len(kern_us))
+        lerp_ms = (np.array(kern_us) / 1e3 if kern_us else np.array([np.nan]), bracket_ms,
+                   n_avg if len(n_avg) else np.array([np.nan]))
         stats = torch.tensor([elapsed, float(averaged), float(len(learners) * steps)], dtype=torch.float64)
         if world > 1:
             got = [None] * world
@@ -1198,7 +1217,7 @@ def main(argv=None):
     # the averaging kernel inside the loop: a separate sampled pass of the same rounds
     wd.enter("in-loop kernel timing", 600.0)
     s_steps = max(args.steps, 8 * args.sample_every)
-    s_el, _, _, (lerp_ms, bracket_ms) = run(s_steps, 2, wt_main, args.sample_every)
+    s_el, _, _, (lerp_ms, bracket_ms, lerp_navg) = run(s_steps, 2, wt_main, args.sample_every)
     pull_us = []
     if world > 1 and not sel_mode.startswith("relay"):
         # the pull alone (side-stream events around each copying fetch), in a short extra run
@@ -1290,7 +1309,10 @@ def main(argv=None):
     if rank == 0:
         value = averaged * unit_bytes / elapsed / 1e9
         lerp_us = float(np.nanmean(lerp_ms) * 1e3)
-        live_gbs = kbytes / (lerp_us * 1e-6) / 1e9
+        # each timed dispatch moved (averages in it) x 4*N*s (3*N*s): the aggregate rate
+        k1 = kbytes / per_launch
+        live_gbs = float(np.nansum(lerp_navg * k1) / np.nansum(lerp_ms * 1e-3) / 1e9) if np.isfinite(lerp_us) \
+            else float("nan")
         k_us = cold["avg_launch_us"] if cold else lerp_us
         achieved = kbytes / (k_us * 1e-6) / 1e9
         variant = "write-through" if wt_main else "full"
@@ -1366,6 +1388,7 @@ def main(argv=None):
                     "frac": round(live_gbs / HBM_PEAK_GBS, 4),
                     "avg_launch_us": round(lerp_us, 2),
                     "launches_timed": int(np.isfinite(lerp_ms).sum()),
+                    "averages_per_launch": round(float(np.nanmean(lerp_navg)), 3),
                     "timing": ("kernel dispatch begin/end events (hipExtLaunchKernelGGL) on the averaging "
                                "kernel's own stream" if args.timing != "bracket" else
                                "HIP event pair recorded around the launch on its stream")
@@ -1423,9 +1446,9 @@ def main(argv=None):
                             "(barriers and the average included): a lower bound on the link rate",
                 }
         if secondary is not None:
-            s_wt, (w_el, w_avg, w_rounds, _), (w_ms, _) = secondary
+            s_wt, (w_el, w_avg, w_rounds, _), (w_ms, _, w_n) = secondary
             w_us = float(np.nanmean(w_ms) * 1e3)
-            w_bytes = (4 if s_wt else 3) * args.numel * esize * per_launch
+            w_bytes = (4 if s_wt else 3) * args.numel * esize * float(np.nanmean(w_n))
             out["secondary_publish"] = {
                 "publish": "write-through" if s_wt else "full",
                 "value": round(w_avg * unit_bytes / w_el / 1e9, 2),

@@ -614,6 +614,7 @@ static int wait_slot_readers(dpwa_learner *l, int k, hipStream_t s)
 static int publish_impl(dpwa_learner *l, const void *flat, double loss, const double *loss_dev, hipStream_t s,
                         bool reuse)
 {
+    l->timing_armed = false;   // armed for the last round's average, which did not happen
     const int k = (int)(l->version % 2);   // slot of publish number version+1
     char *slot = l->slots + (size_t)k * l->slot_stride;
     const bool header_only = reuse && l->wt_valid && l->wt_flat == flat;

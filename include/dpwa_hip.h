@@ -279,8 +279,10 @@ int dpwa_learner_relay_phase2(dpwa_learner *l, const int32_t *picks_dev, int my_
  * (0 frees them; synchronises the device).  After arm_timing, the next averaging launch
  * (average / average_through, 16-B aligned parameters) goes through hipExtLaunchKernelGGL
  * with the next free pair, so it is timed as a profiler times it, without the dispatch gaps
- * of an event pair recorded around the launch.  read_average_times waits for and returns the
- * recorded durations (µs, launch order) and frees the pairs for reuse. */
+ * of an event pair recorded around the launch; the next publish disarms it (a round without an
+ * average times nothing).  A batched dispatch (average_many) is timed with the pair of its first
+ * armed learner, in call order.  read_average_times waits for and returns the recorded
+ * durations (µs, launch order) and frees the pairs for reuse. */
 int dpwa_learner_time_averages(dpwa_learner *l, int capacity);
 int dpwa_learner_arm_timing(dpwa_learner *l);
 int dpwa_learner_read_average_times(dpwa_learner *l, float *us_out, int max, int *count);
