@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kStreamBlock) void k_lerp_relay(typename Ops::V *__
 // single-average span code for its entry, so the per-learner semantics (factor, clock commit by
 // the entry's first workgroup, ragged tail) are those of k_lerp.  One launch instead of one per
 // learner removes a ramp, a drain and a kernel boundary per extra learner.
-template <class Ops, bool DUAL>
+template <class Ops, bool DUAL, int POLICY = 0>
 __global__ __launch_bounds__(kStreamBlock) void k_lerp_batch(AvgBatch batch)
 {
     int i = 0;
@@ -395,8 +395,8 @@ __global__ __launch_bounds__(kStreamBlock) void k_lerp_batch(AvgBatch batch)
     LerpArgs args{};
     args.fused = e.fa;
     args.snap = e.snap;
-    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, 0>(blk, (typename Ops::V *)e.param, ContigSrc{(const char *)e.peer},
-                                                      e.n, args);
+    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, POLICY>(blk, (typename Ops::V *)e.param,
+                                                           ContigSrc{(const char *)e.peer}, e.n, args);
 }
 
 // Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
@@ -595,13 +595,24 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
     }
     const int order = batch_order();
     x.interleave = same && x.count > 1 && (order == 1 || (order < 0 && written <= kInfinityCacheBytes)) ? 1 : 0;
-#define DPWA_BATCH_LAUNCH(OPS, DL)                                                                          \
+#define DPWA_BATCH_LAUNCH_P(OPS, DL, P)                                                                     \
     do {                                                                                                    \
         if (timing)                                                                                         \
-            hipExtLaunchKernelGGL((k_lerp_batch<OPS, DL>), dim3(g), dim3(kStreamBlock), 0, s, timing->start, \
-                                  timing->stop, 0, x);                                                      \
+            hipExtLaunchKernelGGL((k_lerp_batch<OPS, DL, P>), dim3(g), dim3(kStreamBlock), 0, s,             \
+                                  timing->start, timing->stop, 0, x);                                       \
         else                                                                                                \
-            hipLaunchKernelGGL((k_lerp_batch<OPS, DL>), dim3(g), dim3(kStreamBlock), 0, s, x);             \
+            hipLaunchKernelGGL((k_lerp_batch<OPS, DL, P>), dim3(g), dim3(kStreamBlock), 0, s, x);          \
+    } while (0)
+    // cache-policy variants for tuning (DPWA_LERP_POLICY, as the single-learner kernel)
+#define DPWA_BATCH_LAUNCH(OPS, DL)                                                                          \
+    do {                                                                                                    \
+        switch (lerp_policy()) {                                                                            \
+        case 1: DPWA_BATCH_LAUNCH_P(OPS, DL, 1); break;                                                     \
+        case 8: DPWA_BATCH_LAUNCH_P(OPS, DL, 8); break;                                                     \
+        case 9: DPWA_BATCH_LAUNCH_P(OPS, DL, 9); break;                                                     \
+        case 16: DPWA_BATCH_LAUNCH_P(OPS, DL, 16); break;                                                   \
+        default: DPWA_BATCH_LAUNCH_P(OPS, DL, 0); break;                                                    \
+        }                                                                                                   \
     } while (0)
     if (dtype == DPWA_F32) {
         if (dual) DPWA_BATCH_LAUNCH(OpsF32, true);
@@ -611,6 +622,7 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
         else DPWA_BATCH_LAUNCH(OpsBF16, false);
     }
 #undef DPWA_BATCH_LAUNCH
+#undef DPWA_BATCH_LAUNCH_P
     return hipGetLastError();
 }
 
