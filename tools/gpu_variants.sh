@@ -12,8 +12,8 @@ for i in $(seq 1 $PASSES); do
   k=0
   for envs in "${VARS[@]}"; do
     k=$((k+1))
-    env $envs timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sweep --compute-us 0 "$@" \
+    env $envs timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ${VAR_SWEEP:---no-sweep} --compute-us 0 "$@" \
         > gpurun_out/var_${TAG}_v${k}_$i.json 2> gpurun_out/var_${TAG}_v${k}_$i.err || { echo "bench v$k/$i failed"; tail gpurun_out/var_${TAG}_v${k}_$i.err; exit 1; }
-    python3 -c "import json;d=json.load(open('gpurun_out/var_${TAG}_v${k}_$i.json'));r=d['roofline'];print('pass $i', '$envs', 'value',d['value'],'ms',d['ms_per_step'],'inloop_us',r['in_loop']['avg_launch_us'],'cold_us',r['avg_launch_us'],'frac',r['frac'])"
+    python3 -c "import json;d=json.load(open('gpurun_out/var_${TAG}_v${k}_$i.json'));r=d['roofline'];print('pass $i', '$envs', 'value',d['value'],'ms',d['ms_per_step'],'inloop_us',r['in_loop']['avg_launch_us'],'cold_us',r['avg_launch_us'],'frac',r['frac'],'sizes',[(x['numel'],x['publish'],x['learners_per_launch'],x['frac']) for x in r.get('size_sweep',[])],'rounds',[x['value'] for x in d.get('round_sweep',[])])"
   done
 done
