@@ -233,9 +233,9 @@ __device__ __forceinline__ void span_store(__amdgpu_buffer_rsrc_t r, int lane_of
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, lane_off, 0, AUX);
 }
 
-// Cache policies of the averaging kernel (tuning; DPWA_LERP_POLICY, a bit set): the peer
-// snapshot is always read `nt`; the parameters are read `nt` or, with bit 1, with the default
-// policy; the result is stored `sc1`, with bit 2 `sc0 sc1`, with bit 4 `nt sc1`.
+// Cache policies of the averaging kernel (a bit set; the product uses 8, see lerp_policy()):
+// the peer snapshot is always read `nt`; the parameters are read `nt` or, with bit 1, with the
+// default policy; the result is stored `sc1`, with bit 2 `sc0 sc1`, with bit 4 `nt sc1`.
 template <int POLICY> struct LerpPolicy {
     static constexpr int param_load = (POLICY & 1) ? 0 : kAuxStream;
     static constexpr int base_store = kAuxStore | ((POLICY & 2) ? 1 : 0) | ((POLICY & 4) ? kAuxStream : 0);
@@ -243,8 +243,8 @@ template <int POLICY> struct LerpPolicy {
     // later; this learner's parameters, re-read by its next average one average later, keep
     // the Infinity Cache)
     static constexpr int snap_store = base_store | ((POLICY & 16) ? kAuxStream : 0);
-    // bit 8: the parameters (re-read only two averages later, past the Infinity Cache's
-    // reach) are stored `nt`, leaving the cache to the snapshot the peer reads next
+    // bit 8: the parameters are stored `nt`, leaving the Infinity Cache to the snapshot a peer
+    // reads next (the product policy)
     static constexpr int store = base_store | ((POLICY & 8) ? kAuxStream : 0);
 };
 
@@ -466,12 +466,19 @@ static hipError_t launch_blocks(void *param, const void *peer, int64_t n, const 
     return hipGetLastError();
 }
 
+// The product policy is 8 (parameters stored `nt`, the snapshot `sc1`): with the batched
+// dispatch it lifts every cold averaging kernel by 1-3 % of peak (11.17M batched 0.78 -> 0.80-0.81,
+// 7B bf16 full 0.81 -> 0.82) and leaves the N=1 loop within noise (-0.4 %, two interleaved passes
+// with sweeps, profiles/r03_policy_ab.log).  Round 2's one-launch-per-learner loop lost 2-5 % with it
+// (profiles/r02_policy_ab2.json).  DPWA_LERP_POLICY overrides (tuning).
+constexpr int kProductPolicy = 8;
+
 static int lerp_policy()
 {
     static const int forced = [] {
         const char *e = getenv("DPWA_LERP_POLICY");
-        const int p = e ? atoi(e) : 0;
-        return (p >= 0 && p <= 31) ? p : 0;
+        const int p = e ? atoi(e) : kProductPolicy;
+        return (p >= 0 && p <= 31) ? p : kProductPolicy;
     }();
     return forced;
 }
