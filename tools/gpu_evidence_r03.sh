@@ -18,7 +18,7 @@ for L in 2 1; do
         || { echo "$c pass x$L failed"; tail gpurun_out/pmc_${c}_x$L.log; exit 1; }
   done
   k="k_lerp<dpwa::OpsF32, 2, true,"; suf=""
-  [ $L -gt 1 ] && { k="k_lerp_batch<dpwa::OpsF32, true>"; suf="_x$L"; }
+  [ $L -gt 1 ] && { k="k_lerp_batch<dpwa::OpsF32, true"; suf="_x$L"; }
   python3 tools/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE_x$L gpurun_out/pmc_WRITE_SIZE_x$L --kernel "$k" \
       --publish write-through --learners $L --basis cold --out gpurun_out/traffic_${TAG}_write-through$suf.json || exit 1
 done
