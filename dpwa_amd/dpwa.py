@@ -350,59 +350,61 @@ class DpwaConnection:
     # ---------------------------------------------------------------- extensions
     @staticmethod
     def update_wait_average_many(conns, parameters, losses, write_through=False):
-        """update_wait_average of several connections of this process whose learners share a
-        GPU (co-resident learners of a LocalGroup), in the given order: each fetch is resolved
-        as the single calls would resolve it, and the averages run as ONE dispatch instead of
-        one per learner (same results; a kernel boundary and a launch ramp/drain fewer per
-        extra learner).  Returns the list of what update_wait returns, per connection."""
+        """update_wait_average of several connections of this process (the learners of a
+        LocalGroup): each fetch is resolved as the single calls would resolve it, and the
+        averages of the learners that share a GPU run as ONE dispatch on that GPU's current
+        stream instead of one per learner (same results; a kernel boundary and a launch
+        ramp/drain fewer per extra learner).  Returns the list of what update_wait returns,
+        per connection."""
         if not (len(conns) == len(parameters) == len(losses)):
             raise ValueError("update_wait_average_many: %d connections, %d buffers, %d losses"
                              % (len(conns), len(parameters), len(losses)))
-        # the ctypes argument arrays of this set of connections, reused across rounds (the call
-        # is on the per-round path: its host cost must stay well under the dispatch it replaces)
+        # the ctypes argument arrays of this set of connections, per device, reused across rounds
+        # (the call is on the per-round path: its host cost must stay well under the dispatch it
+        # replaces)
         key = tuple((c._node.value, c._learner.device.index) if c._learner is not None else None for c in conns)
         calls = _MANY_CALLS
         cache = calls.get(key)
         if cache is None:
-            bound = [i for i, c in enumerate(conns) if c._learner is not None]
-            if not bound:
-                return [(None, 0)] * len(conns)
-            dev = conns[bound[0]]._learner.device
-            if any(conns[i]._learner.device != dev for i in bound):
-                raise ValueError("update_wait_average_many: the learners are on different devices")
-            k = len(bound)
-            nodes = (ctypes.c_void_p * k)(*[conns[i]._node.value for i in bound])
-            cache = (bound, dev.index, nodes, (ctypes.c_void_p * k)(), (ctypes.c_double * k)(),
-                     (ctypes.c_void_p * k)(), (ctypes.c_int * k)(), conns[bound[0]]._lib)
+            by_dev = {}
+            for i, c in enumerate(conns):
+                if c._learner is not None:
+                    by_dev.setdefault(c._learner.device.index, []).append(i)
+            cache = []
+            for dev_index, bound in by_dev.items():     # one dispatch per device, node order kept
+                k = len(bound)
+                nodes = (ctypes.c_void_p * k)(*[conns[i]._node.value for i in bound])
+                cache.append((bound, dev_index, nodes, (ctypes.c_void_p * k)(), (ctypes.c_double * k)(),
+                              (ctypes.c_void_p * k)(), (ctypes.c_int * k)(), conns[bound[0]]._lib))
             if len(calls) > 64:
                 calls.clear()
             calls[key] = cache
-        bound, dev_index, nodes, flats, hs, ds, peers, lib = cache
-        flags = _lib.FLAG_WRITE_THROUGH if write_through else 0
-        keep = []
-        for j, i in enumerate(bound):
-            c = conns[i]
-            learner = c._learner
-            if learner.take_status():
-                c._zero_division()
-            flats[j] = learner._ptr(parameters[i])
-            h, d, learner._keep = learner.loss_args(losses[i])
-            keep.append(learner._keep)
-            hs[j] = h
-            ds[j] = d.value if d is not None else None
-            flags |= c._flags
-        rc = lib.dpwa_node_update_wait_average_many(nodes, flats, hs, ds, len(bound), flags,
-                                                     torch._C._cuda_getCurrentRawStream(dev_index), peers)
-        for i in bound:
-            conns[i].fetching = False
-        if rc:
-            raise _lib.DpwaError("dpwa_node_update_wait_average_many", rc,
-                                 lib.dpwa_last_error().decode(errors="replace"))
         out = [(None, 0)] * len(conns)
-        for j, i in enumerate(bound):
-            if peers[j] >= 0:
+        keep = []
+        for bound, dev_index, nodes, flats, hs, ds, peers, lib in cache:
+            flags = _lib.FLAG_WRITE_THROUGH if write_through else 0
+            for j, i in enumerate(bound):
                 c = conns[i]
-                out[i] = (PeerSnapshot(c, peers[j], c._learner.version), DeviceFactor(c._learner))
+                learner = c._learner
+                if learner.take_status():
+                    c._zero_division()
+                flats[j] = learner._ptr(parameters[i])
+                h, d, learner._keep = learner.loss_args(losses[i])
+                keep.append(learner._keep)
+                hs[j] = h
+                ds[j] = d.value if d is not None else None
+                flags |= c._flags
+            rc = lib.dpwa_node_update_wait_average_many(nodes, flats, hs, ds, len(bound), flags,
+                                                         torch._C._cuda_getCurrentRawStream(dev_index), peers)
+            for i in bound:
+                conns[i].fetching = False
+            if rc:
+                raise _lib.DpwaError("dpwa_node_update_wait_average_many", rc,
+                                     lib.dpwa_last_error().decode(errors="replace"))
+            for j, i in enumerate(bound):
+                if peers[j] >= 0:
+                    c = conns[i]
+                    out[i] = (PeerSnapshot(c, peers[j], c._learner.version), DeviceFactor(c._learner))
         return out
 
     @property

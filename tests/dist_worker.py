@@ -402,3 +402,53 @@ def resnet_worker(rank, world, port, cfg_path, out_dir, T, group):
     dist.barrier()
     conn.close()
     dist.destroy_process_group()
+
+
+def async_timeout_worker(rank, world, port, cfg_path, out_dir, n, T, hold_round, pull="copy"):
+    """Free-running rounds (the gossip board) where rank 0's pull of round `hold_round` is held
+    on its side stream behind a ~0.6 s spin kernel and its update_wait comes 0.3 s later, past
+    the config's timeout_ms (100): that request times out (conn.py:304-309), the loop picks
+    again and the re-selected pull goes to the rescue buffer.  Records what async_worker
+    records plus the fetch attempts and scores."""
+    import ctypes
+    import time
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from dpwa_amd import DpwaConnection, _lib
+    names = ["r%d" % i for i in range(world)]
+    conn = DpwaConnection(names[rank], cfg_path, seed=710 + rank, group="async", pull=pull)
+    flat = torch.empty(n, device=dev, dtype=torch.float32)
+    bases = [torch.from_numpy(async_base(rank, r, n)).to(dev) for r in range(T)]
+    params, clocks, peers, versions, scores, attempts = np.zeros((T, n), np.float32), np.zeros(T), [], [], [], []
+    for r in range(T):
+        flat.copy_(bases[r])
+        held = rank == 0 and r == hold_round
+        if held:
+            s = ctypes.c_void_p()
+            _lib.call("dpwa_learner_side_stream", conn._learner.handle, ctypes.byref(s))
+            with torch.cuda.stream(torch.cuda.ExternalStream(s.value, device=dev)):
+                torch.cuda._sleep(1_500_000_000)        # this round's pull queues behind it
+        conn.update_send(flat, async_loss(rank, r))
+        if held:
+            time.sleep(0.3)                             # past timeout_ms
+        payload, _ = conn.update_wait_average(flat, async_loss(rank, r, wait=True))
+        peers.append(payload.peer if payload is not None else "")
+        versions.append(conn._info()[2] if payload is not None else 0)
+        attempts.append(conn.last_fetch_attempts)
+        params[r] = flat.cpu().numpy()
+        clocks[r] = conn.clock
+        scores.append([conn.flow_control_scores()[p] for p in names if p != names[rank]])
+        if held:
+            torch.cuda.synchronize()                    # the stalled pull has landed
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=params, clocks=clocks, peers=np.array(peers),
+             versions=np.array(versions, dtype=np.int64), attempts=np.array(attempts),
+             scores=np.array([[-1 if s is None else s for s in row] for row in scores]))
+    dist.barrier()
+    conn.close()
+    dist.destroy_process_group()

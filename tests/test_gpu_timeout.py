@@ -143,3 +143,54 @@ def test_slow_but_in_time_pull_is_data(tmp_path):
             assert conns[g].flow_control_scores() == dict(zip([x for x in names if x != names[g]], scores[g]))
     for c in conns:
         c.close()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("pull", ["copy", "kernel:256"])
+def test_board_pull_times_out_and_the_rescue_pull_reads_a_whole_snapshot(tmp_path, pull):
+    """Free-running rounds over the gossip board, two ranks on one GPU: rank 0's pull of round 3
+    is held past timeout_ms.  Its only peer is scored -100 and disconnected, picked again
+    (reconnect: the board still shows it live), and the rescue pull's snapshot is a whole,
+    consistent version: every average of rank 0 equals the oracle lerp with the version the
+    board handed out (oracle/async_check.py), versions never go backwards, and the scores follow
+    the reference's increments (+10 per reply, -100 for the timeout)."""
+    import torch.multiprocessing as mp
+    from oracle.async_check import AsyncRuns
+    from tests import dist_worker
+    world, n, T, hold = 2, 200_003, 8, 3
+    names = ["r%d" % i for i in range(world)]
+    cfg = str(tmp_path / "to_board.yaml")
+    dist_worker.write_cfg(cfg, names, 1.0, "constant", 0.0)
+    text = open(cfg).read().replace("- timeout_ms: 2500", "- timeout_ms: 100")
+    open(cfg, "w").write(text)
+    mp.spawn(dist_worker.async_timeout_worker, args=(world, _free_port(), cfg, str(tmp_path), n, T, hold, pull),
+             nprocs=world, join=True)
+    runs = {g: np.load(tmp_path / ("rank%d.npz" % g)) for g in range(world)}
+    check = AsyncRuns(names, {g: runs[g]["peers"] for g in range(world)},
+                      {g: runs[g]["versions"] for g in range(world)}, "constant", 0.5, 0.0)
+    for g in range(world):
+        bad = check.check_rank(g, runs[g]["params"], runs[g]["clocks"], n)
+        assert not bad, (g, bad[:5])
+    r0 = runs[0]
+    assert int(r0["attempts"][hold]) == 2 and str(r0["peers"][hold]) == "r1"     # a timeout, then data
+    # scores of r1 as seen by r0: 1000 (max) until the timeout, 1000 - 100 + 10 after it, +10 per
+    # later reply (conn.py:264-272)
+    seen = [int(x[0]) for x in r0["scores"]]
+    exp, sc = [], 1000
+    for r in range(T):
+        if str(r0["peers"][r]) == "" and r != hold:
+            exp.append(sc)       # (an empty reply before r1's first publish is +10 too: capped)
+            continue
+        if r == hold:
+            sc = max(sc - 100, 10)
+        sc = min(sc + 10, 1000)
+        exp.append(sc)
+    assert seen == exp, (seen, exp)
