@@ -1,0 +1,49 @@
+"""bench.py's N>1 path as the driver starts it, on one GPU over gloo (RCCL refuses two ranks per
+GPU): `python bench.py --gpus 2` with no launcher starts torch.distributed.run as a child and
+must print exactly one result line, every parity transport true; an exception injected at the
+end of one transport on one rank must turn into that transport's `false` with the line still
+printed and exit status 1."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+ARGS = ["--gpus", "2", "--dist-backend", "gloo", "--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-sweep",
+        "--compute-us", "0", "--no-secondary", "--trial-passes", "1", "--trial-ms", "5"]
+
+
+def _bench(extra_env=None):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(extra_env or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + ARGS, cwd=ROOT, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=280)
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    return p.returncode, lines, p.stderr
+
+
+def test_self_launched_two_ranks_print_one_line():
+    rc, lines, err = _bench()
+    assert rc == 0, err[-3000:]
+    assert len(lines) == 1, lines
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    parity = {k: v for k, v in out["parity"].items() if k != "workload"}
+    assert len(parity) == 10 and all(parity.values()), parity
+    assert out["parity_of_timed_transport"]["ok"]
+
+
+def test_injected_transport_failure_is_isolated():
+    rc, lines, err = _bench({"DPWA_BENCH_INJECT": "lockstep/kernel:256@1:end"})
+    assert rc == 1, err[-3000:]
+    assert len(lines) == 1, lines
+    out = json.loads(lines[0])
+    assert out["parity"]["lockstep/kernel:256"] is False
+    assert all(v for k, v in out["parity"].items() if k not in ("workload", "lockstep/kernel:256"))
+    assert out["value"] > 0 and not any(k.startswith("kernel") for k in out["pull_trials_gbs"])
