@@ -874,7 +874,7 @@ def main(argv=None):
     wd.enter("start: world %d, numel %d %s" % (world, args.numel, args.dtype), 600.0)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        wd.enter("cpu baseline", 600.0)
+        wd.enter("cpu baseline", 600.0 + 20.0 * args.cpu_seconds)
         cpu = cpu_baseline(args.numel, args.cpu_seconds, rows=not args.no_cpu_rows)
     # one GPU per rank; the modulo only matters for rehearsals with more ranks than GPUs
     wd.enter("gpu init", 600.0)
