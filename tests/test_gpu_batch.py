@@ -16,7 +16,7 @@ from oracle import gossip as ogossip
 from oracle import lerp as olerp
 from oracle import policy as opolicy
 from tests.test_gpu_gossip import Net
-from tests.test_gpu_kernels import average_slot, from_u16, ptr, stream, to_u16
+from tests.test_gpu_kernels import average_slot, from_u16, header_bytes, stream, to_u16
 
 pytestmark = pytest.mark.gpu
 
@@ -259,3 +259,41 @@ def test_wire_write_through_serves_the_update_send_loss(tmp_path):
         assert olerp.bits_equal(flats[g].cpu().numpy(), exp["params"][-1, g]), g
         assert conns[g].clock == exp["clocks"][-1, g]
         conns[g].close()
+
+
+def test_average_many_beyond_4gib_offsets():
+    """Two bf16 entries of 2^31 + 1001 elements (4.3 GB per operand: byte offsets past 2^32) in one
+    batched write-through dispatch: sampled windows at the start, around 2^30 and 2^31 elements
+    and at the ragged end of both entries, against the oracle bf16 lerp of the same windows."""
+    n = (1 << 31) + 1001
+    cfg = _lib.Interp(_lib.INTERP_CLOCK, 0, 0.0, 0.0)
+    hdr = _lib.SLOT_PAYLOAD_OFFSET // 2
+    ents = []
+    for i in range(2):
+        g = torch.Generator(device=DEV).manual_seed(70 + i)
+        p = torch.empty(n, dtype=torch.bfloat16, device=DEV).normal_(generator=g)
+        slot = torch.zeros(hdr + n, dtype=torch.bfloat16, device=DEV)
+        slot[hdr:].normal_(generator=g)
+        slot.view(torch.uint8)[:256].copy_(torch.frombuffer(bytearray(header_bytes(3.0 + i, 1.0)), dtype=torch.uint8))
+        snap = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        clock = torch.tensor([1.0 + i, -1.0], dtype=torch.float64, device=DEV)
+        coef = torch.zeros(32, dtype=torch.uint8, device=DEV)
+        ents.append(dict(p=p, slot=slot, snap=snap, clock=clock, coef=coef, my=1.0 + i, peer=3.0 + i))
+    wins = [0, (1 << 30) - 5, (1 << 31) - 7, n - 4096]
+    before = [[to_u16(e["p"][w:w + 4096]) for w in wins] for e in ents]
+    peers = [[to_u16(e["slot"][hdr + w:hdr + w + 4096]) for w in wins] for e in ents]
+    d = (_lib.AverageDesc * 2)()
+    for j, e in enumerate(ents):
+        d[j] = _lib.AverageDesc(e["p"].data_ptr(), e["slot"].data_ptr(), n, e["clock"].data_ptr(), 1.0,
+                                e["coef"].data_ptr(), e["snap"].data_ptr())
+    _lib.call("dpwa_average_many", _lib.BF16, d, 2, ctypes.byref(cfg), stream(), None, None)
+    torch.cuda.synchronize()
+    for j, e in enumerate(ents):
+        f, new_clock = opolicy.factor_and_clock("clock", None, 0.0, e["my"], e["peer"], 1.0, 1.0)
+        assert e["clock"][1].item() == new_clock
+        for k, w in enumerate(wins):
+            want = olerp.lerp_bf16(before[j][k], peers[j][k], f)
+            assert olerp.bits_equal(to_u16(e["p"][w:w + 4096]), want), (j, w)
+            assert olerp.bits_equal(to_u16(e["snap"][w:w + 4096]), want), (j, w)
+    del ents
+    torch.cuda.empty_cache()
