@@ -166,7 +166,25 @@ def self_launch(args, argv):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
            "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + list(argv)
     progress("self-launch: %s" % " ".join(cmd[1:]))
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, start_new_session=True)
+
+    def orphan_guard():
+        # in the child, before exec: if this process dies (even SIGKILL), torchrun gets SIGTERM and
+        # stops its ranks, so no rank outlives the job on the GPU (Linux prctl PR_SET_PDEATHSIG = 1)
+        try:
+            ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM, 0, 0, 0)
+        except Exception:   # noqa: BLE001 -- best effort
+            pass
+
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, start_new_session=True, preexec_fn=orphan_guard)
+
+    def forward(signum, _frame):   # a stop request for this process stops the whole job
+        try:
+            os.killpg(p.pid, signum)
+        except ProcessLookupError:
+            pass
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, forward)
 
     def stop():
         progress("self-launch: %.0f s limit reached, stopping the job" % args.launch_timeout)
