@@ -412,7 +412,7 @@ def cpu_baseline(numel, seconds, rows=True):
         if el >= seconds / 2:
             break
     out["c_oracle_round"] = {
-        "value": rounds * 3 * numel * 4 / el / 1e9, "unit": "GB/s", "cores": 1,
+        "value": rounds * 3 * numel * 4 / el / 1e9, "unit": "GB/s", "cores": 1, "cpu_count": os.cpu_count(),
         "sample": "%d rounds of publish-copy + fp32 lerp over %d elements (oracle/dpwa_oracle.c, -O3, 1 thread, "
                   "%.1f s): the arithmetic alone, no transport" % (rounds, numel, el),
         "ms_per_round": 1e3 * el / rounds}
@@ -429,6 +429,7 @@ def cpu_baseline(numel, seconds, rows=True):
             break
     out["torch_cpu_lerp"] = {
         "value": rounds * 3 * numel * 4 / el / 1e9, "unit": "GB/s", "cores": torch.get_num_threads(),
+        "threads": torch.get_num_threads(), "cpu_count": os.cpu_count(),
         "sample": "%d evaluations of the reference's lerp statement (pytorch.py:68) as torch-CPU fp32 eager ops "
                   "over %d elements, %.1f s" % (rounds, numel, el),
         "ms_per_round": 1e3 * el / rounds}
