@@ -361,11 +361,11 @@ __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ pa
 // The relay's fused second phase: the fused average reads the peer's snapshot stripe by stripe
 // where the relay left it (stripe s in rank s's relay buffer, the peer's own stripe in its slot,
 // ours in local HBM) instead of gathering it into staging first.
-template <class Ops, bool DUAL>
+template <class Ops, bool DUAL, int POLICY = 0>
 __global__ __launch_bounds__(kStreamBlock) void k_lerp_relay(typename Ops::V *__restrict__ param, int64_t n,
                                                              LerpArgs args, StripeSrc src)
 {
-    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, 0>(blockIdx.x, param, src, n, args);
+    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, POLICY>(blockIdx.x, param, src, n, args);
 }
 
 // Several independent fused averages in ONE dispatch (co-resident learners of one round:
@@ -635,18 +635,27 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
 
 __global__ void k_acquire_system();
 
-template <class Ops, bool DUAL>
-static void launch_relay_kernel(void *param, int64_t n, const LerpArgs &args, const StripeSrc &src, hipStream_t s,
+template <class Ops, bool DUAL, int POLICY>
+static void launch_relay_policy(void *param, int64_t n, const LerpArgs &args, const StripeSrc &src, hipStream_t s,
                                 const LaunchTiming *timing)
 {
     // every span of every stripe (the spans past the payload are range-checked away)
     const int64_t g = (int64_t)src.parts * (src.stripe / (kStreamBlock * 16));
     if (timing)
-        hipExtLaunchKernelGGL((k_lerp_relay<Ops, DUAL>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s, timing->start,
-                              timing->stop, 0, (typename Ops::V *)param, n, args, src);
+        hipExtLaunchKernelGGL((k_lerp_relay<Ops, DUAL, POLICY>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s,
+                              timing->start, timing->stop, 0, (typename Ops::V *)param, n, args, src);
     else
-        hipLaunchKernelGGL((k_lerp_relay<Ops, DUAL>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s,
+        hipLaunchKernelGGL((k_lerp_relay<Ops, DUAL, POLICY>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s,
                            (typename Ops::V *)param, n, args, src);
+}
+
+// the product cache policy (lerp_policy(): local parameters stored nt) or, forced to 0, the old one
+template <class Ops, bool DUAL>
+static void launch_relay_kernel(void *param, int64_t n, const LerpArgs &args, const StripeSrc &src, hipStream_t s,
+                                const LaunchTiming *timing)
+{
+    if (lerp_policy() == 8) launch_relay_policy<Ops, DUAL, 8>(param, n, args, src, s, timing);
+    else launch_relay_policy<Ops, DUAL, 0>(param, n, args, src, s, timing);
 }
 
 hipError_t launch_average_relay(int32_t dtype, void *param, int64_t n, const FusedArgs &fa, void *snap,
