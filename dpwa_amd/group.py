@@ -155,6 +155,16 @@ class _FdServer:
         except Exception as e:      # reported by finish()
             self.error = e
 
+    def abort(self):
+        """Stops serving now (the exchange failed elsewhere): no one gets the fds."""
+        self._allowed = set()
+        self._ready.set()
+        try:
+            self.sock.shutdown(socket.SHUT_RDWR)
+        except OSError:
+            pass
+        self.sock.close()
+
     def finish(self):
         self.thread.join(self.TIMEOUT_S)
         self.sock.close()
@@ -254,7 +264,15 @@ class DistGroup:
                     for fd in fds:
                         os.close(fd)
                 conn._set_peer(k, _lib.NODE_PEER_REMOTE, None)
-        finally:
+        except BaseException:
+            if server is not None:      # do not leave the serving thread in accept() for TIMEOUT_S
+                server.abort()
+                server.thread.join(5)
+                for fd in server.fds:
+                    os.close(fd)
+                server.fds = []
+            raise
+        else:
             if server is not None:
                 server.finish()
         if self.relay_blocks:

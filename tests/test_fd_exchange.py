@@ -82,3 +82,22 @@ def test_fds_are_served_only_to_the_ranks():
         os.close(fd)
     server.finish()
     assert server.rejected == 1
+
+
+def test_abort_stops_serving_at_once():
+    """An exchange that failed elsewhere (on_bind's collective raised): abort() ends the serving
+    thread immediately instead of leaving it in accept() for TIMEOUT_S."""
+    import time
+    from dpwa_amd.group import _FdServer, _fetch_fds
+    fd = os.memfd_create("c")
+    server = _FdServer([fd], 2)
+    t0 = time.monotonic()
+    server.abort()
+    server.thread.join(5)
+    assert not server.thread.is_alive() and time.monotonic() - t0 < 5
+    try:
+        _fetch_fds(server.address, 1)
+        raise AssertionError("an aborted server handed out fds")
+    except OSError:
+        pass
+    os.close(fd)
