@@ -297,3 +297,37 @@ def test_average_many_beyond_4gib_offsets():
             assert olerp.bits_equal(to_u16(e["snap"][w:w + 4096]), want), (j, w)
     del ents
     torch.cuda.empty_cache()
+
+
+def test_update_wait_average_many_unaligned_buffers_fall_back(tmp_path):
+    """Flat buffers that are not 16-B aligned (views at a 4-byte offset) cannot join the batched
+    dispatch: each such average is launched on its own (the element-wise kernel), with the same
+    results as the single calls -- checked against oracle/gossip.py."""
+    G, n, T = 3, 10_007, 5
+    names = ["u%d" % g for g in range(G)]
+    cfg = tmp_path / "ua.yaml"
+    _write_cfg(cfg, names, 1.0, "clock")
+    rng = np.random.default_rng(12)
+    init = rng.standard_normal((G, n)).astype(np.float32)
+    deltas = (0.01 * rng.standard_normal((T, G, n))).astype(np.float32)
+    send = [[1.0 + g + r for g in range(G)] for r in range(T)]
+    wait = [[1.5 + g + r for g in range(G)] for r in range(T)]
+    seeds = [500 + g for g in range(G)]
+    exp = ogossip.simulate(names, init, deltas, send, wait, "clock", None, 0.0, 1.0, seeds)
+    group = LocalGroup()
+    conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group) for g in range(G)]
+    backing = [torch.zeros(n + 1, device=DEV) for _ in range(G)]
+    flats = [b[1:] for b in backing]                       # 4-byte offset: not 16-B aligned
+    for g in range(G):
+        flats[g].copy_(torch.from_numpy(init[g]).to(DEV))
+    for r in range(T):
+        for g in range(G):
+            conns[g].update_send(flats[g], send[r][g], reuse_snapshot=r > 0)
+        for g in range(G):
+            flats[g].add_(torch.from_numpy(deltas[r, g]).to(DEV))
+        DpwaConnection.update_wait_average_many(conns, flats, wait[r], write_through=True)
+        for g in range(G):
+            assert olerp.bits_equal(flats[g].cpu().numpy(), exp["params"][r, g]), (r, g)
+            assert conns[g].clock == exp["clocks"][r, g]
+    for c in conns:
+        c.close()
