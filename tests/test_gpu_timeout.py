@@ -194,3 +194,78 @@ def test_board_pull_times_out_and_the_rescue_pull_reads_a_whole_snapshot(tmp_pat
         sc = min(sc + 10, 1000)
         exp.append(sc)
     assert seen == exp, (seen, exp)
+
+
+def test_stalled_rescue_pull_ends_the_round_without_data(tmp_path):
+    """Both the side stream and the rescue stream stalled: the first pull times out, the
+    re-selected rescue pull times out too, and the next pick finds the rescue buffer still
+    taken -- that request times out and the round ends without data (the learner's own
+    transport is stuck; the reference would keep picking).  Three timeouts, -100 each, no average
+    -- the oracle policy with three scripted timeouts and the loop cut after them."""
+    G = 3
+    names = ["x%d" % g for g in range(G)]
+    cfg = tmp_path / "stall.yaml"
+    write_cfg(cfg, names, timeout_ms=100)
+    rng = np.random.default_rng(5)
+    n, T = 50_003, 3
+    init = rng.standard_normal((G, n)).astype(np.float32)
+    send = [[1.0 + g + r for g in range(G)] for r in range(T)]
+    wait = [[2.0 + g + r for g in range(G)] for r in range(T)]
+    seeds = [90 + g for g in range(G)]
+    # the oracle: round 1 of learner 0 -> one timeout then data; round 2 -> three timeouts, no data
+    idx = {nm: i for i, nm in enumerate(names)}
+    L = [OracleLearner(names[g], [x for x in names if x != names[g]], 1.0, "clock", None, 0.0, seeds[g])
+         for g in range(G)]
+    params = init.copy()
+    exp = []
+    for r in range(T):
+        states = [L[g].update_send(send[r][g]) for g in range(G)]
+        snaps = [params[g].copy() for g in range(G)]
+        for g in range(G):
+            n_req = [0]
+
+            def request(peer, g=g, r=r, n_req=n_req):
+                n_req[0] += 1
+                if g == 0 and ((r == 1 and n_req[0] == 1) or r == 2):
+                    return "timeout", None, None
+                return "payload", states[idx[peer]], snaps[idx[peer]]
+
+            state, payload, attempts = L[g].fetch(lambda p: "ok", request,
+                                                  max_attempts=3 if (g == 0 and r == 2) else None)
+            averaged, factor = L[g].update_wait(wait[r][g], state, payload is not None)
+            if averaged:
+                params[g] = olerp.lerp_f32(params[g], payload, factor)
+        exp.append((params.copy(), [L[g].clock for g in range(G)],
+                    [L[g].scores([x for x in names if x != names[g]]) for g in range(G)]))
+    group = LocalGroup(prefetch=True, zero_copy=False)
+    conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group) for g in range(G)]
+    flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
+    import time
+    rescue = None
+    for r in range(T):
+        if r in (1, 2):
+            with torch.cuda.stream(side_stream(conns[0])):
+                torch.cuda._sleep(HOLD_CYCLES)
+        if r == 2:
+            with torch.cuda.stream(rescue):
+                torch.cuda._sleep(2 * HOLD_CYCLES)       # the rescue pull queues behind this
+        for g in range(G):
+            conns[g].update_send(flats[g], send[r][g])
+        if r in (1, 2):
+            time.sleep(0.3)
+        got = [conns[g].update_wait_average(flats[g], wait[r][g]) for g in range(G)]
+        if r == 1:   # the stream the rescue pull ran on
+            s = ctypes.c_void_p()
+            _lib.call("dpwa_learner_fetch_stream", conns[0]._learner.handle, ctypes.byref(s))
+            rescue = torch.cuda.ExternalStream(s.value, device=DEV)
+            assert rescue.cuda_stream != side_stream(conns[0]).cuda_stream
+        torch.cuda.synchronize()
+        p_exp, c_exp, s_exp = exp[r]
+        if r == 2:
+            assert got[0][0] is None and conns[0].last_fetch_attempts == 3
+        for g in range(G):
+            assert olerp.bits_equal(flats[g].cpu().numpy(), p_exp[g]), (r, g)
+            assert conns[g].clock == c_exp[g], (r, g)
+            assert conns[g].flow_control_scores() == dict(zip([x for x in names if x != names[g]], s_exp[g])), (r, g)
+    for c in conns:
+        c.close()
