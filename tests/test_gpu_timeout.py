@@ -196,12 +196,14 @@ def test_board_pull_times_out_and_the_rescue_pull_reads_a_whole_snapshot(tmp_pat
     assert seen == exp, (seen, exp)
 
 
-def test_stalled_rescue_pull_ends_the_round_without_data(tmp_path):
-    """Both the side stream and the rescue stream stalled: the first pull times out, the
-    re-selected rescue pull times out too, and the next pick finds the rescue buffer still
-    taken -- that request times out and the round ends without data (DESIGN §4: the learner's own
-    transport is stuck; the reference would keep picking).  Three timeouts, -100 each, no average
-    -- the oracle policy with three scripted timeouts and the loop cut after them."""
+def _stalled_rescue(_rank, tmp):
+    import os
+    import pathlib
+    # a hardware queue per stream: the spin kernels that stall learner 0's side and rescue streams
+    # must not hold the other learners' streams too (with the default 4 queues per process a
+    # stream may share one; read before the HIP runtime starts in this fresh process)
+    os.environ["GPU_MAX_HW_QUEUES"] = "12"
+    tmp_path = pathlib.Path(tmp)
     G = 3
     names = ["x%d" % g for g in range(G)]
     cfg = tmp_path / "stall.yaml"
@@ -217,7 +219,7 @@ def test_stalled_rescue_pull_ends_the_round_without_data(tmp_path):
     L = [OracleLearner(names[g], [x for x in names if x != names[g]], 1.0, "clock", None, 0.0, seeds[g])
          for g in range(G)]
     params = init.copy()
-    exp = []
+    exp, picks = [], []
     for r in range(T):
         states = [L[g].update_send(send[r][g]) for g in range(G)]
         snaps = [params[g].copy() for g in range(G)]
@@ -235,8 +237,9 @@ def test_stalled_rescue_pull_ends_the_round_without_data(tmp_path):
             averaged, factor = L[g].update_wait(wait[r][g], state, payload is not None)
             if averaged:
                 params[g] = olerp.lerp_f32(params[g], payload, factor)
+            picks.append([a["peer"] for a in attempts])
         exp.append((params.copy(), [L[g].clock for g in range(G)],
-                    [L[g].scores([x for x in names if x != names[g]]) for g in range(G)]))
+                    [L[g].scores([x for x in names if x != names[g]]) for g in range(G)], picks[-G:]))
     group = LocalGroup(prefetch=True, zero_copy=False)
     conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group) for g in range(G)]
     flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
@@ -260,12 +263,27 @@ def test_stalled_rescue_pull_ends_the_round_without_data(tmp_path):
             rescue = torch.cuda.ExternalStream(s.value, device=DEV)
             assert rescue.cuda_stream != side_stream(conns[0]).cuda_stream
         torch.cuda.synchronize()
-        p_exp, c_exp, s_exp = exp[r]
+        p_exp, c_exp, s_exp, pk_exp = exp[r]
         if r == 2:
             assert got[0][0] is None and conns[0].last_fetch_attempts == 3
         for g in range(G):
+            peer = got[g][0].peer if got[g][0] is not None else ""
+            assert (peer, conns[g].last_fetch_attempts) == ((pk_exp[g][-1] if g or r != 2 else ""), len(pk_exp[g])), \
+                (r, g, peer, conns[g].last_fetch_attempts, pk_exp[g])
+            assert conns[g].flow_control_scores() == dict(zip([x for x in names if x != names[g]], s_exp[g])), (r, g)
             assert olerp.bits_equal(flats[g].cpu().numpy(), p_exp[g]), (r, g)
             assert conns[g].clock == c_exp[g], (r, g)
             assert conns[g].flow_control_scores() == dict(zip([x for x in names if x != names[g]], s_exp[g])), (r, g)
     for c in conns:
         c.close()
+
+
+def test_stalled_rescue_pull_ends_the_round_without_data(tmp_path):
+    """Both the side stream and the rescue stream stalled: the first pull times out, the
+    re-selected rescue pull times out too, and the next pick finds the rescue buffer still
+    taken -- that request times out and the round ends without data (DESIGN §4: the learner's own
+    transport is stuck; the reference would keep picking).  Three timeouts, -100 each, no average
+    -- the oracle policy with three scripted timeouts and the loop cut after them.  Runs in a
+    fresh process (its own hardware-queue setting)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_stalled_rescue, args=(str(tmp_path),), nprocs=1, join=True)
