@@ -379,7 +379,8 @@ struct dpwa_learner {
     bool relay_deferred = false;
     RelayArgs relay_saved{};
     int relay_saved_pick = -1, relay_saved_blocks = 0;
-    // host readers of published slots (wire bridge) run on other threads
+    // host readers of published slots (wire bridge) run on other threads; their stream is created
+    // at the first read, under pub_mu
     std::mutex pub_mu;
     hipStream_t read_stream = nullptr;
     hipEvent_t ev_read = nullptr;
@@ -521,8 +522,6 @@ int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype
         if (e != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_factor, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_wt, hipEventDisableTiming)) != hipSuccess) break;
-        if ((e = hipEventCreateWithFlags(&l->ev_read, hipEventDisableTiming)) != hipSuccess) break;
-        if ((e = hipStreamCreateWithFlags(&l->read_stream, hipStreamNonBlocking)) != hipSuccess) break;
         if ((e = hipHostMalloc((void **)&l->host_status, sizeof(int32_t), hipHostMallocMapped)) != hipSuccess) break;
         *l->host_status = 0;
         if ((e = hipHostGetDevicePointer((void **)&l->host_status_dev, l->host_status, 0)) != hipSuccess) break;
@@ -1226,6 +1225,11 @@ int dpwa_learner_read_snapshot(dpwa_learner *l, void *header_out, void *payload_
                 return DPWA_OK;   // nothing published: the reference replies without state
             }
             k = (int)((v - 1) % 2);
+            if (!l->read_stream) {   // created at the first host read: no stream (and no hardware
+                                     // queue share) for learners nobody reads over the wire
+                HIP_TRY(hipEventCreateWithFlags(&l->ev_read, hipEventDisableTiming));
+                HIP_TRY(hipStreamCreateWithFlags(&l->read_stream, hipStreamNonBlocking));
+            }
             // order after the publish (and everything before it) on the publisher's stream
             HIP_TRY(hipEventRecord(l->ev_read, l->publish_stream[k]));
         }
