@@ -829,7 +829,11 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
         // publish of the snapshot (above, local peers) and after the last reader of the buffer
         if (!l->rescue_buf) {
             HIP_TRY(hipMalloc(&l->rescue_buf, l->slot_stride));
-            HIP_TRY(hipStreamCreateWithFlags(&l->rescue_stream, hipStreamNonBlocking));
+            // the greatest priority: a hardware queue of its own, not one a stalled normal-priority
+            // stream (the side stream, or any other of the process's streams) may share
+            int least = 0, greatest = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            HIP_TRY(hipStreamCreateWithPriority(&l->rescue_stream, hipStreamNonBlocking, greatest));
             HIP_TRY(hipEventCreateWithFlags(&l->ev_rescue, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&l->ev_stage_done[2], hipEventDisableTiming));
         }

@@ -197,12 +197,7 @@ def test_board_pull_times_out_and_the_rescue_pull_reads_a_whole_snapshot(tmp_pat
 
 
 def _stalled_rescue(_rank, tmp):
-    import os
     import pathlib
-    # a hardware queue per stream: the spin kernels that stall learner 0's side and rescue streams
-    # must not hold the other learners' streams too (with the default 4 queues per process a
-    # stream may share one; read before the HIP runtime starts in this fresh process)
-    os.environ["GPU_MAX_HW_QUEUES"] = "12"
     tmp_path = pathlib.Path(tmp)
     G = 3
     names = ["x%d" % g for g in range(G)]
@@ -284,6 +279,6 @@ def test_stalled_rescue_pull_ends_the_round_without_data(tmp_path):
     taken -- that request times out and the round ends without data (the learner's own
     transport is stuck; the reference would keep picking).  Three timeouts, -100 each, no average
     -- the oracle policy with three scripted timeouts and the loop cut after them.  Runs in a
-    fresh process (its own hardware-queue setting)."""
+    fresh process (a stream map of its own).""" 
     import torch.multiprocessing as mp
     mp.spawn(_stalled_rescue, args=(str(tmp_path),), nprocs=1, join=True)
