@@ -83,7 +83,7 @@ def test_configs0_resnet18_four_learners_training(tmp_path):
             loss = F.cross_entropy(nets[g](x), y)
             loss.backward()
             opts[g].step()
-            wait.append(loss.item() *(0.1 if r >= 3 else 1.0))         # from round 3 below the threshold
+            wait.append(loss.item() * (0.1 if r >= 3 else 1.0))         # from round 3 below the threshold
         before = [a.flat.buffer.cpu().numpy() for a in adapters]
         for g in range(G):
             adapters[g].update_wait(wait[g])
