@@ -14,6 +14,11 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs on the GPU box via gpurun)")
 
 
+def pytest_report_header(config):
+    from dpwa_amd import _lib
+    return "native library: %s" % _lib.LIB_PATH
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
