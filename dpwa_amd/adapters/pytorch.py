@@ -10,10 +10,12 @@ Differences that are intentional: the average is written in place (the reference
 rebinds ``param.data`` to a new tensor), and float32 *and* bfloat16 models are accepted
 (the reference maps only FloatTensor, pytorch.py:11-14).
 """
+import ctypes
 import logging
 
 import torch
 
+from .. import _lib
 from ..dpwa import DpwaConfiguration, DpwaConnection
 from ..flat import FlatParameters
 
@@ -30,10 +32,14 @@ class DpwaPyTorchAdapter:
     (``param.data = ...``), that no parameter's version counter moved (optimizer steps,
     ``param.add_``, ``load_state_dict``) and that the flat buffer's own counter did not move;
     any of these forces a full publish.  In-place writes through ``param.data`` bypass version
-    counters: a loop that does that between update_wait and update_send must pass
-    ``write_through=False``."""
+    counters; for them the reuse guard (``reuse_guard``, on by default) compares 4096 16-byte
+    words spread over the parameters with the snapshot on the device and publishes in full when
+    any differs (two small kernels per update_send, no host sync).  A write that changes none
+    of the sampled words is not seen: a loop that writes parameters sparsely through
+    ``param.data`` between update_wait and update_send should pass ``write_through=False``."""
 
-    def __init__(self, net, name, config_file, write_through=True, transport="device", **connection_kwargs):
+    def __init__(self, net, name, config_file, write_through=True, transport="device", reuse_guard=True,
+                 **connection_kwargs):
         """transport: "device" (peers are learners of this process or of the torch.distributed
         job, pulled from HBM/over xGMI) or "wire" (peers are reached over TCP at the YAML's
         host/port with the reference's protocol -- e.g. reference CPU nodes; dpwa_amd/bridge.py)."""
@@ -49,6 +55,8 @@ class DpwaPyTorchAdapter:
         else:
             raise ValueError("transport must be 'device' or 'wire'")
         self._write_through = bool(write_through) and transport == "device"
+        self._reuse_guard = bool(reuse_guard)
+        self._guard_set = False
         self._versions = None
 
     def _param_versions(self):
@@ -61,6 +69,9 @@ class DpwaPyTorchAdapter:
                  and self._versions == self._param_versions())
         self._versions = None
         self._conn.update_send(self._flat.buffer, loss, reuse_snapshot=reuse)
+        if self._write_through and self._reuse_guard and not self._guard_set:    # bound by now
+            _lib.call("dpwa_learner_set_reuse_guard", self._conn._learner.handle, 1)
+            self._guard_set = True
 
     def update_wait(self, loss):
         """pytorch.py:55-68: wait for the fetch and average in place."""
@@ -90,6 +101,16 @@ class DpwaPyTorchAdapter:
         for a, (payload, _) in zip(adapters, res):
             if wt and payload is not None:
                 a._versions = a._param_versions()
+
+    @property
+    def reuse_guard_hits(self):
+        """Publishes whose reuse guard found the parameters changed behind the version counters
+        (synchronises the device; 0 before the first publish)."""
+        if self._conn._learner is None:
+            return 0
+        hits = ctypes.c_uint32()
+        _lib.call("dpwa_learner_reuse_guard_hits", self._conn._learner.handle, ctypes.byref(hits))
+        return hits.value
 
     @property
     def connection(self):

@@ -917,6 +917,78 @@ hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *c
     return hipGetLastError();
 }
 
+// Reuse guard of a header-only publish (the adapter's write-through): writes
+// through `param.data` move no version counter, so before a snapshot the last average wrote is
+// published as is, kGuardSamples 16-B words spread evenly over the parameters (first and last
+// included) and their tail bytes are compared with it.  Any difference makes the publish a full
+// one: the payload is copied from the parameters.  Two launches, so every workgroup of the copy
+// sees the same verdict: one workgroup compares and writes *dirty (and counts it in *hits), the
+// copy's workgroups return at once when it is clear.
+constexpr int kGuardSamples = 4096;
+
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void k_guard_compare(const char *__restrict__ flat,
+                                                          const char *__restrict__ payload, int64_t nbytes,
+                                                          int32_t *__restrict__ dirty, uint32_t *__restrict__ hits)
+{
+    const int64_t n16 = nbytes >> 4;
+    const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
+    int diff = 0;
+    for (int64_t k = threadIdx.x; k < samples; k += kBlock) {
+        const int64_t o = (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4;   // 0 .. n16-1
+        if (VEC) {
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(flat + o);
+            const u32x4 b = *reinterpret_cast<const u32x4 *>(payload + o);
+            diff |= (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
+        } else {
+            for (int j = 0; j < 16; ++j) diff |= flat[o + j] != payload[o + j];
+        }
+    }
+    if (threadIdx.x < (nbytes & 15)) diff |= flat[(n16 << 4) + threadIdx.x] != payload[(n16 << 4) + threadIdx.x];
+    diff = __syncthreads_or(diff);
+    if (threadIdx.x == 0) {
+        *dirty = diff;
+        if (diff) *hits += 1;
+    }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void k_copy_if(char *__restrict__ dst, const char *__restrict__ src,
+                                                    int64_t nbytes, const int32_t *__restrict__ dirty)
+{
+    if (*dirty == 0) return;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const int64_t first = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (VEC) {
+        const int64_t n16 = nbytes >> 4;
+        u32x4 *d = reinterpret_cast<u32x4 *>(dst);
+        const u32x4 *s = reinterpret_cast<const u32x4 *>(src);
+        for (int64_t i = first; i < n16; i += stride) d[i] = s[i];
+        if (blockIdx.x == 0 && threadIdx.x < (nbytes & 15)) dst[(n16 << 4) + threadIdx.x] = src[(n16 << 4) + threadIdx.x];
+    } else {
+        for (int64_t i = first; i < nbytes; i += stride) dst[i] = src[i];
+    }
+}
+
+hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes, int32_t *dirty, uint32_t *hits,
+                                hipStream_t s)
+{
+    if (nbytes <= 0) return hipSuccess;
+    const char *src = (const char *)flat;
+    if (aligned16(flat) && aligned16(payload)) {
+        int64_t g = ((nbytes >> 4) + kBlock * 4 - 1) / (kBlock * 4);
+        g = g < 1 ? 1 : g > 2048 ? 2048 : g;
+        hipLaunchKernelGGL(k_guard_compare<true>, dim3(1), dim3(kBlock), 0, s, src, payload, nbytes, dirty, hits);
+        hipLaunchKernelGGL(k_copy_if<true>, dim3((uint32_t)g), dim3(kBlock), 0, s, payload, src, nbytes, dirty);
+    } else {
+        int64_t g = blocks_for(nbytes);
+        g = g > 2048 ? 2048 : g;
+        hipLaunchKernelGGL(k_guard_compare<false>, dim3(1), dim3(kBlock), 0, s, src, payload, nbytes, dirty, hits);
+        hipLaunchKernelGGL(k_copy_if<false>, dim3((uint32_t)g), dim3(kBlock), 0, s, payload, src, nbytes, dirty);
+    }
+    return hipGetLastError();
+}
+
 // One 64-bit word into (host-mapped) memory after everything before it on the stream: a
 // system-scope release store, so the bytes written before it are visible first.  Used by
 // the gossip board (board.cpp) for versions and read marks.

@@ -111,6 +111,12 @@ hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *c
                                  const double *loss_dev, bool loss_f32, uint64_t version, bool system_release,
                                  hipStream_t s);
 
+// Reuse guard of a header-only publish: sampled words of `flat` against the snapshot `payload`
+// the last average wrote; on a difference the payload is copied from `flat` and *hits += 1
+// (*dirty: the verdict, device memory; both written by the device).
+hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes, int32_t *dirty, uint32_t *hits,
+                                hipStream_t s);
+
 // A system-scope L2 write-back on every XCD after the work already on `s` (a publish whose
 // bytes were written by an earlier kernel, read by other devices).
 hipError_t launch_release_system(hipStream_t s);

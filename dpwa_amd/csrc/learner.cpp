@@ -251,6 +251,8 @@ struct Ctl {            // device control block
                         // write-through average also writes the next publish's clock+1 into
                         // clock[cur+2], which that publish then selects without a kernel
     dpwa_coef coef;
+    int32_t guard_dirty;   // reuse guard: the last header-only publish found the parameters changed
+    uint32_t guard_hits;   // ... and how many publishes did
 };
 
 
@@ -351,6 +353,7 @@ struct dpwa_learner {
     bool wt_valid = false;
     bool wt_header = false;             // the write-through average also wrote the next header
     bool header_on_publish = false;     // never write the next header ahead (served to wire peers)
+    bool reuse_guard = false;           // check a header-only publish's parameters on the device
     const void *wt_flat = nullptr;
     hipStream_t wt_stream = nullptr;
     hipEvent_t ev_wt = nullptr;
@@ -626,6 +629,9 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
             HIP_TRY(hipEventRecord(l->ev_wt, l->wt_stream));
             HIP_TRY(hipStreamWaitEvent(s, l->ev_wt, 0));
         }
+        if (l->reuse_guard)
+            HIP_TRY(launch_guard_payload(slot + kPayloadOff, flat, (int64_t)l->payload_bytes, &l->ctl->guard_dirty,
+                                         &l->ctl->guard_hits, s));
         if (l->exported) HIP_TRY(launch_release_system(s));
         l->cur = (l->cur + 1) & 3;
     } else if (header_only) {
@@ -634,6 +640,9 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
             HIP_TRY(hipEventRecord(l->ev_wt, l->wt_stream));
             HIP_TRY(hipStreamWaitEvent(s, l->ev_wt, 0));
         }
+        if (l->reuse_guard)
+            HIP_TRY(launch_guard_payload(slot + kPayloadOff, flat, (int64_t)l->payload_bytes, &l->ctl->guard_dirty,
+                                         &l->ctl->guard_hits, s));
         HIP_TRY(launch_publish_header(slot, l->n, l->dtype, &l->ctl->clock[l->cur], loss, loss_dev, l->loss_f32,
                                       l->version + 1, l->exported, s));
     } else {
@@ -1208,6 +1217,22 @@ int dpwa_learner_set_header_publish(dpwa_learner *l, int always)
 {
     if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_set_header_publish: NULL learner");
     l->header_on_publish = always != 0;
+    return DPWA_OK;
+}
+
+int dpwa_learner_set_reuse_guard(dpwa_learner *l, int on)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_set_reuse_guard: NULL learner");
+    l->reuse_guard = on != 0;
+    return DPWA_OK;
+}
+
+int dpwa_learner_reuse_guard_hits(dpwa_learner *l, uint32_t *hits)
+{
+    if (!l || !hits) return set_error(DPWA_ERR_ARG, "dpwa_learner_reuse_guard_hits: NULL argument");
+    DeviceGuard dg(l->device);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(hits, &l->ctl->guard_hits, sizeof(uint32_t), hipMemcpyDeviceToHost));
     return DPWA_OK;
 }
 

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DPWA_ABI_VERSION 4
+#define DPWA_ABI_VERSION 5
 
 #define DPWA_OK 0
 #define DPWA_ERR_ARG (-1)     /* bad argument (API misuse)                          */
@@ -235,6 +235,13 @@ int dpwa_learner_set_header_publish(dpwa_learner *l, int always);
  * (the caller asserts `flat` is unchanged since): header only; otherwise a full publish. */
 int dpwa_learner_publish_reuse(dpwa_learner *l, const void *flat, double loss, const double *loss_dev,
                                dpwa_stream_t stream);
+/* on != 0: a reusing publish (above) first compares 4096 16-B words spread over `flat` with
+ * the written-through snapshot on the device, and copies the payload from `flat` when any
+ * differs -- a write the caller's bookkeeping missed (pytorch.py:49-53 then holds anyway: the
+ * snapshot is the parameters at update_send).  Two small launches, no host sync.
+ * reuse_guard_hits: how many publishes found a difference (synchronises the device). */
+int dpwa_learner_set_reuse_guard(dpwa_learner *l, int on);
+int dpwa_learner_reuse_guard_hits(dpwa_learner *l, uint32_t *hits);
 
 /* Split form of dpwa_learner_average for the DpwaConnection / adapter seam:
  * factor only (update_wait's return value), then lerp with the learner's coefficients. */

@@ -1,0 +1,123 @@
+"""The adapter's reuse guard: with write-through snapshots, an update_send whose parameters'
+version counters did not move publishes the snapshot the last average wrote -- unless the
+device check of sampled words finds the parameters changed (a write through ``param.data``,
+which no version counter sees).  The reference always publishes the parameters as they are at
+update_send (pytorch.py:49-53), so the learners' trajectories must equal the oracle's, which
+folds every write into the parameters before the next publish."""
+import numpy as np
+import pytest
+import torch
+
+from dpwa_amd import DpwaPyTorchAdapter
+from dpwa_amd.group import LocalGroup
+from oracle import lerp as olerp
+from tests.test_gpu_gossip import DEV, Net, load_flat, write_cfg
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(tmp_path, mode, n=100_032, T=5):
+    """Two learners averaging with constant 0.5 every round; after each update_wait, `mode`
+    writes through param.data: 'dense' (every element), 'first' / 'last' (one element: the
+    payload's first / last 16-B word, both always sampled; n is a multiple of the flat
+    buffer's 64-element alignment, so the parameter ends where the payload does), 'none'.
+    reuse_guard is off for 'unguarded' (dense)."""
+    rng = np.random.default_rng(21)
+    G = 2
+    names = ["a", "b"]
+    init = rng.standard_normal((G, n)).astype(np.float32)
+    cfg = tmp_path / ("guard_%s.yaml" % mode)
+    write_cfg(cfg, names, 1.0, "constant", 0.0, 0.5)
+    group = LocalGroup()
+    nets, adapters = [], []
+    for g in range(G):
+        net = Net([(n,)]).to(DEV)
+        load_flat(net, init[g])
+        nets.append(net)
+        adapters.append(DpwaPyTorchAdapter(net, names[g], str(cfg), seed=5 + g, group=group, write_through=True,
+                                           reuse_guard=mode != "unguarded"))
+    params = init.copy()
+    for r in range(T):
+        for g in range(G):
+            adapters[g].update_send(1.0)
+        snaps = [params[g].copy() for g in range(G)]
+        for g in range(G):
+            adapters[g].update_wait(1.0)
+            params[g] = olerp.lerp_f32(params[g], snaps[1 - g], 0.5)
+        for g in range(G):
+            bump = np.zeros(n, np.float32)
+            if mode in ("dense", "unguarded"):
+                bump[:] = (0.25 * rng.standard_normal(n)).astype(np.float32)
+            elif mode == "first":
+                bump[0] = 1.5
+            elif mode == "last":
+                bump[-1] = -2.5
+            if mode != "none":
+                with torch.no_grad():
+                    nets[g].p0.data.add_(torch.from_numpy(bump).to(DEV))    # no version counter moves
+                params[g] = np.add(params[g], bump, dtype=np.float32)
+    torch.cuda.synchronize()
+    same = [olerp.bits_equal(nets[g].p0.detach().cpu().numpy(), params[g]) for g in range(G)]
+    hits = [a.reuse_guard_hits for a in adapters]
+    for a in adapters:
+        a.connection.close()
+    return same, hits, T
+
+
+@pytest.mark.parametrize("mode", ["dense", "first", "last"])
+def test_reuse_guard_catches_writes_through_param_data(tmp_path, mode):
+    same, hits, T = _run(tmp_path, mode)
+    assert all(same), same
+    assert hits == [T - 1, T - 1], hits       # every publish after the first reused, and was caught
+
+
+def test_reuse_guard_stays_quiet_without_writes(tmp_path):
+    same, hits, _ = _run(tmp_path, "none")
+    assert all(same), same
+    assert hits == [0, 0], hits
+
+
+def test_without_the_guard_peers_get_the_stale_snapshot(tmp_path):
+    """The hazard the guard closes: the same loop with the guard off diverges from the oracle."""
+    same, hits, _ = _run(tmp_path, "unguarded")
+    assert not any(same), same
+    assert hits == [0, 0], hits
+
+
+def test_reuse_guard_compares_the_tail_bytes(tmp_path):
+    """Connection level, an odd element count (payload not a multiple of 16 bytes): a write to
+    the last element, which lies in the tail bytes, makes the reusing publish a full one."""
+    import ctypes
+
+    from dpwa_amd import DpwaConnection, _lib
+    n, T = 100_003, 4
+    names = ["a", "b"]
+    cfg = tmp_path / "tail.yaml"
+    write_cfg(cfg, names, 1.0, "constant", 0.0, 0.5)
+    rng = np.random.default_rng(4)
+    init = rng.standard_normal((2, n)).astype(np.float32)
+    group = LocalGroup()
+    conns = [DpwaConnection(names[g], str(cfg), seed=5 + g, group=group) for g in range(2)]
+    flats = [torch.from_numpy(init[g]).to(DEV) for g in range(2)]
+    params = init.copy()
+    for r in range(T):
+        for g in range(2):
+            conns[g].update_send(flats[g], 1.0, reuse_snapshot=r > 0)
+            if r == 0:
+                _lib.call("dpwa_learner_set_reuse_guard", conns[g]._learner.handle, 1)
+        snaps = [params[g].copy() for g in range(2)]
+        for g in range(2):
+            conns[g].update_wait_average(flats[g], 1.0, write_through=True)
+            params[g] = olerp.lerp_f32(params[g], snaps[1 - g], 0.5)
+        flats[0][-1] += 3.0                     # learner a only, behind the caller's assertion
+        params[0][-1] = np.float32(params[0][-1] + np.float32(3.0))
+    torch.cuda.synchronize()
+    for g in range(2):
+        assert olerp.bits_equal(flats[g].cpu().numpy(), params[g]), g
+    hits = []
+    for c in conns:
+        h = ctypes.c_uint32()
+        _lib.call("dpwa_learner_reuse_guard_hits", c._learner.handle, ctypes.byref(h))
+        hits.append(h.value)
+        c.close()
+    assert hits == [T - 1, 0], hits
