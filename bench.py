@@ -127,6 +127,8 @@ def parse(argv=None):
     ap.add_argument("--trial-ms", type=float, default=50.0,
                     help="N>1: minimum wall time of one transport trial (and at least 30 rounds)")
     ap.add_argument("--trial-passes", type=int, default=3, help="N>1: interleaved passes over the candidates")
+    ap.add_argument("--dist-sweep-max-numel", type=int, default=None,
+                    help="N>1: leave sizes above this out of the round sweep (rehearsals with ranks sharing a GPU)")
     ap.add_argument("--compute-us", type=float, default=1000.0,
                     help="per-learner synthetic training step (bf16 GEMM loop) for the 'overlap' field; 0 = skip")
     ap.add_argument("--no-parity", action="store_true",
@@ -841,6 +843,95 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True):
     return rows
 
 
+def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, watchdog, min_steps=3, warmup=2,
+                     max_numel=None):
+    """N > 1: whole gossip rounds at every north_star size (configs[1..4] sizes and dtypes), one
+    learner per rank, on the transport the trials chose (`pull`: "<mode>" lock-step or
+    "async/<mode>[+wt]"), constant 0.5, fetch_probability 1 -- the GB/s and rounds/s table of
+    BASELINE's north_star at 2/4/8 GPUs.  A size that fails on any rank is reported with its
+    error and the sweep goes on.  max_numel: skip larger sizes (rehearsals with several ranks
+    on one GPU)."""
+    from dpwa_amd import DpwaConnection
+    names = ["w%d" % (r + 1) for r in range(world)]
+    cfg = os.path.join(cfg_dir, "dist_sweep.yaml")     # every rank its own copy (cfg_dir is per rank)
+    write_config(cfg, names, "constant")
+    sel_async = pull.startswith("async/")
+    mode = pull.split("/")[-1].replace("+wt", "")
+    # ranks sharing a device (rehearsals) split its free memory
+    share = max(1, -(-world // max(1, torch.cuda.device_count())))
+    rows = []
+    for numel, dt in SWEEP:
+        if max_numel is not None and numel > max_numel:
+            continue
+        watchdog.enter("dist round sweep %d %s" % (numel, dt), 900.0)
+        dtype = torch.float32 if dt == "f32" else torch.bfloat16
+        esize = 4 if dt == "f32" else 2
+        # parameters, two snapshot slots, staging (two under the board), relay buffer + margin:
+        # checked on every rank before anything is allocated, so no rank fails alone inside the
+        # binding collectives
+        need = 6 * numel * esize + (2 << 30)
+        free = torch.cuda.mem_get_info(device)[0]
+        if not _agree(free >= need * share, world, ctl):
+            rows.append({"numel": numel, "dtype": dt, "transport": pull,
+                         "error": "device memory: %.1f GB needed per rank, %.1f GB free on rank %d for %d rank(s)"
+                                  % (need / 1e9, free / 1e9, rank, share)})
+            progress("dist sweep %d %s skipped: %s" % (numel, dt, rows[-1]["error"]))
+            continue
+        conn, flat, err, el, averaged, steps = None, None, None, None, 0, 0
+        try:
+            flat = torch.empty(numel, dtype=dtype, device=device)
+            flat.normal_(generator=torch.Generator(device=device).manual_seed(rank))
+            conn = DpwaConnection(names[rank], cfg, seed=1000 + rank, group="async" if sel_async else "lockstep",
+                                  pull=mode)
+
+            def step():
+                conn.update_send(flat, 1.0, reuse_snapshot=write_through)
+                return conn.update_wait_average(flat, 1.0, write_through=write_through)[0] is not None
+
+            for _ in range(warmup):
+                step()
+            torch.cuda.synchronize()
+            dist.barrier(group=ctl)
+            t0 = time.perf_counter()      # one more round sizes the timed run: >= ~0.25 s, 3..50 rounds
+            step()
+            torch.cuda.synchronize()
+            got = [None] * world
+            dist.all_gather_object(got, time.perf_counter() - t0, group=ctl)
+            steps = int(min(50, max(min_steps, np.ceil(0.25 / max(got)))))
+            dist.barrier(group=ctl)
+            t0 = time.perf_counter()
+            averaged = sum(step() for _ in range(steps))
+            torch.cuda.synchronize()
+            dist.barrier(group=ctl)
+            el = time.perf_counter() - t0
+        except Exception as e:   # noqa: BLE001 -- the size is reported failed, the sweep goes on
+            err = "%s: %s" % (type(e).__name__, e)
+            progress("dist sweep %d %s FAILED: %s" % (numel, dt, err))
+        ok = _agree(err is None, world, ctl)
+        got = [None] * world
+        dist.all_gather_object(got, (el, averaged), group=ctl)
+        if ok:
+            el_max = max(g[0] for g in got)
+            av = sum(g[1] for g in got)
+            rows.append({"numel": numel, "dtype": dt, "value": round(av * 3 * numel * esize / el_max / 1e9, 1),
+                         "ms_per_step": round(1e3 * el_max / steps, 3),
+                         "gossip_rounds_per_s": round(world * steps / el_max, 1), "averagings": int(av),
+                         "steps": steps, "transport": pull, "publish": "write-through" if write_through else "full"})
+            progress("dist sweep %d %s: %.1f GB/s" % (numel, dt, rows[-1]["value"]))
+        else:
+            rows.append({"numel": numel, "dtype": dt, "error": err or "failed on another rank", "transport": pull})
+        if conn is not None:
+            try:
+                conn.close()
+            except Exception as e:   # noqa: BLE001
+                progress("dist sweep close: %s" % e)
+        del conn, flat
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        dist.barrier(group=ctl)
+    return rows
+
+
 def size_sweep(device):
     """The averaging kernel, cold, per launch, at every north_star size (11.17M/100M fp32,
     1B/7B bf16), in both publish forms: plain (3*N*s bytes per launch) and write-through
@@ -1324,6 +1415,16 @@ def main(argv=None):
         size_rows = size_sweep(device)
         wd.enter("round sweep", 900.0)
         round_rows = round_sweep(device, tmp, batch=batched)
+    elif world > 1 and not args.no_sweep:
+        # the timed learners' buffers go first: the sweep's 7B learner needs ~80 GB per GPU
+        for conn, _ in lockstep_learners + async_learners:
+            conn.close()
+        lockstep_learners, async_learners = [], []
+        learners[:] = []
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        round_rows = dist_round_sweep(world, rank, device, tmp, pull, wt_main, ctl, wd,
+                                      max_numel=args.dist_sweep_max_numel)
     wd.enter("report", 120.0)
     if rank == 0:
         value = averaged * unit_bytes / elapsed / 1e9
@@ -1365,7 +1466,7 @@ def main(argv=None):
                                 args.fetch_probability, args.divergence_threshold, args.loss_schedule,
                                 "free-running" if sel_async else "lock-step", variant)),
                 "learners": int(rounds / args.steps),
-                "learners_per_gpu": len(learners),
+                "learners_per_gpu": len(mine),
                 "numel": args.numel,
                 "publish": variant,
                 "averaging_dispatch": ("one batched dispatch per round for the %d co-resident learners" % per_launch

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 t0=$(date +%s)
 timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
-    --master-port 29611 bench.py --gpus $N --steps 10 --warmup 3 --dist-backend gloo --numel 1000000000 --dtype bf16 \
+    --master-port 29611 bench.py --gpus $N --steps 10 --warmup 3 --dist-backend gloo --dist-sweep-max-numel 100000000 --numel 1000000000 --dtype bf16 \
     --interpolation loss --divergence-threshold 0.5 --loss-schedule decay --no-cpu-baseline --no-sweep --no-cold \
     --compute-us 0 --no-secondary --trial-passes 1 --phase-scale 3 \
     > gpurun_out/r1b_${TAG}_n$N.json 2> gpurun_out/r1b_${TAG}_n$N.err

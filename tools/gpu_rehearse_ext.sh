@@ -10,6 +10,7 @@ for N in 8 2; do
   t0=$(date +%s)
   timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
       --master-port $((29500 + N)) bench.py --gpus $N --steps 20 --warmup 5 --dist-backend gloo \
+      --dist-sweep-max-numel 100000000 \
       > gpurun_out/ext_${TAG}_n$N.json 2> gpurun_out/ext_${TAG}_n$N.err
   rc=$?
   echo "N=$N rc=$rc $(( $(date +%s) - t0 ))s stdout lines: $(wc -l < gpurun_out/ext_${TAG}_n$N.json)"

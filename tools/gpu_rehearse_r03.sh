@@ -12,7 +12,7 @@ TAG=${1:-r03}
 N=${2:-4}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-B="--gpus $N --dist-backend gloo --steps 20 --warmup 5 --no-cpu-baseline --compute-us 0"
+B="--gpus $N --dist-backend gloo --dist-sweep-max-numel 100000000 --steps 20 --warmup 5 --no-cpu-baseline --compute-us 0"
 t0=$(date +%s)
 timeout -k 10 500 python -u bench.py $B > gpurun_out/rh_${TAG}_clean.json 2> gpurun_out/rh_${TAG}_clean.err
 echo "clean rc=$? $(( $(date +%s) - t0 ))s, stdout lines: $(wc -l < gpurun_out/rh_${TAG}_clean.json)"
