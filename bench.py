@@ -234,6 +234,7 @@ class Watchdog:
         self.phase, self.deadline = "start", None
         self.parity = {}
         self.transport = None
+        self.held, self.held_rc = None, None   # hold(): the finished line and the run's exit status
         self._lock = threading.Lock()
         t = threading.Thread(target=self._run, name="bench-watchdog", daemon=True)
         t.start()
@@ -244,6 +245,12 @@ class Watchdog:
             self.transport = transport
             self.deadline = time.monotonic() + seconds * self.args.phase_scale
         progress(phase)
+
+    def hold(self, result, rc):
+        """From here on an overrun prints `result` (rank 0's finished line; None on other ranks)
+        with the phase and the error added, and exits with `rc`; hold(None, None) undoes it."""
+        with self._lock:
+            self.held, self.held_rc = result, rc
 
     def idle(self):
         with self._lock:
@@ -256,9 +263,19 @@ class Watchdog:
             with self._lock:
                 late = self.deadline is not None and time.monotonic() > self.deadline
                 phase, transport = self.phase, self.transport
+                held, held_rc = self.held, self.held_rc
             if not late:
                 continue
             progress("WATCHDOG: phase '%s' overran its budget; exiting" % phase)
+            if held_rc is not None:      # the measurement is complete: the line as it stands
+                if held is not None:
+                    out = dict(held)
+                    out["error"] = "watchdog: phase '%s' overran its budget (the line up to it)" % phase
+                    out["phase"] = phase
+                    emit(json.dumps(out))
+                faulthandler.dump_traceback(all_threads=True)
+                sys.stderr.flush()
+                os._exit(held_rc)
             if self.rank == 0:
                 out = base_line(self.args, self.world)
                 out["error"] = "watchdog: phase '%s' overran its budget" % phase
@@ -794,14 +811,14 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
             "rotating_buffer_sets": sets, "learners_per_launch": learners, "batch_bracket_us": float(batch_us)}
 
 
-def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True):
+def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None):
     """Whole gossip rounds (two co-resident learners, write-through publish, constant 0.5,
     fetch_probability 1, both averages in one dispatch) at every north_star size in its
     config's dtype: the averaged GB/s and rounds/s the north star asks for at 11M/100M/1B/7B
     on one GPU."""
     from dpwa_amd import DpwaConnection
     from dpwa_amd.group import LocalGroup
-    rows = []
+    rows = [] if rows is None else rows
     cfg = os.path.join(cfg_dir, "sweep.yaml")
     write_config(cfg, ["w1", "w2"], "constant")
     for numel, dt in SWEEP:
@@ -844,7 +861,7 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True):
 
 
 def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, watchdog, min_steps=3, warmup=2,
-                     max_numel=None):
+                     max_numel=None, rows=None):
     """N > 1: whole gossip rounds at every north_star size (configs[1..4] sizes and dtypes), one
     learner per rank, on the transport the trials chose (`pull`: "<mode>" lock-step or
     "async/<mode>[+wt]"), constant 0.5, fetch_probability 1 -- the GB/s and rounds/s table of
@@ -859,7 +876,7 @@ def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, wat
     mode = pull.split("/")[-1].replace("+wt", "")
     # ranks sharing a device (rehearsals) split its free memory
     share = max(1, -(-world // max(1, torch.cuda.device_count())))
-    rows = []
+    rows = [] if rows is None else rows
     for numel, dt in SWEEP:
         if max_numel is not None and numel > max_numel:
             continue
@@ -932,12 +949,12 @@ def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, wat
     return rows
 
 
-def size_sweep(device):
+def size_sweep(device, rows=None):
     """The averaging kernel, cold, per launch, at every north_star size (11.17M/100M fp32,
     1B/7B bf16), in both publish forms: plain (3*N*s bytes per launch) and write-through
     (4*N*s: the next snapshot is written by the same pass); and at 11.17M / 100M the batched
     dispatch of two learners' write-through averages (the N=1 loop's kernel, 2 x 4*N*s)."""
-    rows = []
+    rows = [] if rows is None else rows
     for numel, dt in SWEEP:
         esize = 4 if dt == "f32" else 2
         forms = [(False, 1), (True, 1)] + ([(True, 2)] if numel <= 100_000_000 else [])
@@ -1409,23 +1426,8 @@ def main(argv=None):
     if not args.no_cold:
         wd.enter("cold kernel", 300.0)
         cold = cold_kernel(args.numel, dtype, device, wt_main, learners=per_launch)
-    size_rows, round_rows = None, None
-    if world == 1 and not args.no_sweep:
-        wd.enter("size sweep", 900.0)
-        size_rows = size_sweep(device)
-        wd.enter("round sweep", 900.0)
-        round_rows = round_sweep(device, tmp, batch=batched)
-    elif world > 1 and not args.no_sweep:
-        # the timed learners' buffers go first: the sweep's 7B learner needs ~80 GB per GPU
-        for conn, _ in lockstep_learners + async_learners:
-            conn.close()
-        lockstep_learners, async_learners = [], []
-        learners[:] = []
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-        round_rows = dist_round_sweep(world, rank, device, tmp, pull, wt_main, ctl, wd,
-                                      max_numel=args.dist_sweep_max_numel)
     wd.enter("report", 120.0)
+    out = None
     if rank == 0:
         value = averaged * unit_bytes / elapsed / 1e9
         lerp_us = float(np.nanmean(lerp_ms) * 1e3)
@@ -1584,15 +1586,39 @@ def main(argv=None):
             }
         if overlap is not None:
             out["overlap"] = overlap
-        if size_rows is not None:
-            out["roofline"]["size_sweep"] = size_rows
-        if round_rows is not None:
-            out["round_sweep"] = round_rows
         out["cpu_baseline"] = cpu
         if parity is not None:
             out["parity"] = parity
             out["parity_of_timed_transport"] = {"transport": used, "ok": bool(parity.get(used, False))}
+    # The sweeps over the north_star sizes come last: their rows go into the line as they are
+    # measured, and a watchdog overrun in them prints the line built above (with the rows so
+    # far and the error) and exits as the run would have (1 only for a failed parity check).
+    parity_failed = parity is not None and any(not v for k, v in parity.items() if k != "workload")
+    size_rows, round_rows = [], []
+    if out is not None and not args.no_sweep:
+        if world == 1:
+            out["roofline"]["size_sweep"] = size_rows
+        out["round_sweep"] = round_rows
+    wd.hold(out, 1 if parity_failed else 0)
+    if world == 1 and not args.no_sweep:
+        wd.enter("size sweep", 900.0)
+        size_sweep(device, rows=size_rows)
+        wd.enter("round sweep", 900.0)
+        round_sweep(device, tmp, batch=batched, rows=round_rows)
+    elif world > 1 and not args.no_sweep:
+        # the timed learners' buffers go first: the sweep's 7B learner needs ~80 GB per GPU
+        for conn, _ in lockstep_learners + async_learners:
+            conn.close()
+        lockstep_learners, async_learners = [], []
+        learners[:] = []
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        dist_round_sweep(world, rank, device, tmp, pull, wt_main, ctl, wd, max_numel=args.dist_sweep_max_numel,
+                         rows=round_rows)
+    wd.enter("result", 60.0)
+    if out is not None:
         emit(json.dumps(out))
+    wd.hold(None, 1 if parity_failed else 0)      # the line is out: an overrun now only exits
     wd.enter("shutdown", 300.0)
     for conn, _ in lockstep_learners + async_learners:
         conn.close()

@@ -62,3 +62,33 @@ def test_partial_line_keeps_the_contract_keys():
               "vs_baseline", "dtype", "data"):
         assert k in out
     assert out["n_gpus"] == 8 and out["steps"] == 20 and out["value"] is None
+
+
+def _watchdog_child(held, rc):
+    """A process whose watchdog overruns a 0.05 s phase after hold(held, rc)."""
+    import subprocess
+    code = ("import sys, time, json; sys.path.insert(0, %r); import bench\n"
+            "wd = bench.Watchdog(bench.parse(['--gpus', '1']), 1, 0)\n"
+            "wd.hold(%s, %s)\n"
+            "wd.enter('dist round sweep 7000000000 bf16', 0.05)\n"
+            "time.sleep(30)\n" % (ROOT, held, rc))
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+
+
+def test_overrun_after_the_measurement_prints_the_finished_line():
+    """An overrun in the sweeps (after the timed measurement) prints the line built so far with
+    the error added and exits with the run's own status (0, or 1 for a failed parity check)."""
+    import json
+    p = _watchdog_child("{'value': 5200.0, 'round_sweep': [{'numel': 11173962, 'value': 5100.0}]}", 0)
+    assert p.returncode == 0, p.stderr
+    lines = [x for x in p.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] == 5200.0 and d["round_sweep"][0]["value"] == 5100.0
+    assert "overran" in d["error"] and d["phase"].startswith("dist round sweep")
+    p = _watchdog_child("None", 1)           # a rank other than 0 (no line), parity failed
+    assert p.returncode == 1 and not p.stdout.strip()
+    p = _watchdog_child("None", "None")      # before the measurement: the partial line, status 3
+    assert p.returncode == 3
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["value"] is None and "overran" in d["error"]
