@@ -32,6 +32,7 @@ from .dpwa import DeviceFactor, DpwaConnection, PeerSnapshot
 LOGGER = logging.getLogger(__name__)
 
 TCP_SOCKET_BUFFER_SIZE = 8 * 1024 * 1024      # conn.py:40
+_PICKLE_FRAME_TARGET = 64 * 1024              # pickle writes bytes objects this large outside its frames
 
 
 def _tune(sock):
@@ -47,6 +48,7 @@ class SnapshotCodec:
 
     def __init__(self, names, offsets, numels, total):
         self.names, self.offsets, self.numels, self.total = list(names), list(offsets), list(numels), int(total)
+        self._placeholders = {}
 
     @classmethod
     def from_flat(cls, flat):
@@ -65,6 +67,39 @@ class SnapshotCodec:
             params[name] = a[off:off + n].tobytes()
         import pickle
         return pickle.dumps(params)
+
+    def to_parts(self, payload):
+        """payload: a buffer holding the flat fp32 buffer (page-locked host memory, say) -> the
+        parts of to_blob's bytes, every parameter of 64 KiB or more as a view of `payload` (no
+        copy).  The pickler is run over same-length placeholders (bytes(n) is lazily zeroed
+        memory, never touched), which it hands on by identity; each is then swapped for its view."""
+        mv = memoryview(payload).cast("B")
+        params, swap = {}, {}
+        for i, (name, off, n) in enumerate(zip(self.names, self.offsets, self.numels)):
+            seg = mv[off * 4:(off + n) * 4]
+            if n * 4 >= _PICKLE_FRAME_TARGET:
+                ph = self._placeholders.get((i, n))
+                if ph is None:
+                    ph = self._placeholders[(i, n)] = bytes(n * 4)
+                params[name] = ph
+                swap[id(ph)] = seg
+            else:
+                params[name] = bytes(seg)
+        return [swap.get(id(p), p) for p in wire.dumps_parts(params)]
+
+    def is_identity(self):
+        """One parameter covering the whole flat buffer: a received blob is the flat layout."""
+        return len(self.names) == 1 and self.offsets[0] == 0 and self.numels[0] == self.total
+
+    def assemble(self, views, out):
+        """{name: buffer} (param_views / safe_loads of a reference blob) -> the flat layout in
+        `out` (a float32 array of `total` elements whose gaps stay as they are).  KeyError for a
+        missing parameter, like the adapter's other_params[name] (pytorch.py:67)."""
+        for name, off, n in zip(self.names, self.offsets, self.numels):
+            a = np.frombuffer(views[name], dtype=np.float32)
+            if a.size != n:
+                raise ValueError("parameter %r has %d elements in the peer's blob, %d here" % (name, a.size, n))
+            out[off:off + n] = a
 
     def from_blob(self, blob):
         """Reference blob -> bytes of the flat layout (gaps zero).  KeyError for a missing
@@ -86,7 +121,9 @@ def header_bytes(clock, loss, n, version=1):
 
 
 class WireServer:
-    """RxThread (conn.py:51-172) for a GPU learner; ``snapshot_fn() -> (state, blob) | None``."""
+    """RxThread (conn.py:51-172) for a GPU learner; ``snapshot_fn() -> (state, blob) | None``, or
+    ``(state, parts, release)``: the payload as a list of buffers, and a callable run once they
+    have been sent."""
 
     def __init__(self, host, port, snapshot_fn, timeout_ms):
         self.snapshot_fn = snapshot_fn
@@ -121,6 +158,11 @@ class WireServer:
                 snap = self.snapshot_fn()
                 if snap is None:
                     wire.send_frame(client, wire.MESSAGE_TYPE_FETCH_PARAMETERS)           # conn.py:106-107
+                elif len(snap) == 3:      # (state, payload parts, release): views of a pinned buffer
+                    try:
+                        wire.send_frame_parts(client, wire.MESSAGE_TYPE_FETCH_PARAMETERS, snap[0], snap[1])
+                    finally:
+                        snap[2]()
                 else:
                     wire.send_frame(client, wire.MESSAGE_TYPE_FETCH_PARAMETERS, snap[0], snap[1])
         except (wire.MessageError, OSError) as e:
@@ -145,11 +187,12 @@ class _Peer:
         self.sock = None
 
 
-def fetch_loop(sched, peers, timeout_ms, max_attempts=100000):
+def fetch_loop(sched, peers, timeout_ms, max_attempts=100000, alloc=None):
     """TxThread.run for one queue item (conn.py:277-315) over real sockets.
 
     `sched` is the native scheduler (dpwa_amd.sched.Scheduler); `peers` are _Peer objects in
-    scheduler order.  Returns (k, state, payload) or None."""
+    scheduler order.  Returns (k, state, payload) or None.  alloc(n): where a reply's payload
+    is received (wire.recv_frame_into; the payload is then a view of it), else a bytes object."""
     timeout = timeout_ms / 1000.0
     for _ in range(max_attempts):
         k, connected = sched.pick()                      # conn.py:227-240
@@ -171,7 +214,7 @@ def fetch_loop(sched, peers, timeout_ms, max_attempts=100000):
             sched.report(k, "connect_ok")
         try:                                             # conn.py:294-313
             wire.send_frame(p.sock, wire.MESSAGE_TYPE_FETCH_PARAMETERS)
-            _, state, payload = wire.recv_frame(p.sock)
+            _, state, payload = wire.recv_frame_into(p.sock, alloc) if alloc else wire.recv_frame(p.sock)
         except socket.timeout:
             sched.report(k, "timeout")
             p.sock.close()
@@ -221,32 +264,61 @@ class WireConnection(DpwaConnection):
         self._thread = None
         self._result = None
         self._averaged_once = False
-        self._blob_cache = (None, None)
+        # served snapshots: page-locked host copies, each with the frame parts viewing it and
+        # the number of replies still sending it (a new version takes a copy nobody is sending)
+        self._snap_lock = threading.Lock()
+        self._snaps = []
+        self._snap_cur = None
+        # received replies land in page-locked memory the host-to-device copy reads directly
+        self._rx = None
+        self._flat_host = None
         self._server = WireServer(self.me.host, self.me.port, self._snapshot, self.timeout_ms) if serve else None
 
     # -- serving (RxThread) ---------------------------------------------------------
     def _snapshot(self):
+        """(state, parts, release) of the newest published snapshot, or None before the first
+        publish (conn.py:106-110).  The device copy goes straight to page-locked memory and the
+        reply's parameter bytes are views of it (SnapshotCodec.to_parts)."""
         learner = self._learner
         if learner is None:
             return None
-        hdr = ctypes.create_string_buffer(256)
-        payload = bytearray(learner.numel * 4)
-        buf = (ctypes.c_char * len(payload)).from_buffer(payload)
-        v = ctypes.c_uint64()
-        _lib.call("dpwa_learner_read_snapshot", learner.handle, hdr, buf, len(payload), ctypes.byref(v))
-        if v.value == 0:
-            return None
-        clock, loss = struct.unpack_from("<dd", hdr.raw)
-        if not self._averaged_once and float(clock).is_integer():
-            clock = int(clock)       # the reference's clock is an int until the first averaging
-        if self._blob_cache[0] != v.value:
-            self._blob_cache = (v.value, self.codec.to_blob(bytes(payload)))
-        return {"clock": clock, "loss": loss}, self._blob_cache[1]
+        with self._snap_lock:
+            cur = self._snap_cur
+            if cur is not None and cur["version"] == learner.native_version():
+                cur["users"] += 1
+                return cur["state"], cur["parts"], lambda e=cur: self._release(e)
+            ent = next((e for e in self._snaps if e["users"] == 0 and e is not cur), None)
+            if ent is None:
+                buf = torch.empty(learner.numel * 4, dtype=torch.uint8, pin_memory=True)
+                ent = {"buf": buf, "users": 0, "version": 0}
+                self._snaps.append(ent)
+            hdr = ctypes.create_string_buffer(256)
+            v = ctypes.c_uint64()
+            _lib.call("dpwa_learner_read_snapshot", learner.handle, hdr, ctypes.c_void_p(ent["buf"].data_ptr()),
+                      learner.numel * 4, ctypes.byref(v))
+            if v.value == 0:
+                return None
+            clock, loss = struct.unpack_from("<dd", hdr.raw)
+            if not self._averaged_once and float(clock).is_integer():
+                clock = int(clock)       # the reference's clock is an int until the first averaging
+            ent.update(version=v.value, state={"clock": clock, "loss": loss},
+                       parts=self.codec.to_parts(ent["buf"].numpy()), users=1)
+            self._snap_cur = ent
+            return ent["state"], ent["parts"], lambda e=ent: self._release(e)
+
+    def _release(self, ent):
+        with self._snap_lock:
+            ent["users"] -= 1
+
+    def _rx_alloc(self, n):
+        if self._rx is None or self._rx.numel() < n:
+            self._rx = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        return self._rx.numpy()
 
     # -- fetching (TxThread) --------------------------------------------------------
     def _fetch(self):
         try:
-            self._result = fetch_loop(self._sched, self._wire_peers, self.timeout_ms)
+            self._result = fetch_loop(self._sched, self._wire_peers, self.timeout_ms, alloc=self._rx_alloc)
         except Exception as e:      # noqa: BLE001
             LOGGER.exception("wire fetch failed")
             self._result = e
@@ -282,10 +354,24 @@ class WireConnection(DpwaConnection):
         if res is None:
             return None
         k, state, payload = res
-        flat = self.codec.from_blob(payload)
+        views = wire.param_views(payload)        # views of the received bytes, no copy
+        if views is None:
+            views = wire.safe_loads(bytes(payload))   # any other pickle: plain data or an error
+        if self.codec.is_identity():             # the blob's one parameter is the flat layout
+            src = np.frombuffer(views[self.codec.names[0]], dtype=np.float32)
+            if src.size != self.codec.total:
+                raise ValueError("parameter %r has %d elements in the peer's blob, %d here"
+                                 % (self.codec.names[0], src.size, self.codec.total))
+        else:
+            if self._flat_host is None:          # gaps between parameters stay zero
+                self._flat_host = torch.zeros(self.codec.total, dtype=torch.float32, pin_memory=True).numpy()
+            src = self._flat_host
+            self.codec.assemble(views, src)
         hdr = header_bytes(state["clock"], state["loss"], self.codec.total)
         learner = self._learner
-        _lib.call("dpwa_learner_fetch_host", learner.handle, hdr, flat, len(flat),
+        # returns once the bytes are on the device side (a page-locked source is waited for),
+        # so the receive buffer is free for the next reply
+        _lib.call("dpwa_learner_fetch_host", learner.handle, hdr, ctypes.c_void_p(src.ctypes.data), src.nbytes,
                   _lib.stream_handle(torch.cuda.current_stream(learner.device)))
         return k
 

@@ -1286,19 +1286,23 @@ int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *pay
         return set_error(DPWA_ERR_ARG, "dpwa_learner_fetch_host: need a header and %zu payload bytes",
                          l ? l->payload_bytes : (size_t)0);
     DeviceGuard dg(l->device);
-    hipStream_t s = (hipStream_t)stream;
-    HIP_TRY(hipEventRecord(l->ev_issue, s));
-    HIP_TRY(hipStreamWaitEvent(l->side, l->ev_issue, 0));
-    if (l->consumed_once && l->consume_stream != s) {
-        HIP_TRY(hipEventRecord(l->ev_consumed, l->consume_stream));
-        HIP_TRY(hipStreamWaitEvent(l->side, l->ev_consumed, 0));
-    }
+    (void)stream;
+    // The copy waits only for the last reader of the staging buffer (every consumer of a fetch
+    // records ev_stage_done), not for all the work queued on the caller's stream: it starts
+    // at once, beside a training step already enqueued.
     if (l->stage_read[0]) HIP_TRY(hipStreamWaitEvent(l->side, l->ev_stage_done[0], 0));
-    // pageable host sources: the calls return once the host bytes have been taken
+    // Pageable host sources: the calls return once the host bytes have been taken.  A
+    // page-locked source is copied asynchronously, so the copy is waited for: either way the
+    // caller may reuse its buffer when this returns.
+    hipPointerAttribute_t attr{};
+    const bool pinned = payload_bytes > 0 && hipPointerGetAttributes(&attr, payload) == hipSuccess &&
+                        attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();   // a pageable pointer is "invalid" to hipPointerGetAttributes
     HIP_TRY(hipMemcpyAsync(l->staging, header, kHeader, hipMemcpyHostToDevice, l->side));
     if (payload_bytes)
         HIP_TRY(hipMemcpyAsync(l->staging + kPayloadOff, payload, (size_t)payload_bytes, hipMemcpyHostToDevice, l->side));
     HIP_TRY(hipEventRecord(l->ev_fetched, l->side));
+    if (pinned) HIP_TRY(hipEventSynchronize(l->ev_fetched));
     l->src = l->staging;
     l->src_copied = true;
     l->src_stage = 0;

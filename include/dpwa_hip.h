@@ -252,7 +252,9 @@ int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream);
  * snapshot to host memory (header 256 B + up to payload_bytes), from any host thread --
  * RxThread's reply (conn.py:108-110); *version_out = 0 when nothing was published.
  * fetch_host: stage a snapshot received in host memory (a reference node's reply,
- * conn.py:298) as the fetch to average with; payload_bytes must equal n*sizeof(dtype). */
+ * conn.py:298) as the fetch to average with; payload_bytes must equal n*sizeof(dtype).  The
+ * copy waits only for the last reader of the staging buffer (not for `stream`'s queued work);
+ * the host buffer may be reused on return (a page-locked one is DMA'd, and waited for). */
 int dpwa_learner_read_snapshot(dpwa_learner *l, void *header_out, void *payload_out, int64_t payload_bytes,
                                uint64_t *version_out);
 int dpwa_learner_fetch_host(dpwa_learner *l, const void *header, const void *payload, int64_t payload_bytes,

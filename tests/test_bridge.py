@@ -26,6 +26,32 @@ def test_codec_matches_reference_blob():
     assert codec.from_blob(bytes.fromhex(fx["blob_hex"])) == flat
 
 
+def test_codec_parts_and_views_match_the_reference_blob():
+    """The zero-copy forms: to_parts concatenates to the reference's blob (also with parameters
+    above pickle's 64 KiB frame target, served as views), and param_views + assemble restore the
+    flat layout from it."""
+    from dpwa_amd import wire
+    fx, codec = fixture_codec()
+    flat = bytes.fromhex(fx["flat_f32_hex"])
+    assert b"".join(bytes(p) for p in codec.to_parts(bytearray(flat))).hex() == fx["blob_hex"]
+    out = np.zeros(codec.total, np.float32)
+    codec.assemble(wire.param_views(bytes.fromhex(fx["blob_hex"])), out)
+    assert out.tobytes() == flat
+    rng = np.random.default_rng(2)
+    numels = [5, 40_000, 3, 70_001]                    # two of them served as views
+    offsets = [0, 64, 40_064, 40_128]                  # with gaps, as the flat buffer aligns
+    big = SnapshotCodec(["a", "b", "c", "d"], offsets, numels, 110_144)
+    buf = rng.standard_normal(big.total).astype(np.float32)
+    parts = big.to_parts(buf)
+    assert sum(isinstance(p, memoryview) for p in parts) == 2
+    blob = b"".join(bytes(p) for p in parts)
+    assert blob == big.to_blob(buf.tobytes())
+    back = np.zeros(big.total, np.float32)
+    big.assemble(wire.param_views(blob), back)
+    for off, n in zip(offsets, numels):
+        assert np.array_equal(back[off:off + n], buf[off:off + n])
+
+
 def recv_all(sock, n):
     out = b""
     while len(out) < n:

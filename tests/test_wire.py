@@ -73,3 +73,45 @@ def test_oversize_payload_is_refused():
 
     with pytest.raises(wire.MessageError):
         wire.encode(1, None, Huge())
+
+
+def test_dumps_parts_is_pickle_dumps_with_large_bytes_by_identity():
+    """Zero-copy serving: the parts concatenate to pickle.dumps' bytes, and every bytes object of
+    64 KiB or more is handed over as itself (so a view of page-locked memory can stand in)."""
+    rng = __import__("numpy").random.default_rng(0)
+    for sizes in ([10], [100_000], [3, 70_000, 5, 200_000], [0, 1, 65_535, 65_536, 65_537]):
+        d = {"p%d" % i: rng.integers(0, 255, s, dtype="uint8").tobytes() for i, s in enumerate(sizes)}
+        parts = wire.dumps_parts(d)
+        assert b"".join(bytes(p) for p in parts) == pickle.dumps(d)
+        big = {id(v) for v in d.values() if len(v) >= 65_536}
+        assert {id(p) for p in parts if id(p) in big} == big
+
+
+def test_param_views_reads_every_protocol_without_copies_and_refuses_the_rest():
+    rng = __import__("numpy").random.default_rng(1)
+    d = {"w%d" % i: rng.integers(0, 255, s, dtype="uint8").tobytes() for i, s in enumerate([0, 7, 300, 70_000])}
+    for proto in (3, 4, 5):
+        blob = bytearray(pickle.dumps(d, protocol=proto))
+        v = wire.param_views(blob)
+        assert {k: bytes(x) for k, x in v.items()} == d
+        assert all(x.obj is not None for x in v.values())        # views of `blob`, not copies
+        blob[-1] = 0                                              # no STOP: not accepted
+        assert wire.param_views(blob) is None
+    for other in ({"a": 1}, [b"x"], {1: b"x"}, {"a": {"b": b"x"}}, "s"):
+        assert wire.param_views(pickle.dumps(other)) is None
+
+
+def test_parts_and_receive_into_a_caller_buffer():
+    a, b = socket.socketpair()
+    big = bytes(range(256)) * 50_000
+    parts = [b"head", memoryview(big)[100:], b"tail"]
+    state = {"clock": 3, "loss": 0.5}
+    th = threading.Thread(target=wire.send_frame_parts, args=(a, 1, state, parts))
+    th.start()
+    buf = bytearray(len(big) + 64)
+    t, m, p = wire.recv_frame_into(b, lambda n: buf)
+    th.join()
+    assert t == 1 and m == state and bytes(p) == b"head" + big[100:] + b"tail"
+    assert p.obj is buf
+    a.close()
+    b.close()
