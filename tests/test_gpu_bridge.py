@@ -2,6 +2,7 @@
 reference's frame format and averages with snapshots that arrive over TCP."""
 import socket
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -146,3 +147,50 @@ def test_two_gpu_learners_gossip_over_tcp(tmp_path):
         assert olerp.bits_equal(flats[g].cpu().numpy(), exp["params"][-1, g]), g
         assert conns[g].clock == exp["clocks"][-1, g]
         conns[g].close()
+
+
+def test_served_snapshots_are_never_torn_while_publishing(tmp_path):
+    """Replies are sent from page-locked copies shared by concurrent readers: while the learner
+    keeps publishing, every reply three clients receive is one whole published snapshot (each
+    publish is a constant vector), never a mix of two."""
+    n, V = 300_000, 25                       # 1.2 MB per snapshot: served as views of the copy
+    ports = [free_port(), free_port()]
+    cfg = tmp_path / "torn.yaml"
+    wire_cfg(cfg, ["s", "absent"], ports, fp=0.0)
+    conn = WireConnection("s", str(cfg), codec=SnapshotCodec.single("w", n), seed=1)
+    flat = torch.zeros(n, device=DEV)
+    flat.fill_(1.0)
+    conn.update_send(flat, 1.0)
+    torch.cuda.synchronize()
+    stop = threading.Event()
+    seen, errors = [], []
+
+    def client():
+        try:
+            c = socket.create_connection(("127.0.0.1", ports[0]))
+            while not stop.is_set():
+                wire.send_frame(c, wire.MESSAGE_TYPE_FETCH_PARAMETERS)
+                _, state, payload = wire.recv_frame(c)
+                a = np.frombuffer(wire.param_views(payload)["w"], dtype=np.float32)
+                seen.append((float(state["loss"]), float(a[0]), bool((a == a[0]).all())))
+            c.close()
+        except Exception as e:      # noqa: BLE001 -- reported below
+            errors.append(e)
+
+    ths = [threading.Thread(target=client) for _ in range(3)]
+    for t in ths:
+        t.start()
+    for v in range(2, V + 1):
+        flat.fill_(float(v))
+        conn.update_send(flat, float(v))    # loss == value: a reply's state names its payload
+        torch.cuda.synchronize()
+        time.sleep(0.02)
+    stop.set()
+    for t in ths:
+        t.join(60)
+    conn.close()
+    assert not errors, errors
+    assert len(seen) >= V
+    assert all(whole for _, _, whole in seen)
+    assert all(loss == val for loss, val, _ in seen)
+    assert len({val for _, val, _ in seen}) > 2           # the replies followed the publishes
