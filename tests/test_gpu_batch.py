@@ -247,7 +247,8 @@ def test_wire_write_through_serves_the_update_send_loss(tmp_path):
                                  reuse_snapshot=r > 0)
         torch.cuda.synchronize()
         for g in range(G):
-            state, _ = conns[g]._snapshot()
+            state, _, release = conns[g]._snapshot()
+            release()
             assert state["loss"] == send[r][g], (r, g, state)
         for g in range(G):
             flats[g].add_(torch.from_numpy(deltas[r, g]).to(DEV))
