@@ -11,7 +11,7 @@ run() {
   name=$1; shift
   timeout -k 10 600 python3 bench.py $B "$@" > gpurun_out/${TAG}_$name.json 2> gpurun_out/${TAG}_$name.err \
       || { echo "$name failed"; tail gpurun_out/${TAG}_$name.err; exit 1; }
-  python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_$name.json'));r=d['roofline'];print('$name','value',d['value'],'ms',d['ms_per_step'],'avg',d['averagings'],'cold',r['frac'],'inloop',r['in_loop']['frac'],'parity',d['parity_of_timed_transport'])"
+  python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_$name.json'));r=d['roofline'];print('$name','value',d['value'],'ms',d['ms_per_step'],'avg',d['averagings'],'cold',r['frac'],'plain',r.get('plain_average',{}).get('frac'),'inloop',r['in_loop']['frac'],'parity',d['parity_of_timed_transport'])"
 }
 run 100m_clock --numel 100000000 --interpolation clock
 run 1b_bf16_loss_decay --numel 1000000000 --dtype bf16 --interpolation loss --divergence-threshold 0.5 --loss-schedule decay
