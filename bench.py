@@ -101,11 +101,13 @@ def parse(argv=None):
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the sweeps over the north_star sizes (cold kernel, and whole rounds at N=1)")
-    ap.add_argument("--publish", choices=["write-through", "full"], default="write-through",
-                    help="how update_send publishes in the timed loop: write-through (the adapter's default: "
-                         "the averaging kernel also writes the next snapshot, the publish moves the header only) "
-                         "or full (a 2*N*s snapshot copy every round); at N>1 free-running trials try both")
-    ap.add_argument("--no-secondary", action="store_true", help="skip the run of the other publish form")
+    ap.add_argument("--publish", choices=["resident", "write-through", "full"], default="resident",
+                    help="how a round publishes and averages in the timed loop: resident (the parameters live in "
+                         "the learner's two snapshot slots: the publish moves nothing, the average reads the "
+                         "published slot and writes the other, 3*N*s), write-through (the averaging kernel also "
+                         "writes the next snapshot, 4*N*s, the publish moves the header only) or full (a 2*N*s "
+                         "snapshot copy every round, then the 3*N*s average)")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the run of the other publish form(s)")
     ap.add_argument("--no-write-through", action="store_true", help="same as --publish full --no-secondary")
     ap.add_argument("--no-batch", action="store_true",
                     help="N=1: one averaging dispatch per learner instead of one batched dispatch per round")
@@ -475,13 +477,15 @@ def parity_transports(world, gossip="auto"):
     path that configs[3]/[4] use above 1.5 GiB, through the lock-step fused relay (slots and
     relay buffers fd-imported) and the free-running board."""
     if world == 1:
-        return ["local"]
+        return ["local", "local+res"]
     t = []
     if gossip != "async":
         t += ["lockstep/copy", "lockstep/kernel:256", "lockstep/relay:32", "lockstep/relay-avg:32",
-              "lockstep/relay-avg:32+vmm"]
+              "lockstep/relay-avg:32+vmm", "lockstep/copy+res", "lockstep/kernel:256+res", "lockstep/relay:32+res",
+              "lockstep/relay-avg:32+res", "lockstep/relay-avg:32+res+vmm"]
     if gossip != "lockstep":
-        t += ["async/copy", "async/kernel:256", "async/copy+wt", "async/kernel:256+wt", "async/copy+vmm"]
+        t += ["async/copy", "async/kernel:256", "async/copy+wt", "async/kernel:256+wt", "async/copy+vmm",
+              "async/copy+res", "async/kernel:256+res", "async/copy+res+vmm"]
     return t
 
 
@@ -498,14 +502,17 @@ def parity_loss(g, r, wait):
     return 0.95 * x if wait else x
 
 
-def parity_lockstep(names, mine, cfg, group, pull, device, n=PARITY_N, T=PARITY_T, conns=None, batch=False):
+def parity_lockstep(names, mine, cfg, group, pull, device, n=PARITY_N, T=PARITY_T, conns=None, batch=False,
+                    resident=False):
     """T lock-step rounds (clock interpolation, fetch_probability PARITY_FP) of the learners
     `mine` = [(name, g)] through the drop-in API: the training step adds a seeded delta; two
     of three rounds average with the fused kernel and write-through snapshots (the adapter's
     default; with `batch`, all of this process's learners in one dispatch), every third through
-    the split update_wait + average.  Returns per learner g the per-round (sha1 of the
-    parameters, clock, peer averaged with).  `conns` (a list) receives the connections as they
-    are made, so a caller can close them after a failure."""
+    the split update_wait + average.  `resident`: the parameters live in the learners' slots
+    (make_resident), every round averages fused (batched with `batch`) and the training step
+    comes after update_wait, as a resident loop must run.  Returns per learner g the per-round
+    (sha1 of the parameters after the average, clock, peer averaged with).  `conns` (a list)
+    receives the connections as they are made, so a caller can close them after a failure."""
     import hashlib
     from dpwa_amd import DpwaConnection
     conns = [] if conns is None else conns
@@ -513,6 +520,8 @@ def parity_lockstep(names, mine, cfg, group, pull, device, n=PARITY_N, T=PARITY_
     for name, g in mine:
         conns.append(DpwaConnection(name, cfg, seed=900 + g, group=group, pull=pull))
         flats.append(torch.from_numpy(parity_init(g, n)).to(device))
+    if resident:
+        return conns, _parity_lockstep_resident(conns, flats, mine, device, n, T, batch)
     rec = {g: [] for _, g in mine}
     for r in range(T):
         wt_prev = r % 3 != 0        # the previous round averaged write-through (r % 3 == 2 is split)
@@ -540,7 +549,30 @@ def parity_lockstep(names, mine, cfg, group, pull, device, n=PARITY_N, T=PARITY_
     return conns, rec
 
 
-def parity_lockstep_expected(names, n=PARITY_N, T=PARITY_T):
+def _parity_lockstep_resident(conns, flats, mine, device, n, T, batch):
+    import hashlib
+    from dpwa_amd import DpwaConnection
+    for conn, flat in zip(conns, flats):
+        conn.make_resident(flat)
+    rec = {g: [] for _, g in mine}
+    for r in range(T):
+        for conn, (_, g) in zip(conns, mine):
+            conn.update_send(conn.parameters, parity_loss(g, r, False))
+        if batch:
+            res = DpwaConnection.update_wait_average_many(conns, [c.parameters for c in conns],
+                                                          [parity_loss(g, r, True) for _, g in mine])
+        else:
+            res = [conn.update_wait_average(conn.parameters, parity_loss(g, r, True)) for conn, (_, g) in zip(conns, mine)]
+        for conn, (_, g), (p, _) in zip(conns, mine, res):
+            rec[g].append((hashlib.sha1(conn.parameters.cpu().numpy().tobytes()).hexdigest(), conn.clock,
+                           p.peer if p is not None else ""))
+        for conn, (_, g) in zip(conns, mine):      # the training step, after update_wait
+            conn.parameters.add_(torch.from_numpy(parity_delta(g, r, n)).to(device))
+    torch.cuda.synchronize()
+    return rec
+
+
+def parity_lockstep_expected(names, n=PARITY_N, T=PARITY_T, resident=False):
     """The oracle's trajectory of parity_lockstep (oracle/gossip.py, pinned to the reference)."""
     import hashlib
     from oracle import gossip as ogossip
@@ -550,19 +582,22 @@ def parity_lockstep_expected(names, n=PARITY_N, T=PARITY_T):
     send = [[parity_loss(g, r, False) for g in range(G)] for r in range(T)]
     wait = [[parity_loss(g, r, True) for g in range(G)] for r in range(T)]
     exp = ogossip.simulate(names, init, deltas, send, wait, "clock", None, 0.0, PARITY_FP,
-                           [900 + g for g in range(G)])
+                           [900 + g for g in range(G)], train_after_wait=resident)
     return {g: [(hashlib.sha1(exp["params"][r, g].tobytes()).hexdigest(), float(exp["clocks"][r, g]),
                  (exp["picks"][r][g][-1] if exp["picks"][r][g] else ""))
                 for r in range(T)] for g in range(G)}
 
 
-def parity_async(names, rank, cfg, pull, device, n=PARITY_N, T=PARITY_ASYNC_T, write_through=False, conns=None):
+def parity_async(names, rank, cfg, pull, device, n=PARITY_N, T=PARITY_ASYNC_T, write_through=False, conns=None,
+                 resident=False):
     """Free-running rounds over the gossip board (AsyncDistGroup): each round publishes, runs
     an uneven synthetic step that sets the parameters to the checker's known values for
     (rank, round) and averages with whatever version the board hands out.  Without
     write-through the publish comes after that step (it publishes the known values); with it,
-    before (it publishes what the last average wrote through).  Returns (params, clocks,
-    peers, versions)."""
+    before (it publishes what the last average wrote through).  `resident`: the parameters live
+    in the learner's slots; the step sets them after the average (before the next publish, as
+    a resident loop must), so the publish carries the known values as without write-through.
+    Returns (params, clocks, peers, versions)."""
     from dpwa_amd import DpwaConnection
     from oracle.async_check import async_base, async_loss
     conn = DpwaConnection(names[rank], cfg, seed=700 + rank, group="async", pull=pull)
@@ -572,6 +607,19 @@ def parity_async(names, rank, cfg, pull, device, n=PARITY_N, T=PARITY_ASYNC_T, w
     flat = torch.from_numpy(async_base(rank, -1, n)).to(device)
     bases = [torch.from_numpy(async_base(rank, r, n)).to(device) for r in range(T)]
     params, clocks, peers, versions = np.zeros((T, n), np.float32), np.zeros(T), [], []
+    if resident:
+        conn.make_resident(flat)
+        for r in range(T):
+            conn.parameters.copy_(bases[r])
+            conn.update_send(conn.parameters, async_loss(rank, r))
+            torch.cuda._sleep(int(rng.integers(0, 200_000)))   # uneven "training steps" (nothing written)
+            payload, _ = conn.update_wait_average(conn.parameters, async_loss(rank, r, wait=True))
+            peers.append(payload.peer if payload is not None else "")
+            versions.append(conn._info()[2] if payload is not None else 0)
+            params[r] = conn.parameters.cpu().numpy()
+            clocks[r] = conn.clock
+        torch.cuda.synchronize()
+        return params, clocks, peers, versions
     for r in range(T):
         if not write_through:
             flat.copy_(bases[r])
@@ -589,14 +637,19 @@ def parity_async(names, rank, cfg, pull, device, n=PARITY_N, T=PARITY_ASYNC_T, w
 
 
 def parity_key(trial):
-    """The parity transport that vouches for a transport trial key ("<mode>" lock-step or
-    "async/<mode>[+wt]"): kernel pulls of any grid and relays of any block count share the
+    """The parity transport that vouches for a transport trial key ("<mode>[+res]" lock-step or
+    "async/<mode>[+wt|+res]"): kernel pulls of any grid and relays of any block count share the
     kernels of the parity run's kernel:256 / relay:32."""
     kind, _, mode = trial.rpartition("/")
-    wt = "+wt" if mode.endswith("+wt") else ""
-    base = mode.replace("+wt", "").partition(":")[0]
+    form = "+wt" if mode.endswith("+wt") else "+res" if mode.endswith("+res") else ""
+    base = trial_mode(mode).partition(":")[0]
     pull = {"copy": "copy", "kernel": "kernel:256", "relay": "relay:32", "relay-avg": "relay-avg:32"}[base]
-    return "%s/%s%s" % (kind or "lockstep", pull, wt)
+    return "%s/%s%s" % (kind or "lockstep", pull, form)
+
+
+def trial_mode(key):
+    """The pull mode of a trial key: "async/copy+wt" -> "copy", "relay-avg:32+res" -> "relay-avg:32"."""
+    return key.split("/")[-1].replace("+wt", "").replace("+res", "")
 
 
 class _Env:
@@ -631,7 +684,8 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
     if world > 1 and ctl is None:
         ctl = dist.new_group(backend="gloo")
     result = {}
-    expected = parity_lockstep_expected(names) if rank == 0 else None
+    expected = ({False: parity_lockstep_expected(names), True: parity_lockstep_expected(names, resident=True)}
+                if rank == 0 else None)
     for t in transports:
         if watchdog is not None:
             watchdog.enter("parity %s" % t, PARITY_PHASE_S, transport=t)
@@ -640,6 +694,8 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
         kind, _, pull = t.partition("/")
         vmm = pull.endswith("+vmm")
         pull = pull.replace("+vmm", "")
+        res = kind.endswith("+res") or pull.endswith("+res")
+        kind, pull = kind.replace("+res", ""), pull.replace("+res", "")
         conns, err, rec, check = [], None, None, None
         try:
             with _Env(DPWA_VMM="1") if vmm else _Env():
@@ -648,14 +704,15 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
                 if kind == "local":                   # one GPU: both learners in this process, batched
                     from dpwa_amd.group import LocalGroup
                     _, rec = parity_lockstep(names, [(names[0], 0), (names[1], 1)], cfg, LocalGroup(), None, device,
-                                             conns=conns, batch=True)
+                                             conns=conns, batch=True, resident=res)
                 elif kind == "lockstep":
-                    _, r = parity_lockstep(names, [(names[rank], rank)], cfg, "lockstep", pull, device, conns=conns)
+                    _, r = parity_lockstep(names, [(names[rank], rank)], cfg, "lockstep", pull, device, conns=conns,
+                                           resident=res)
                     rec = r[rank]
                 else:                                  # async: free-running over the gossip board
                     wt = pull.endswith("+wt")
                     check = parity_async(names, rank, cfg, pull.replace("+wt", ""), device, write_through=wt,
-                                         conns=conns)
+                                         conns=conns, resident=res)
                 if injected(t, rank, "end"):
                     raise RuntimeError("injected failure (DPWA_BENCH_INJECT, end)")
         except Exception as e:   # noqa: BLE001 -- reported as this transport's parity false
@@ -667,12 +724,13 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
                     c.close()
                 except Exception as e:   # noqa: BLE001
                     progress("parity %s: close failed: %s" % (t, e))
+        want = expected[res] if expected is not None else None
         if kind == "local":
-            ok = err is None and rec == expected
+            ok = err is None and rec == want
         elif kind == "lockstep":
             got = [None] * world
             dist.all_gather_object(got, rec if err is None else None, group=ctl)
-            ok = rank != 0 or (all(g is not None for g in got) and all(got[g] == expected[g] for g in range(world)))
+            ok = rank != 0 or (all(g is not None for g in got) and all(got[g] == want[g] for g in range(world)))
         else:
             ok = _async_verdict(t, names, world, rank, check, err, ctl)
         if err is not None:
@@ -729,7 +787,7 @@ def _async_verdict(t, names, world, rank, check, err, ctl):
 
 
 # ---------------------------------------------------------------- kernel measurements
-def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners=1):
+def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners=1, resident=False):
     """The product averaging kernel alone over rotating buffers (> 1.2 GB of other traffic
     between two uses of a buffer, so nothing is served from the 256 MiB Infinity Cache).  With
     learners == 1 it is dpwa_average (k_lerp<Ops, COEF_FUSED, write_through>: fp64 device
@@ -738,9 +796,12 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
     dispatch (k_lerp_batch, the N=1 loop's kernel).  Every launch is timed by its own dispatch
     begin/end events (hipExtLaunchKernelGGL), as rocprofv3 times a kernel: the inter-kernel
     gaps of a back-to-back batch are not counted.  Also returns the rate of one event pair
-    around the whole batch (which does include the gaps)."""
+    around the whole batch (which does include the gaps).  `resident`: the resident form
+    (dpwa_average_many_resident): the parameters are read from one snapshot payload and the result
+    stored into another, nothing written back in place (3*N*s)."""
     from dpwa_amd import _lib
     esize = 4 if dtype == torch.float32 else 2
+    write_through = write_through or resident
     nbuf = 3 if write_through else 2
     per_set = learners * nbuf * numel * esize
     # > 1.2 GB of other traffic between two uses of a buffer; a set that large by itself is its
@@ -781,7 +842,10 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
     def run(i, timed):
         a, b = ev[i] if timed else (None, None)
         ea, eb = (a.cuda_event, b.cuda_event) if timed else (None, None)
-        if learners == 1:
+        if resident:
+            rc = lib.dpwa_average_many_resident(dt, descs[i % sets], learners, ctypes.byref(cfg), s, ea, eb)
+            name = "dpwa_average_many_resident"
+        elif learners == 1:
             param, slot, snap = bufs[i % sets][0]
             rc = lib.dpwa_average(dt, param.data_ptr(), slot.data_ptr(), numel, ctypes.byref(cfg),
                                   clocks[0].data_ptr(), 1.0, coefs[0].data_ptr(),
@@ -811,10 +875,10 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
             "rotating_buffer_sets": sets, "learners_per_launch": learners, "batch_bracket_us": float(batch_us)}
 
 
-def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None):
-    """Whole gossip rounds (two co-resident learners, write-through publish, constant 0.5,
-    fetch_probability 1, both averages in one dispatch) at every north_star size in its
-    config's dtype: the averaged GB/s and rounds/s the north star asks for at 11M/100M/1B/7B
+def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None, publish="resident"):
+    """Whole gossip rounds (two co-resident learners, `publish` form -- resident or write-through --,
+    constant 0.5, fetch_probability 1, both averages in one dispatch) at every north_star size in
+    its config's dtype: the averaged GB/s and rounds/s the north star asks for at 11M/100M/1B/7B
     on one GPU."""
     from dpwa_amd import DpwaConnection
     from dpwa_amd.group import LocalGroup
@@ -831,16 +895,25 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None):
             flats.append(t)
         group = LocalGroup()
         conns = [DpwaConnection(nm, cfg, seed=1000 + g, group=group) for g, nm in enumerate(("w1", "w2"))]
+        resident = publish == "resident"
+        if resident:
+            for c, f in zip(conns, flats):
+                c.make_resident(f)
+            del flats
+            flats = [c.parameters for c in conns]
 
         def step():
             for c, f in zip(conns, flats):
                 c.update_send(f, 1.0, reuse_snapshot=True)
             if batch:
                 res = DpwaConnection.update_wait_average_many(conns, flats, [1.0, 1.0], write_through=True)
-                return sum(p is not None for p, _ in res)
-            n = 0
-            for c, f in zip(conns, flats):
-                n += c.update_wait_average(f, 1.0, write_through=True)[0] is not None
+                n = sum(p is not None for p, _ in res)
+            else:
+                n = 0
+                for c, f in zip(conns, flats):
+                    n += c.update_wait_average(f, 1.0, write_through=True)[0] is not None
+            if resident:
+                flats[:] = [c.parameters for c in conns]
             return n
 
         for _ in range(warmup):
@@ -852,7 +925,7 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None):
         el = time.perf_counter() - t0
         rows.append({"numel": numel, "dtype": dt, "value": round(averaged * 3 * numel * esize / el / 1e9, 1),
                      "ms_per_step": round(1e3 * el / steps, 4), "gossip_rounds_per_s": round(2 * steps / el, 1),
-                     "steps": steps, "batched": batch})
+                     "steps": steps, "batched": batch, "publish": publish})
         for c in conns:
             c.close()
         del flats, conns
@@ -861,7 +934,7 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None):
 
 
 def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, watchdog, min_steps=3, warmup=2,
-                     max_numel=None, rows=None):
+                     max_numel=None, rows=None, resident=False):
     """N > 1: whole gossip rounds at every north_star size (configs[1..4] sizes and dtypes), one
     learner per rank, on the transport the trials chose (`pull`: "<mode>" lock-step or
     "async/<mode>[+wt]"), constant 0.5, fetch_probability 1 -- the GB/s and rounds/s table of
@@ -873,7 +946,7 @@ def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, wat
     cfg = os.path.join(cfg_dir, "dist_sweep.yaml")     # every rank its own copy (cfg_dir is per rank)
     write_config(cfg, names, "constant")
     sel_async = pull.startswith("async/")
-    mode = pull.split("/")[-1].replace("+wt", "")
+    mode = trial_mode(pull)
     # ranks sharing a device (rehearsals) split its free memory
     share = max(1, -(-world // max(1, torch.cuda.device_count())))
     rows = [] if rows is None else rows
@@ -900,10 +973,15 @@ def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, wat
             flat.normal_(generator=torch.Generator(device=device).manual_seed(rank))
             conn = DpwaConnection(names[rank], cfg, seed=1000 + rank, group="async" if sel_async else "lockstep",
                                   pull=mode)
+            if resident:
+                conn.make_resident(flat)
+                del flat
+                flat = None
 
             def step():
-                conn.update_send(flat, 1.0, reuse_snapshot=write_through)
-                return conn.update_wait_average(flat, 1.0, write_through=write_through)[0] is not None
+                f = conn.parameters if resident else flat
+                conn.update_send(f, 1.0, reuse_snapshot=write_through)
+                return conn.update_wait_average(f, 1.0, write_through=write_through)[0] is not None
 
             for _ in range(warmup):
                 step()
@@ -933,7 +1011,8 @@ def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, wat
             rows.append({"numel": numel, "dtype": dt, "value": round(av * 3 * numel * esize / el_max / 1e9, 1),
                          "ms_per_step": round(1e3 * el_max / steps, 3),
                          "gossip_rounds_per_s": round(world * steps / el_max, 1), "averagings": int(av),
-                         "steps": steps, "transport": pull, "publish": "write-through" if write_through else "full"})
+                         "steps": steps, "transport": pull,
+                         "publish": "resident" if resident else "write-through" if write_through else "full"})
             progress("dist sweep %d %s: %.1f GB/s" % (numel, dt, rows[-1]["value"]))
         else:
             rows.append({"numel": numel, "dtype": dt, "error": err or "failed on another rank", "transport": pull})
@@ -951,18 +1030,23 @@ def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, wat
 
 def size_sweep(device, rows=None):
     """The averaging kernel, cold, per launch, at every north_star size (11.17M/100M fp32,
-    1B/7B bf16), in both publish forms: plain (3*N*s bytes per launch) and write-through
-    (4*N*s: the next snapshot is written by the same pass); and at 11.17M / 100M the batched
-    dispatch of two learners' write-through averages (the N=1 loop's kernel, 2 x 4*N*s)."""
+    1B/7B bf16), in every publish form: plain (3*N*s bytes per launch), write-through
+    (4*N*s: the next snapshot is written by the same pass) and resident (3*N*s: read one slot,
+    write the other); and at 11.17M / 100M the batched dispatch of two learners' averages (the
+    N=1 loop's kernel, 2 x the form's bytes)."""
     rows = [] if rows is None else rows
     for numel, dt in SWEEP:
         esize = 4 if dt == "f32" else 2
-        forms = [(False, 1), (True, 1)] + ([(True, 2)] if numel <= 100_000_000 else [])
-        for wt, learners in forms:
-            c = cold_kernel(numel, torch.float32 if dt == "f32" else torch.bfloat16, device, wt, learners=learners)
+        forms = [("full", 1), ("write-through", 1), ("resident", 1)]
+        if numel <= 100_000_000:
+            forms += [("write-through", 2), ("resident", 2)]
+        for form, learners in forms:
+            wt = form == "write-through"
+            c = cold_kernel(numel, torch.float32 if dt == "f32" else torch.bfloat16, device, wt, learners=learners,
+                            resident=form == "resident")
             nbytes = learners * (4 if wt else 3) * numel * esize
             gbs = nbytes / (c["avg_launch_us"] * 1e-6) / 1e9
-            rows.append({"numel": numel, "dtype": dt, "publish": "write-through" if wt else "full",
+            rows.append({"numel": numel, "dtype": dt, "publish": form,
                          "learners_per_launch": learners,
                          "bytes_per_launch": nbytes, "avg_launch_us": round(c["avg_launch_us"], 2),
                          "median_launch_us": round(c["median_launch_us"], 2), "achieved": round(gbs, 1),
@@ -1055,6 +1139,12 @@ def main(argv=None):
         conn = DpwaConnection(name, cfg, seed=1000 + seed, group=group if world == 1 else "lockstep",
                               pull="relay" if world > 1 else None)
         learners.append((conn, flat))
+    resident_main = args.publish == "resident"
+    if resident_main:
+        # the parameters move into each learner's own snapshot slots (binds it: at N>1 every rank
+        # runs this in the same order, the binding's exchange is collective)
+        for conn, flat in learners:
+            conn.make_resident(flat)
 
     stream = torch.cuda.current_stream(device)
     # co-resident learners on their own streams (their kernels overlap) or all on one
@@ -1085,7 +1175,9 @@ def main(argv=None):
         timed_learners = []
 
         conns_ = [c for c, _ in learners]
-        flats_ = [f for _, f in learners]
+        # resident learners: their parameters are where the learner keeps them (read once a round)
+        resident = conns_[0]._learner is not None and conns_[0].parameters is not None
+        flats_ = [c.parameters for c in conns_] if resident else [f for _, f in learners]
         one_stream = all(st is stream for st in streams)
         const_loss = [1.0] * len(learners) if args.loss_schedule == "constant" else None
 
@@ -1093,12 +1185,12 @@ def main(argv=None):
             done = 0
             losses = const_loss or [loss_of(i) for i in range(len(learners))]
             loss_t[0] += 1
-            for i, (conn, flat) in enumerate(learners):
+            for i, conn in enumerate(conns_):
                 if one_stream:      # (a stream context costs microseconds of host time per round)
-                    conn.update_send(flat, losses[i], reuse_snapshot=write_through)
+                    conn.update_send(flats_[i], losses[i], reuse_snapshot=write_through)
                 else:
                     with torch.cuda.stream(streams[i]):
-                        conn.update_send(flat, losses[i], reuse_snapshot=write_through)
+                        conn.update_send(flats_[i], losses[i], reuse_snapshot=write_through)
             sample = timed and sample_every and k % sample_every == 0
             if batched:
                 if sample:
@@ -1109,6 +1201,8 @@ def main(argv=None):
                         for c in timed_learners:
                             lib.dpwa_learner_arm_timing(c._learner.handle)
                 res = DpwaConnection.update_wait_average_many(conns_, flats_, losses, write_through=write_through)
+                if resident:
+                    flats_[:] = [c.parameters for c in conns_]
                 got = [p is not None for p, _ in res]
                 if sample and any(got):
                     sampled.append((got.index(True), sum(got)))     # (pair owner, averages in the dispatch)
@@ -1116,7 +1210,8 @@ def main(argv=None):
                         b.record(stream)
                         lerp_events.append((a, b))
                 return sum(got)
-            for i, (conn, flat) in enumerate(learners):
+            for i, conn in enumerate(conns_):
+                flat = flats_[i]
                 st = streams[i]
                 with (_NoCtx if one_stream else torch.cuda.stream(st)):
                     # the adapter's update_wait: fused device factor + lerp (one kernel)
@@ -1129,6 +1224,8 @@ def main(argv=None):
                         if args.timing != "bracket" and conn in timed_learners:
                             lib.dpwa_learner_arm_timing(conn._learner.handle)
                     payload, _ = conn.update_wait_average(flat, losses[i], write_through=write_through)
+                    if resident:
+                        flats_[i] = conn.parameters
                     if sample and args.timing != "dispatch":
                         b.record(st)
                         if payload is not None:
@@ -1185,6 +1282,11 @@ def main(argv=None):
             return (max(g[0] for g in got), sum(g[1] for g in got), sum(g[2] for g in got), lerp_ms)
         return elapsed, float(averaged), float(len(learners) * steps), lerp_ms
 
+    def params_of(conn, flat):
+        """Where a learner's parameters are now: its resident slot, else its flat buffer."""
+        p = conn.parameters if conn._learner is not None else None
+        return flat if p is None else p
+
     def make_compute(target_us):
         """A fixed-duration stand-in for a training step: k back-to-back
         4096^3 bf16 GEMMs on the compute stream, k calibrated to ~target_us."""
@@ -1220,18 +1322,18 @@ def main(argv=None):
             loss_t[0] += 1
             if gossip:
                 for i, (conn, flat) in enumerate(learners):
-                    conn.update_send(flat, losses[i], reuse_snapshot=wt_main)
+                    conn.update_send(params_of(conn, flat), losses[i], reuse_snapshot=wt_main)
             for _ in learners:
                 compute()
             if gossip:
                 if batched:
                     res = DpwaConnection.update_wait_average_many([c for c, _ in learners],
-                                                                  [f for _, f in learners], losses,
+                                                                  [params_of(c, f) for c, f in learners], losses,
                                                                   write_through=wt_main)
                     done += sum(p is not None for p, _ in res)
                 else:
                     for i, (conn, flat) in enumerate(learners):
-                        payload, _ = conn.update_wait_average(flat, losses[i], write_through=wt_main)
+                        payload, _ = conn.update_wait_average(params_of(conn, flat), losses[i], write_through=wt_main)
                         done += payload is not None
             return done
 
@@ -1263,7 +1365,8 @@ def main(argv=None):
     pull_trials = {}
     trial_errors = {}
     pull = args.pull
-    wt_lockstep = args.publish == "write-through"     # free-running rounds always publish in full
+    wt_lockstep = args.publish == "write-through"     # lock-step rounds' publish form (resident: resident_main)
+    res_sfx = "+res" if resident_main else ""
     lockstep_learners = list(learners)
     async_learners = []
     if world > 1:
@@ -1274,19 +1377,21 @@ def main(argv=None):
                                                          "relay-avg:128", "relay-avg:512"]
         cands = []          # (key, lockstep?, pull mode, write-through)
         if args.gossip != "async":
-            cands += [(m, True, m, wt_lockstep) for m in modes if verified(m)]
+            cands += [(m + res_sfx, True, m, wt_lockstep) for m in modes if verified(m + res_sfx)]
         if args.gossip != "lockstep":
             wd.enter("binding free-running learner(s)", 600.0)
-            # free-running rounds over the gossip board, same learners' parameters (a second
-            # set of nodes: a connection's group is fixed at construction)
+            # free-running rounds over the gossip board, same learners' initial parameters (a
+            # second set of nodes: a connection's group is fixed at construction)
             for (name, seed), (_, flat) in zip(mine, lockstep_learners):
                 conn = DpwaConnection(name, cfg, seed=1000 + seed, group="async", pull="copy")
+                if resident_main:
+                    conn.make_resident(flat)
                 async_learners.append((conn, flat))
             learners[:] = async_learners
             run(2, 2, False)
             for m in [m for m in modes if not m.startswith("relay")]:
                 for wt in ((False, True) if wt_lockstep else (False,)):
-                    key = "async/" + m + ("+wt" if wt else "")
+                    key = "async/" + m + ("+wt" if wt else res_sfx)
                     if verified(key):
                         cands.append((key, False, m, wt))
         # interleaved passes, each trial >= --trial-ms and >= 30 rounds; the median decides
@@ -1325,20 +1430,20 @@ def main(argv=None):
         pull = max(medians, key=medians.get)
         if pull.startswith("async/"):
             learners[:] = async_learners
-            set_pull(pull[len("async/"):].replace("+wt", ""))
+            set_pull(trial_mode(pull))
         else:
             learners[:] = lockstep_learners
             for conn, _ in async_learners:   # free their streams and slots (fewer HW queues in use)
                 conn.close()
             async_learners = []
             hbarrier()
-            set_pull(pull)
-    # trial key: "<mode>" (lock-step, publish per --publish) or "async/<mode>[+wt]"
+            set_pull(trial_mode(pull))
+    # trial key: "<mode>[+res]" (lock-step, publish per --publish) or "async/<mode>[+wt|+res]"
     sel_async = pull.startswith("async/")
-    sel_mode = pull.split("/")[-1].replace("+wt", "")
+    sel_mode = trial_mode(pull)
     wt_main = pull.endswith("+wt") if sel_async else wt_lockstep
-    wd.enter("timed run: %s, %s publish" % (pull, "write-through" if wt_main else "full"),
-             600.0 + 0.05 * (args.steps + args.warmup))
+    form = "resident" if resident_main else "write-through" if wt_main else "full"
+    wd.enter("timed run: %s, %s publish" % (pull, form), 600.0 + 0.05 * (args.steps + args.warmup))
     elapsed, averaged, rounds, _ = run(args.steps, args.warmup, wt_main)
     progress("timed run: %.4f ms/step" % (1e3 * elapsed / args.steps))
     # the averaging kernel inside the loop: a separate sampled pass of the same rounds
@@ -1363,11 +1468,25 @@ def main(argv=None):
         dist.all_gather_object(got, float(np.mean(pull_us)) if pull_us else float("nan"), group=ctl)
         pull_us = [float(np.mean(got))]
     secondary = None
-    if not args.no_secondary:      # the other publish form, same learners and transport, for comparison
+    if not args.no_secondary and not resident_main:   # the other publish form, same learners and transport
         wd.enter("secondary publish form", 600.0)
         s2 = run(args.steps, args.warmup, not wt_main)
         s2_k = run(s_steps, 2, not wt_main, args.sample_every)
-        secondary = (not wt_main, s2, s2_k[3])
+        secondary = ("write-through" if not wt_main else "full", s2, s2_k[3])
+    elif not args.no_secondary and world == 1:
+        # resident learners cannot leave their slots: the write-through form runs on a second pair
+        # of learners (same initial parameters, same rounds)
+        wd.enter("secondary publish form", 600.0)
+        main_set = list(learners)
+        grp2 = LocalGroup()
+        learners[:] = [(DpwaConnection(name, cfg, seed=1000 + seed, group=grp2), flat.clone())
+                       for (name, seed), (_, flat) in zip(mine, main_set)]
+        s2 = run(args.steps, args.warmup, True)
+        s2_k = run(s_steps, 2, True, args.sample_every)
+        secondary = ("write-through", s2, s2_k[3])
+        for conn, _ in learners:
+            conn.close()
+        learners[:] = main_set
     overlap = None
     if args.compute_us > 0:
         wd.enter("overlap", 600.0)
@@ -1381,7 +1500,7 @@ def main(argv=None):
             # the copy engine leaves every CU to the training step: try it beside the
             # pure-loop winner and keep the cheaper overlap
             for m in [m for m in (o_mode, "copy")
-                      if verified(m if not sel_async else "async/" + m + ("+wt" if wt_main else ""))]:
+                      if verified((m + res_sfx) if not sel_async else "async/" + m + ("+wt" if wt_main else res_sfx))]:
                 set_pull(m)
                 o_trials[m] = run_overlap(o_steps, 3, compute, gossip=True)
             o_mode = min(o_trials, key=o_trials.get)
@@ -1416,18 +1535,19 @@ def main(argv=None):
                               "oracle/gossip.py (lock-step) and oracle/async_check.py (per version read); '+vmm': "
                               "snapshot slots (and relay buffers) fd-shared hipMemCreate chunks, the configs[3]/[4] "
                               "path" % (PARITY_N, PARITY_T, PARITY_FP, PARITY_ASYNC_T))
-    used = "local" if world == 1 else parity_key(pull)
+    used = ("local+res" if resident_main else "local") if world == 1 else parity_key(pull)
 
     unit_bytes = 3 * args.numel * esize
     per_launch = len(learners) if batched else 1
-    kbytes = (4 if wt_main else 3) * args.numel * esize * per_launch   # the timed loop's averaging dispatch
+    wt_kernel = wt_main and not resident_main      # resident: the kernel moves the averaging's 3*N*s only
+    kbytes = (4 if wt_kernel else 3) * args.numel * esize * per_launch   # the timed loop's averaging dispatch
     # the same kernel alone, cold (rotating buffers, per-launch dispatch events): the roofline's basis
     cold = None
     cold_plain = None
     if not args.no_cold:
         wd.enter("cold kernel", 300.0)
-        cold = cold_kernel(args.numel, dtype, device, wt_main, learners=per_launch)
-        if wt_main:     # BASELINE's target kernel: the same dispatch without the snapshot write
+        cold = cold_kernel(args.numel, dtype, device, wt_kernel, learners=per_launch, resident=resident_main)
+        if wt_kernel:   # BASELINE's target kernel: the same dispatch without the snapshot write
             cold_plain = cold_kernel(args.numel, dtype, device, False, learners=per_launch)
     wd.enter("report", 120.0)
     out = None
@@ -1440,7 +1560,7 @@ def main(argv=None):
             else float("nan")
         k_us = cold["avg_launch_us"] if cold else lerp_us
         achieved = kbytes / (k_us * 1e-6) / 1e9
-        variant = "write-through" if wt_main else "full"
+        variant = form
         traffic, traffic_src = None, None
         tname = "traffic_r03_%s%s.json" % (variant, "_x%d" % per_launch if per_launch > 1 else "")
         tpath = args.traffic or os.path.join(ROOT, "profiles", tname)
@@ -1452,12 +1572,20 @@ def main(argv=None):
                     tr.get("basis", "in-loop") == ("cold" if cold else "in-loop")):
                 traffic = tr.get("hbm_bytes_per_launch")
                 traffic_src = os.path.relpath(tpath, ROOT)
-        kname = ("dpwa::k_lerp_batch<Ops%s, %s> (%d learners' fused device factor + lerp%s in one dispatch)"
-                 % (args.dtype.upper(), "true" if wt_main else "false", per_launch,
-                    " + write-through of the next snapshot" if wt_main else "") if per_launch > 1 else
-                 "dpwa::k_lerp<Ops%s, COEF_FUSED, %s> (fused device factor + lerp%s)"
-                 % (args.dtype.upper(), "true" if wt_main else "false",
-                    " + write-through of the next snapshot" if wt_main else ""))
+        if resident_main:
+            kname = ("dpwa::k_lerp_batch<Ops%s, true, 8, true> (%d resident learners' fused device factor + lerp "
+                     "in one dispatch: each reads its published slot and writes the other)" % (args.dtype.upper(),
+                                                                                               per_launch)
+                     if per_launch > 1 else
+                     "dpwa::k_lerp<Ops%s, COEF_FUSED, true, 64, 8, true> (resident: fused device factor + lerp "
+                     "from the published slot into the other)" % args.dtype.upper())
+        else:
+            kname = ("dpwa::k_lerp_batch<Ops%s, %s> (%d learners' fused device factor + lerp%s in one dispatch)"
+                     % (args.dtype.upper(), "true" if wt_main else "false", per_launch,
+                        " + write-through of the next snapshot" if wt_main else "") if per_launch > 1 else
+                     "dpwa::k_lerp<Ops%s, COEF_FUSED, %s> (fused device factor + lerp%s)"
+                     % (args.dtype.upper(), "true" if wt_main else "false",
+                        " + write-through of the next snapshot" if wt_main else ""))
         out = base_line(args, world)
         out.update({
             "value": round(value, 2),
@@ -1498,7 +1626,10 @@ def main(argv=None):
                 "learners_per_launch": per_launch,
                 "bytes_per_launch": kbytes,
                 "bytes_note": (("%d x " % per_launch if per_launch > 1 else "") +
-                               ("4*N*s: read parameters, read peer snapshot, write parameters, write the next "
+                               ("3*N*s: read the parameters (the published slot they are in), read the peer "
+                                "snapshot, write the parameters into the learner's other slot (the next publish "
+                                "then moves nothing)" if resident_main else
+                                "4*N*s: read parameters, read peer snapshot, write parameters, write the next "
                                 "snapshot (which the publish then does not copy)" if wt_main else
                                 "3*N*s: read parameters, read peer snapshot, write parameters")),
                 "avg_launch_us": round(k_us, 2),
@@ -1549,7 +1680,7 @@ def main(argv=None):
                         "next snapshot, i.e. what the full-publish rounds run; the timed loop's kernel is the "
                         "write-through one above",
             }
-        if wt_main and args.numel == RESNET18_NUMEL and args.dtype == "f32":
+        if wt_kernel and args.numel == RESNET18_NUMEL and args.dtype == "f32":
             out["roofline"]["vs_mix_ceiling"] = dict(MIX_CEILING_11M, kernel_frac_over_ceiling=round(
                 achieved / HBM_PEAK_GBS / MIX_CEILING_11M["frac"], 4),
                 note="the chip's cold ceiling for one 11.17M-element 2R:2W launch (single learner); a batched "
@@ -1585,17 +1716,20 @@ def main(argv=None):
                             "(barriers and the average included): a lower bound on the link rate",
                 }
         if secondary is not None:
-            s_wt, (w_el, w_avg, w_rounds, _), (w_ms, _, w_n) = secondary
+            s_form, (w_el, w_avg, w_rounds, _), (w_ms, _, w_n) = secondary
+            s_wt = s_form == "write-through"
             w_us = float(np.nanmean(w_ms) * 1e3)
             w_bytes = (4 if s_wt else 3) * args.numel * esize * float(np.nanmean(w_n))
             out["secondary_publish"] = {
-                "publish": "write-through" if s_wt else "full",
+                "publish": s_form,
                 "value": round(w_avg * unit_bytes / w_el / 1e9, 2),
                 "ms_per_step": round(1e3 * w_el / args.steps, 4),
                 "avg_launch_us": round(w_us, 2),
                 "kernel_gbs": round(w_bytes / (w_us * 1e-6) / 1e9, 1),
-                "note": "the same rounds with the other publish form (value from an uninstrumented pass, the kernel "
-                        "from a sampled one). write-through: the averaging kernel also writes the next snapshot "
+                "note": "the same rounds with another publish form (value from an uninstrumented pass, the kernel "
+                        "from a sampled one; under a resident main run, a second pair of learners). resident: the "
+                        "parameters live in the learner's two slots, the average reads one and writes the other "
+                        "(3*N*s) and the publish moves nothing. write-through: the averaging kernel also writes the next snapshot "
                         "(4*N*s) and the publish moves nothing; full: every publish copies the 2*N*s snapshot. "
                         "Write-through is valid when nothing modifies the parameters between update_wait and the "
                         "next update_send (the reference's loop, examples/pytorch-cifar/main.py:130-145); the "
@@ -1621,7 +1755,8 @@ def main(argv=None):
         wd.enter("size sweep", 900.0)
         size_sweep(device, rows=size_rows)
         wd.enter("round sweep", 900.0)
-        round_sweep(device, tmp, batch=batched, rows=round_rows)
+        round_sweep(device, tmp, batch=batched, rows=round_rows,
+                    publish="resident" if resident_main else "write-through")
     elif world > 1 and not args.no_sweep:
         # the timed learners' buffers go first: the sweep's 7B learner needs ~80 GB per GPU
         for conn, _ in lockstep_learners + async_learners:
@@ -1631,7 +1766,7 @@ def main(argv=None):
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         dist_round_sweep(world, rank, device, tmp, pull, wt_main, ctl, wd, max_numel=args.dist_sweep_max_numel,
-                         rows=round_rows)
+                         rows=round_rows, resident=resident_main)
     wd.enter("result", 60.0)
     if out is not None:
         emit(json.dumps(out))

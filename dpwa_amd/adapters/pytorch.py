@@ -36,13 +36,25 @@ class DpwaPyTorchAdapter:
     words spread over the parameters with the snapshot on the device and publishes in full when
     any differs (two small kernels per update_send, no host sync).  A write that changes none
     of the sampled words is not seen: a loop that writes parameters sparsely through
-    ``param.data`` between update_wait and update_send should pass ``write_through=False``."""
+    ``param.data`` between update_wait and update_send should pass ``write_through=False``.
+
+    resident (extension, off by default): the parameters live in the learner's own two snapshot
+    slots (``DpwaConnection.make_resident``) and every ``param.data`` is re-pointed to the slot
+    they are in after each update_wait -- a publish moves no bytes and an average moves 3*N*s
+    (the write-through form 4*N*s), for one ``.data`` assignment per parameter per round on the
+    host.  Writes through ``param.data`` are then always part of the next snapshot (no reuse
+    guard is needed); what must hold is the reference loop's order: nothing writes the
+    parameters between update_send and update_wait (they are the served snapshot then).  Code
+    that keeps raw data pointers of the parameters across rounds (a captured HIP graph of the
+    training step) must not use it."""
 
     def __init__(self, net, name, config_file, write_through=True, transport="device", reuse_guard=True,
-                 **connection_kwargs):
+                 resident=False, **connection_kwargs):
         """transport: "device" (peers are learners of this process or of the torch.distributed
         job, pulled from HBM/over xGMI) or "wire" (peers are reached over TCP at the YAML's
         host/port with the reference's protocol -- e.g. reference CPU nodes; dpwa_amd/bridge.py)."""
+        if resident and transport != "device":
+            raise ValueError("resident parameters need the device transport")
         self._net = net
         gpu = DpwaConfiguration(config_file).get_gpu(name)      # optional per-node placement
         self._flat = FlatParameters(net.named_parameters(), device=None if gpu is None else torch.device("cuda", gpu))
@@ -55,6 +67,7 @@ class DpwaPyTorchAdapter:
         else:
             raise ValueError("transport must be 'device' or 'wire'")
         self._write_through = bool(write_through) and transport == "device"
+        self._resident = bool(resident)
         self._reuse_guard = bool(reuse_guard)
         self._guard_set = False
         self._versions = None
@@ -64,6 +77,13 @@ class DpwaPyTorchAdapter:
 
     def update_send(self, loss):
         """pytorch.py:42-53: publish the parameters and maybe start a fetch."""
+        if self._resident:
+            if self._conn.parameters is None:          # first round: into the learner's slot 0
+                self._flat.resync()
+                self._flat.rehome(self._conn.make_resident(self._flat.buffer))
+            self._flat.resync()                        # a parameter re-homed by the caller
+            self._conn.update_send(self._flat.buffer, loss)
+            return
         moved = self._flat.resync()
         reuse = (self._write_through and moved == 0 and self._versions is not None
                  and self._versions == self._param_versions())
@@ -74,7 +94,12 @@ class DpwaPyTorchAdapter:
             self._guard_set = True
 
     def update_wait(self, loss):
-        """pytorch.py:55-68: wait for the fetch and average in place."""
+        """pytorch.py:55-68: wait for the fetch and average in place (resident: into the other
+        slot, where the parameters are re-pointed)."""
+        if self._resident:
+            self._conn.update_wait_average(self._flat.buffer, loss)
+            self._flat.rehome(self._conn.parameters)
+            return
         payload, _ = self._conn.update_wait_average(self._flat.buffer, loss, write_through=self._write_through)
         if self._write_through and payload is not None:
             self._versions = self._param_versions()
@@ -88,18 +113,20 @@ class DpwaPyTorchAdapter:
         adapters = list(adapters)
         if not adapters:
             return
-        wts = {a._write_through for a in adapters}
+        wts = {(a._write_through, a._resident) for a in adapters}
         if len(wts) != 1 or any(not isinstance(a._conn, DpwaConnection) or type(a._conn) is not DpwaConnection
                                 for a in adapters):
             for a, loss in zip(adapters, losses):     # mixed forms or wire peers: one by one
                 a.update_wait(loss)
             return
-        wt = wts.pop()
+        wt, resident = wts.pop()
         res = DpwaConnection.update_wait_average_many([a._conn for a in adapters],
                                                       [a._flat.buffer for a in adapters], list(losses),
                                                       write_through=wt)
         for a, (payload, _) in zip(adapters, res):
-            if wt and payload is not None:
+            if resident:
+                a._flat.rehome(a._conn.parameters)
+            elif wt and payload is not None:
                 a._versions = a._param_versions()
 
     @property

@@ -413,6 +413,10 @@ class WireConnection(DpwaConnection):
     def last_fetch_peer(self):
         return None
 
+    def make_resident(self, parameters):
+        raise NotImplementedError("resident parameters need the device transport (the wire bridge reads "
+                                  "published slots from the host)")
+
     def close(self):
         self._join()
         if getattr(self, "_server", None) is not None:

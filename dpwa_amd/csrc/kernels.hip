@@ -286,8 +286,11 @@ struct StripeSrc {
 
 // One 16-byte item per lane; items beyond n/PER (the ragged tail) go to block 0.
 // DUAL also stores the result into args.snap (write-through snapshot: the next publish of
-// these parameters then needs no copy).  BLOCK lanes per workgroup (kStreamBlock).
-template <class Ops, int MODE, bool DUAL, int BLOCK, int POLICY, class Src>
+// these parameters then needs no copy).  OOP (with DUAL): the result is stored into args.snap
+// ONLY -- the resident form, whose parameters live in the learner's own snapshot slots and move
+// from the published slot to the next one at every average (2 reads + 1 write per element, the
+// averaging's own bytes; learner.cpp "resident").  BLOCK lanes per workgroup (kStreamBlock).
+template <class Ops, int MODE, bool DUAL, int BLOCK, int POLICY, class Src, bool OOP = false>
 __device__ __forceinline__ void lerp_span(uint32_t blk, typename Ops::V *__restrict__ param, const Src &src,
                                           int64_t n, const LerpArgs &args)
 {
@@ -338,7 +341,7 @@ __device__ __forceinline__ void lerp_span(uint32_t blk, typename Ops::V *__restr
     }
     {
         const V r = Ops::lerp(a, b, q, p);
-        span_store<V, LerpPolicy<POLICY>::store>(rp, lane_off, r);
+        if (!OOP) span_store<V, LerpPolicy<POLICY>::store>(rp, lane_off, r);
         if (DUAL) span_store<V, LerpPolicy<POLICY>::snap_store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, r);
     }
     if (blk == 0 && threadIdx.x < n - nv * Ops::PER) {
@@ -346,26 +349,27 @@ __device__ __forceinline__ void lerp_span(uint32_t blk, typename Ops::V *__restr
         S *ps = reinterpret_cast<S *>(param);
         const int64_t j = nv * Ops::PER + threadIdx.x;
         const S r = Ops::lerp_s(a, b, *reinterpret_cast<const S *>(src.at(j * (int64_t)sizeof(S))), ps[j]);
-        ps[j] = r;
+        if (!OOP) ps[j] = r;
         if (DUAL) reinterpret_cast<S *>(args.snap)[j] = r;
     }
 }
 
-template <class Ops, int MODE, bool DUAL, int BLOCK = kBlock, int POLICY = 0>
+template <class Ops, int MODE, bool DUAL, int BLOCK = kBlock, int POLICY = 0, bool OOP = false>
 __global__ __launch_bounds__(BLOCK) void k_lerp(typename Ops::V *__restrict__ param,
                                                 const typename Ops::V *__restrict__ peer, int64_t n, LerpArgs args)
 {
-    lerp_span<Ops, MODE, DUAL, BLOCK, POLICY>(blockIdx.x, param, ContigSrc{(const char *)peer}, n, args);
+    lerp_span<Ops, MODE, DUAL, BLOCK, POLICY, ContigSrc, OOP>(blockIdx.x, param, ContigSrc{(const char *)peer}, n,
+                                                              args);
 }
 
 // The relay's fused second phase: the fused average reads the peer's snapshot stripe by stripe
 // where the relay left it (stripe s in rank s's relay buffer, the peer's own stripe in its slot,
 // ours in local HBM) instead of gathering it into staging first.
-template <class Ops, bool DUAL, int POLICY = 0>
+template <class Ops, bool DUAL, int POLICY = 0, bool OOP = false>
 __global__ __launch_bounds__(kStreamBlock) void k_lerp_relay(typename Ops::V *__restrict__ param, int64_t n,
                                                              LerpArgs args, StripeSrc src)
 {
-    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, POLICY>(blockIdx.x, param, src, n, args);
+    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, POLICY, StripeSrc, OOP>(blockIdx.x, param, src, n, args);
 }
 
 // Several independent fused averages in ONE dispatch (co-resident learners of one round:
@@ -373,7 +377,7 @@ __global__ __launch_bounds__(kStreamBlock) void k_lerp_relay(typename Ops::V *__
 // single-average span code for its entry, so the per-learner semantics (factor, clock commit by
 // the entry's first workgroup, ragged tail) are those of k_lerp.  One launch instead of one per
 // learner removes a ramp, a drain and a kernel boundary per extra learner.
-template <class Ops, bool DUAL, int POLICY = 0>
+template <class Ops, bool DUAL, int POLICY = 0, bool OOP = false>
 __global__ __launch_bounds__(kStreamBlock) void k_lerp_batch(AvgBatch batch)
 {
     int i = 0;
@@ -395,8 +399,8 @@ __global__ __launch_bounds__(kStreamBlock) void k_lerp_batch(AvgBatch batch)
     LerpArgs args{};
     args.fused = e.fa;
     args.snap = e.snap;
-    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, POLICY>(blk, (typename Ops::V *)e.param,
-                                                           ContigSrc{(const char *)e.peer}, e.n, args);
+    lerp_span<Ops, COEF_FUSED, DUAL, kStreamBlock, POLICY, ContigSrc, OOP>(blk, (typename Ops::V *)e.param,
+                                                                           ContigSrc{(const char *)e.peer}, e.n, args);
 }
 
 // Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
@@ -545,12 +549,42 @@ hipError_t launch_lerp(int32_t dtype, void *param, const void *peer, int64_t n, 
     return launch_any(dtype, coef ? COEF_DEV : COEF_HOST, param, peer, n, args, s);
 }
 
+// The resident form (OOP): one-wave workgroups, the product cache policy unless 0 is forced.
+template <class Ops, int POLICY>
+static hipError_t launch_oop_policy(void *param, const void *peer, int64_t n, const LerpArgs &args, hipStream_t s,
+                                    const LaunchTiming *timing)
+{
+    const int64_t g = (n / Ops::PER) / kStreamBlock + 1;
+    if (timing)
+        hipExtLaunchKernelGGL((k_lerp<Ops, COEF_FUSED, true, kStreamBlock, POLICY, true>), dim3((uint32_t)g),
+                              dim3(kStreamBlock), 0, s, timing->start, timing->stop, 0, (typename Ops::V *)param,
+                              (const typename Ops::V *)peer, n, args);
+    else
+        hipLaunchKernelGGL((k_lerp<Ops, COEF_FUSED, true, kStreamBlock, POLICY, true>), dim3((uint32_t)g),
+                           dim3(kStreamBlock), 0, s, (typename Ops::V *)param, (const typename Ops::V *)peer, n, args);
+    return hipGetLastError();
+}
+
+template <class Ops>
+static hipError_t launch_oop(void *param, const void *peer, int64_t n, const LerpArgs &args, hipStream_t s,
+                             const LaunchTiming *timing)
+{
+    if (lerp_policy() == 0) return launch_oop_policy<Ops, 0>(param, peer, n, args, s, timing);
+    return launch_oop_policy<Ops, kProductPolicy>(param, peer, n, args, s, timing);
+}
+
 hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa, void *snap,
-                          hipStream_t s, const LaunchTiming *timing)
+                          hipStream_t s, const LaunchTiming *timing, bool oop)
 {
     LerpArgs args{};
     args.fused = fa;
     args.snap = snap;
+    if (oop) {   // resident: 16-B aligned slot payloads only
+        if (n < 0 || (!snap && n > 0) || !aligned16(param) || !aligned16(peer) || !aligned16(snap)) return hipErrorInvalidValue;
+        if (dtype == DPWA_F32) return launch_oop<OpsF32>(param, peer, n, args, s, timing);
+        if (dtype == DPWA_BF16) return launch_oop<OpsBF16>(param, peer, n, args, s, timing);
+        return hipErrorInvalidValue;
+    }
     return launch_any(dtype, COEF_FUSED, param, peer, n, args, s, timing);
 }
 
@@ -575,9 +609,9 @@ static int batch_order()
 }
 
 hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hipStream_t s,
-                                 const LaunchTiming *timing)
+                                 const LaunchTiming *timing, bool oop)
 {
-    if (b.count < 1 || b.count > kMaxAvgBatch) return hipErrorInvalidValue;
+    if (b.count < 1 || b.count > kMaxAvgBatch || (oop && !dual)) return hipErrorInvalidValue;
     AvgBatch x = b;
     uint32_t g = 0;
     const int per = dtype == DPWA_F32 ? OpsF32::PER : dtype == DPWA_BF16 ? OpsBF16::PER : 0;
@@ -598,36 +632,45 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
     size_t written = 0;
     for (int i = 0; i < x.count; ++i) {
         same = same && x.e[i].n == x.e[0].n;
-        written += (size_t)x.e[i].n * (size_t)(per == OpsF32::PER ? 4 : 2) * (dual ? 2 : 1);
+        written += (size_t)x.e[i].n * (size_t)(per == OpsF32::PER ? 4 : 2) * (dual && !oop ? 2 : 1);
     }
     const int order = batch_order();
     x.interleave = same && x.count > 1 && (order == 1 || (order < 0 && written <= kInfinityCacheBytes)) ? 1 : 0;
-#define DPWA_BATCH_LAUNCH_P(OPS, DL, P)                                                                     \
+#define DPWA_BATCH_LAUNCH_P(OPS, DL, P, OOP)                                                                \
     do {                                                                                                    \
         if (timing)                                                                                         \
-            hipExtLaunchKernelGGL((k_lerp_batch<OPS, DL, P>), dim3(g), dim3(kStreamBlock), 0, s,             \
+            hipExtLaunchKernelGGL((k_lerp_batch<OPS, DL, P, OOP>), dim3(g), dim3(kStreamBlock), 0, s,        \
                                   timing->start, timing->stop, 0, x);                                       \
         else                                                                                                \
-            hipLaunchKernelGGL((k_lerp_batch<OPS, DL, P>), dim3(g), dim3(kStreamBlock), 0, s, x);          \
+            hipLaunchKernelGGL((k_lerp_batch<OPS, DL, P, OOP>), dim3(g), dim3(kStreamBlock), 0, s, x);     \
     } while (0)
     // cache-policy variants for tuning (DPWA_LERP_POLICY, as the single-learner kernel)
 #define DPWA_BATCH_LAUNCH(OPS, DL)                                                                          \
     do {                                                                                                    \
         switch (lerp_policy()) {                                                                            \
-        case 1: DPWA_BATCH_LAUNCH_P(OPS, DL, 1); break;                                                     \
-        case 8: DPWA_BATCH_LAUNCH_P(OPS, DL, 8); break;                                                     \
-        case 9: DPWA_BATCH_LAUNCH_P(OPS, DL, 9); break;                                                     \
-        case 16: DPWA_BATCH_LAUNCH_P(OPS, DL, 16); break;                                                   \
-        default: DPWA_BATCH_LAUNCH_P(OPS, DL, 0); break;                                                    \
+        case 1: DPWA_BATCH_LAUNCH_P(OPS, DL, 1, false); break;                                              \
+        case 8: DPWA_BATCH_LAUNCH_P(OPS, DL, 8, false); break;                                              \
+        case 9: DPWA_BATCH_LAUNCH_P(OPS, DL, 9, false); break;                                              \
+        case 16: DPWA_BATCH_LAUNCH_P(OPS, DL, 16, false); break;                                            \
+        default: DPWA_BATCH_LAUNCH_P(OPS, DL, 0, false); break;                                             \
         }                                                                                                   \
     } while (0)
+    // the resident form: the product policy unless 0 is forced
+#define DPWA_BATCH_LAUNCH_OOP(OPS)                                                                          \
+    do {                                                                                                    \
+        if (lerp_policy() == 0) DPWA_BATCH_LAUNCH_P(OPS, true, 0, true);                                    \
+        else DPWA_BATCH_LAUNCH_P(OPS, true, kProductPolicy, true);                                          \
+    } while (0)
     if (dtype == DPWA_F32) {
-        if (dual) DPWA_BATCH_LAUNCH(OpsF32, true);
+        if (oop) DPWA_BATCH_LAUNCH_OOP(OpsF32);
+        else if (dual) DPWA_BATCH_LAUNCH(OpsF32, true);
         else DPWA_BATCH_LAUNCH(OpsF32, false);
     } else {
-        if (dual) DPWA_BATCH_LAUNCH(OpsBF16, true);
+        if (oop) DPWA_BATCH_LAUNCH_OOP(OpsBF16);
+        else if (dual) DPWA_BATCH_LAUNCH(OpsBF16, true);
         else DPWA_BATCH_LAUNCH(OpsBF16, false);
     }
+#undef DPWA_BATCH_LAUNCH_OOP
 #undef DPWA_BATCH_LAUNCH
 #undef DPWA_BATCH_LAUNCH_P
     return hipGetLastError();
@@ -635,35 +678,35 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
 
 __global__ void k_acquire_system();
 
-template <class Ops, bool DUAL, int POLICY>
+template <class Ops, bool DUAL, int POLICY, bool OOP>
 static void launch_relay_policy(void *param, int64_t n, const LerpArgs &args, const StripeSrc &src, hipStream_t s,
                                 const LaunchTiming *timing)
 {
     // every span of every stripe (the spans past the payload are range-checked away)
     const int64_t g = (int64_t)src.parts * (src.stripe / (kStreamBlock * 16));
     if (timing)
-        hipExtLaunchKernelGGL((k_lerp_relay<Ops, DUAL, POLICY>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s,
+        hipExtLaunchKernelGGL((k_lerp_relay<Ops, DUAL, POLICY, OOP>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s,
                               timing->start, timing->stop, 0, (typename Ops::V *)param, n, args, src);
     else
-        hipLaunchKernelGGL((k_lerp_relay<Ops, DUAL, POLICY>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s,
+        hipLaunchKernelGGL((k_lerp_relay<Ops, DUAL, POLICY, OOP>), dim3((uint32_t)g), dim3(kStreamBlock), 0, s,
                            (typename Ops::V *)param, n, args, src);
 }
 
 // the product cache policy (lerp_policy(): local parameters stored nt) or, forced to 0, the old one
-template <class Ops, bool DUAL>
+template <class Ops, bool DUAL, bool OOP = false>
 static void launch_relay_kernel(void *param, int64_t n, const LerpArgs &args, const StripeSrc &src, hipStream_t s,
                                 const LaunchTiming *timing)
 {
-    if (lerp_policy() == 8) launch_relay_policy<Ops, DUAL, 8>(param, n, args, src, s, timing);
-    else launch_relay_policy<Ops, DUAL, 0>(param, n, args, src, s, timing);
+    if (lerp_policy() == 8) launch_relay_policy<Ops, DUAL, 8, OOP>(param, n, args, src, s, timing);
+    else launch_relay_policy<Ops, DUAL, 0, OOP>(param, n, args, src, s, timing);
 }
 
 hipError_t launch_average_relay(int32_t dtype, void *param, int64_t n, const FusedArgs &fa, void *snap,
-                                const RelayArgs &a, int my_pick, hipStream_t s, const LaunchTiming *timing)
+                                const RelayArgs &a, int my_pick, hipStream_t s, const LaunchTiming *timing, bool oop)
 {
     if (n < 0 || a.world < 1 || a.world > kMaxRelayRanks || my_pick < 0 || my_pick >= a.world ||
         my_pick == a.rank || a.stripe <= 0 || a.stripe % (kStreamBlock * 16) || !aligned16(param) ||
-        (snap && !aligned16(snap)))
+        (snap && !aligned16(snap)) || (oop && !snap))
         return hipErrorInvalidValue;
     const int j = my_pick;
     StripeSrc src;
@@ -679,10 +722,12 @@ hipError_t launch_average_relay(int32_t dtype, void *param, int64_t n, const Fus
     args.snap = snap;
     hipLaunchKernelGGL(k_acquire_system, dim3(256), dim3(64), 0, s);   // remote lines in L2 are stale
     if (dtype == DPWA_F32) {
-        if (snap) launch_relay_kernel<OpsF32, true>(param, n, args, src, s, timing);
+        if (oop) launch_relay_kernel<OpsF32, true, true>(param, n, args, src, s, timing);
+        else if (snap) launch_relay_kernel<OpsF32, true>(param, n, args, src, s, timing);
         else launch_relay_kernel<OpsF32, false>(param, n, args, src, s, timing);
     } else if (dtype == DPWA_BF16) {
-        if (snap) launch_relay_kernel<OpsBF16, true>(param, n, args, src, s, timing);
+        if (oop) launch_relay_kernel<OpsBF16, true, true>(param, n, args, src, s, timing);
+        else if (snap) launch_relay_kernel<OpsBF16, true>(param, n, args, src, s, timing);
         else launch_relay_kernel<OpsBF16, false>(param, n, args, src, s, timing);
     } else {
         return hipErrorInvalidValue;

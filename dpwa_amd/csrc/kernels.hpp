@@ -49,9 +49,10 @@ struct LaunchTiming {
     hipEvent_t start, stop;
 };
 
-// Fused factor + lerp (one launch); a non-null `snap` also receives the result.
+// Fused factor + lerp (one launch); a non-null `snap` also receives the result.  `oop` (the
+// resident form): the result goes to `snap` only and `param` is read, never written.
 hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa,
-                          void *snap, hipStream_t s, const LaunchTiming *timing = nullptr);
+                          void *snap, hipStream_t s, const LaunchTiming *timing = nullptr, bool oop = false);
 
 // Several fused averages (co-resident learners) in one dispatch: entry i's workgroups follow
 // entry i-1's.  Every pointer 16-B aligned; `dual` = every entry writes through (snap non-null).
@@ -70,7 +71,7 @@ struct AvgBatch {
     AvgEntry e[kMaxAvgBatch];
 };
 hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hipStream_t s,
-                                const LaunchTiming *timing = nullptr);
+                                const LaunchTiming *timing = nullptr, bool oop = false);
 
 // Factor + clock only (one thread).
 hipError_t launch_factor(const FusedArgs &fa, hipStream_t s);
@@ -105,7 +106,8 @@ hipError_t launch_relay(int phase, const RelayArgs &a, int blocks_per_part, hipS
 // my_pick's snapshot where phase 1 left it (k_lerp_relay), preceded by a system-scope acquire.
 // The header is read from fa.hdr (my_pick's slot).  param / snap 16-B aligned.
 hipError_t launch_average_relay(int32_t dtype, void *param, int64_t n, const FusedArgs &fa, void *snap,
-                                const RelayArgs &a, int my_pick, hipStream_t s, const LaunchTiming *timing = nullptr);
+                                const RelayArgs &a, int my_pick, hipStream_t s, const LaunchTiming *timing = nullptr,
+                                bool oop = false);
 // Publish of the header only (the payload was written through by the last average).
 hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *clock, double loss,
                                  const double *loss_dev, bool loss_f32, uint64_t version, bool system_release,

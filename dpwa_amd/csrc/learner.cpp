@@ -354,6 +354,10 @@ struct dpwa_learner {
     bool wt_header = false;             // the write-through average also wrote the next header
     bool header_on_publish = false;     // never write the next header ahead (served to wire peers)
     bool reuse_guard = false;           // check a header-only publish's parameters on the device
+    // resident parameters (dpwa_learner_set_resident): they live in slot res_slot's payload and
+    // move to the other slot at every average (or relocate)
+    bool resident = false;
+    int res_slot = 0;
     const void *wt_flat = nullptr;
     hipStream_t wt_stream = nullptr;
     hipEvent_t ev_wt = nullptr;
@@ -401,6 +405,11 @@ struct dpwa_learner {
     int32_t *host_status = nullptr;     // pinned mirror of coef.status for non-blocking polls
     int32_t *host_status_dev = nullptr; // its device-side address
 };
+
+static char *slot_payload(const dpwa_learner *l, int k)
+{
+    return l->slots + (size_t)k * l->slot_stride + kPayloadOff;
+}
 
 static int64_t now_ns()
 {
@@ -613,12 +622,25 @@ static int wait_slot_readers(dpwa_learner *l, int k, hipStream_t s)
     return DPWA_OK;
 }
 
+static int relocate_impl(dpwa_learner *l, hipStream_t s);
+
 static int publish_impl(dpwa_learner *l, const void *flat, double loss, const double *loss_dev, hipStream_t s,
                         bool reuse)
 {
     l->timing_armed = false;   // armed for the last round's average, which did not happen
     const int k = (int)(l->version % 2);   // slot of publish number version+1
     char *slot = l->slots + (size_t)k * l->slot_stride;
+    if (l->resident) {
+        // the parameters are the payload already: publish the header of the slot they are in
+        // (after a publish with no average since, they first move on by one copy)
+        if (flat != slot_payload(l, l->res_slot))
+            return set_error(DPWA_ERR_ARG, "resident learner: publish the parameters where they are "
+                                           "(dpwa_learner_resident_params)");
+        int rc = relocate_impl(l, s);
+        if (rc) return rc;
+        flat = slot_payload(l, l->res_slot);
+        reuse = true;
+    }
     const bool header_only = reuse && l->wt_valid && l->wt_flat == flat;
     if (header_only && l->wt_header) {
         // payload, header and clock of this publish were written by the last average: nothing
@@ -629,7 +651,7 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
             HIP_TRY(hipEventRecord(l->ev_wt, l->wt_stream));
             HIP_TRY(hipStreamWaitEvent(s, l->ev_wt, 0));
         }
-        if (l->reuse_guard)
+        if (l->reuse_guard && !l->resident)
             HIP_TRY(launch_guard_payload(slot + kPayloadOff, flat, (int64_t)l->payload_bytes, &l->ctl->guard_dirty,
                                          &l->ctl->guard_hits, s));
         if (l->exported) HIP_TRY(launch_release_system(s));
@@ -640,12 +662,13 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
             HIP_TRY(hipEventRecord(l->ev_wt, l->wt_stream));
             HIP_TRY(hipStreamWaitEvent(s, l->ev_wt, 0));
         }
-        if (l->reuse_guard)
+        if (l->reuse_guard && !l->resident)
             HIP_TRY(launch_guard_payload(slot + kPayloadOff, flat, (int64_t)l->payload_bytes, &l->ctl->guard_dirty,
                                          &l->ctl->guard_hits, s));
         HIP_TRY(launch_publish_header(slot, l->n, l->dtype, &l->ctl->clock[l->cur], loss, loss_dev, l->loss_f32,
                                       l->version + 1, l->exported, s));
     } else {
+        if (l->resident) return set_error(DPWA_ERR_STATE, "resident learner: parameters not in the next slot");
         int rc = wait_slot_readers(l, k, s);
         if (rc) return rc;
         HIP_TRY(launch_publish(slot, flat, (int64_t)l->payload_bytes, l->n, l->dtype, &l->ctl->clock[l->cur], loss,
@@ -978,6 +1001,8 @@ int dpwa_learner_lerp(dpwa_learner *l, void *flat, dpwa_stream_t stream)
 {
     if (!l || (!flat && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_lerp: NULL argument");
     if (!l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_lerp: no factor computed for this fetch");
+    if (l->resident)
+        return set_error(DPWA_ERR_STATE, "dpwa_learner_lerp: a resident learner averages with dpwa_learner_average");
     DeviceGuard dg(l->device);
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(launch_lerp(l->dtype, flat, l->src + kPayloadOff, l->n, &l->ctl->coef, 0.f, 0.f, s));
@@ -999,6 +1024,8 @@ struct AvgPlan {
     FusedArgs fa{};
     bool relay = false;           // the relay's phase 2 fused into this average (k_lerp_relay)
     bool write_through = false;
+    bool oop = false;             // resident: the result goes to `snap` only
+    int snap_slot = -1;
 };
 
 static int average_prepare(dpwa_learner *l, void *flat, double loss, const double *loss_dev, hipStream_t s,
@@ -1006,6 +1033,13 @@ static int average_prepare(dpwa_learner *l, void *flat, double loss, const doubl
 {
     if (!l->have_fetch || l->have_factor) return set_error(DPWA_ERR_STATE, "dpwa_learner_average: no fetch in flight");
     p = AvgPlan();
+    if (l->resident) {   // read where the parameters are (the published slot), write the next slot
+        if (flat != slot_payload(l, l->res_slot))
+            return set_error(DPWA_ERR_ARG, "resident learner: average the parameters where they are "
+                                           "(dpwa_learner_resident_params)");
+        write_through = true;
+        p.oop = true;
+    }
     p.flat = flat;
     p.write_through = write_through;
     p.fa = fused_args(l, loss, loss_dev);
@@ -1013,7 +1047,8 @@ static int average_prepare(dpwa_learner *l, void *flat, double loss, const doubl
         const int k = (int)(l->version % 2);   // slot of the next publish
         int rc = wait_slot_readers(l, k, s);
         if (rc) return rc;
-        p.snap = l->slots + (size_t)k * l->slot_stride + kPayloadOff;
+        p.snap = slot_payload(l, k);
+        p.snap_slot = k;
         if (l->cfg.method != DPWA_INTERP_LOSS && !l->header_on_publish) {   // peers never read this header's loss
             p.fa.next_header = (dpwa_header *)(p.snap - kPayloadOff);
             p.fa.clock_next = &l->ctl->clock[(l->cur + 2) & 3];
@@ -1060,6 +1095,10 @@ static int average_commit(dpwa_learner *l, const AvgPlan &p, hipStream_t s)
     l->wt_header = p.fa.next_header != nullptr;
     l->wt_flat = p.flat;
     l->wt_stream = s;
+    if (p.oop) {   // the parameters moved into the next publish's slot
+        l->res_slot = p.snap_slot;
+        l->wt_flat = p.snap;
+    }
     finish_fetch(l);
     return DPWA_OK;
 }
@@ -1068,10 +1107,10 @@ static int average_launch(dpwa_learner *l, const AvgPlan &p, hipStream_t s)
 {
     if (p.relay) {
         HIP_TRY(launch_average_relay(l->dtype, p.flat, l->n, p.fa, p.snap, l->relay_saved, l->relay_saved_pick, s,
-                                     take_timing(l)));
+                                     take_timing(l), p.oop));
     } else {
         const LaunchTiming *timing = ((uintptr_t)p.flat & 15) == 0 ? take_timing(l) : nullptr;
-        HIP_TRY(launch_average(l->dtype, p.flat, p.peer, l->n, p.fa, p.snap, s, timing));
+        HIP_TRY(launch_average(l->dtype, p.flat, p.peer, l->n, p.fa, p.snap, s, timing, p.oop));
     }
     return DPWA_OK;
 }
@@ -1122,13 +1161,14 @@ static int launch_plans(dpwa_learner *const *ls, const AvgPlan *plans, const int
         add(la, pa);
         for (int c = a + 1; c < count && b.count < kMaxAvgBatch; ++c) {
             const int ic = idx[c];
-            if (done[c] || !batchable(plans[ic]) || ls[ic]->dtype != la->dtype || plans[ic].write_through != pa.write_through)
+            if (done[c] || !batchable(plans[ic]) || ls[ic]->dtype != la->dtype ||
+                plans[ic].write_through != pa.write_through || plans[ic].oop != pa.oop)
                 continue;
             if (!timing) timing = take_timing(ls[ic]);
             add(ls[ic], plans[ic]);
             done[c] = 1;
         }
-        HIP_TRY(launch_average_batch(la->dtype, pa.write_through, b, s, timing));
+        HIP_TRY(launch_average_batch(la->dtype, pa.write_through, b, s, timing, pa.oop));
     }
     return DPWA_OK;
 }
@@ -1181,21 +1221,22 @@ int dpwa_learner_average_many(dpwa_learner *const *ls, void *const *flats, const
     return DPWA_OK;
 }
 
-int dpwa_average_many(int32_t dtype, const dpwa_average_desc *descs, int count, const dpwa_interp *cfg,
-                      dpwa_stream_t stream, void *start_event, void *stop_event)
+static int average_many_impl(const char *fn, int32_t dtype, const dpwa_average_desc *descs, int count,
+                             const dpwa_interp *cfg, dpwa_stream_t stream, void *start_event, void *stop_event,
+                             bool oop)
 {
     if (count < 1 || count > kMaxAvgBatch || !descs || !cfg || dtype_size(dtype) == 0 || (!start_event) != (!stop_event))
-        return set_error(DPWA_ERR_ARG, "dpwa_average_many: bad arguments (1..%d descriptors)", kMaxAvgBatch);
-    if (cfg->method < 0 || cfg->method > 2) return set_error(DPWA_ERR_ARG, "dpwa_average_many: unknown method %d", cfg->method);
+        return set_error(DPWA_ERR_ARG, "%s: bad arguments (1..%d descriptors)", fn, kMaxAvgBatch);
+    if (cfg->method < 0 || cfg->method > 2) return set_error(DPWA_ERR_ARG, "%s: unknown method %d", fn, cfg->method);
     AvgBatch b{};
-    bool dual = false;   // an empty entry may pass no buffers at all
+    bool dual = oop;   // an empty entry may pass no buffers at all
     for (int i = 0; i < count; ++i) dual = dual || descs[i].snap_payload != nullptr;
     for (int i = 0; i < count; ++i) {
         const dpwa_average_desc &d = descs[i];
         if ((!d.param && d.n > 0) || !d.peer_slot || !d.clock_dev || !d.coef_dev || d.n < 0 ||
             (d.snap_payload == nullptr && d.n > 0 && dual) ||
             (((uintptr_t)d.param | (uintptr_t)d.peer_slot | (uintptr_t)d.snap_payload) & 15))
-            return set_error(DPWA_ERR_ARG, "dpwa_average_many: descriptor %d: NULL, unaligned or mixed write-through", i);
+            return set_error(DPWA_ERR_ARG, "%s: descriptor %d: NULL, unaligned or mixed write-through", fn, i);
         AvgEntry &e = b.e[b.count++];
         e.param = d.param;
         e.peer = (const char *)d.peer_slot + kPayloadOff;
@@ -1209,8 +1250,27 @@ int dpwa_average_many(int32_t dtype, const dpwa_average_desc *descs, int count, 
         e.fa.coef_out = d.coef_dev;
     }
     LaunchTiming t{(hipEvent_t)start_event, (hipEvent_t)stop_event};
-    HIP_TRY(launch_average_batch(dtype, dual, b, (hipStream_t)stream, start_event ? &t : nullptr));
+    if (oop && count == 1) {   // one resident average: the single kernel, as a resident learner runs it
+        const AvgEntry &e = b.e[0];
+        HIP_TRY(launch_average(dtype, e.param, e.peer, e.n, e.fa, e.snap, (hipStream_t)stream,
+                               start_event ? &t : nullptr, true));
+        return DPWA_OK;
+    }
+    HIP_TRY(launch_average_batch(dtype, dual, b, (hipStream_t)stream, start_event ? &t : nullptr, oop));
     return DPWA_OK;
+}
+
+int dpwa_average_many(int32_t dtype, const dpwa_average_desc *descs, int count, const dpwa_interp *cfg,
+                      dpwa_stream_t stream, void *start_event, void *stop_event)
+{
+    return average_many_impl("dpwa_average_many", dtype, descs, count, cfg, stream, start_event, stop_event, false);
+}
+
+int dpwa_average_many_resident(int32_t dtype, const dpwa_average_desc *descs, int count, const dpwa_interp *cfg,
+                               dpwa_stream_t stream, void *start_event, void *stop_event)
+{
+    return average_many_impl("dpwa_average_many_resident", dtype, descs, count, cfg, stream, start_event, stop_event,
+                             true);
 }
 
 int dpwa_learner_set_header_publish(dpwa_learner *l, int always)
@@ -1225,6 +1285,63 @@ int dpwa_learner_set_reuse_guard(dpwa_learner *l, int on)
     if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_set_reuse_guard: NULL learner");
     l->reuse_guard = on != 0;
     return DPWA_OK;
+}
+
+// Moves resident parameters from the published slot into the next publish's slot (a round
+// without an average; two publishes in a row).  No-op when they are there already.
+static int relocate_impl(dpwa_learner *l, hipStream_t s)
+{
+    const int k = (int)(l->version % 2);
+    if (!l->resident || l->res_slot == k) return DPWA_OK;
+    int rc = wait_slot_readers(l, k, s);
+    if (rc) return rc;
+    if (l->payload_bytes)
+        HIP_TRY(hipMemcpyAsync(slot_payload(l, k), slot_payload(l, l->res_slot), l->payload_bytes,
+                               hipMemcpyDeviceToDevice, s));
+    l->res_slot = k;
+    l->wt_valid = true;
+    l->wt_header = false;     // the publish writes the header (the clock did not move)
+    l->wt_flat = slot_payload(l, k);
+    l->wt_stream = s;
+    return DPWA_OK;
+}
+
+int dpwa_learner_set_resident(dpwa_learner *l, const void *init, dpwa_stream_t stream)
+{
+    if (!l || (!init && l->n > 0)) return set_error(DPWA_ERR_ARG, "dpwa_learner_set_resident: NULL argument");
+    if (l->resident) return set_error(DPWA_ERR_STATE, "dpwa_learner_set_resident: already resident");
+    if (l->version != 0 || l->have_fetch)
+        return set_error(DPWA_ERR_STATE, "dpwa_learner_set_resident: only before the first publish");
+    DeviceGuard dg(l->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = wait_slot_readers(l, 0, s);
+    if (rc) return rc;
+    char *dst = slot_payload(l, 0);
+    if (l->payload_bytes && dst != init)
+        HIP_TRY(hipMemcpyAsync(dst, init, l->payload_bytes, hipMemcpyDeviceToDevice, s));
+    l->resident = true;
+    l->res_slot = 0;
+    l->wt_valid = true;
+    l->wt_header = false;
+    l->wt_flat = dst;
+    l->wt_stream = s;
+    return DPWA_OK;
+}
+
+int dpwa_learner_resident_params(dpwa_learner *l, void **params, int *slot)
+{
+    if (!l || !params) return set_error(DPWA_ERR_ARG, "dpwa_learner_resident_params: NULL argument");
+    *params = l->resident ? (void *)slot_payload(l, l->res_slot) : nullptr;
+    if (slot) *slot = l->resident ? l->res_slot : -1;
+    return DPWA_OK;
+}
+
+int dpwa_learner_relocate(dpwa_learner *l, dpwa_stream_t stream)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_relocate: NULL learner");
+    if (l->have_fetch) return set_error(DPWA_ERR_STATE, "dpwa_learner_relocate: a fetch is in flight (average it)");
+    DeviceGuard dg(l->device);
+    return relocate_impl(l, (hipStream_t)stream);
 }
 
 int dpwa_learner_reuse_guard_hits(dpwa_learner *l, uint32_t *hits)

@@ -65,6 +65,15 @@ static uint64_t learner_version(dpwa_learner *l)
     return v;
 }
 
+// Slot the learner's resident parameters are in, -1 when it is not resident.
+static int resident_slot(dpwa_learner *l)
+{
+    void *p = nullptr;
+    int k = -1;
+    if (l) dpwa_learner_resident_params(l, &p, &k);
+    return k;
+}
+
 extern "C" {
 
 int dpwa_node_create(dpwa_node **out, int n_peers, const uint32_t *seed_key, int key_len, double fetch_probability,
@@ -426,6 +435,8 @@ int dpwa_node_update_wait(dpwa_node *n, double loss, const double *loss_dev, int
                           int *peer)
 {
     if (!n || !n->learner || !peer) return set_error(DPWA_ERR_STATE, "dpwa_node_update_wait: node not bound");
+    if (resident_slot(n->learner) >= 0)
+        return set_error(DPWA_ERR_STATE, "dpwa_node_update_wait: a resident node averages with update_wait_average");
     int rc = finish_fetch(n, flags, stream, peer);
     if (rc || *peer < 0) return rc;
     if ((rc = dpwa_learner_factor(n->learner, loss, loss_dev, stream))) return rc;
@@ -441,13 +452,35 @@ int dpwa_node_lerp(dpwa_node *n, void *flat, dpwa_stream_t stream)
     return rc;
 }
 
+// A resident node's round without an average: its parameters leave the published slot (one
+// copy into the next publish's slot, whose readers the board must have released first).
+static int relocate(dpwa_node *n, dpwa_stream_t stream)
+{
+    const int k = resident_slot(n->learner);
+    const uint64_t v = learner_version(n->learner);
+    if (k < 0 || (uint64_t)k == v % 2) return DPWA_OK;
+    if (n->board) {
+        const int rc = dpwa_board_publish_wait(n->board, v + 1, n->publish_timeout_ms);
+        if (rc) return rc;
+    }
+    return dpwa_learner_relocate(n->learner, stream);
+}
+
+int dpwa_node_set_resident(dpwa_node *n, const void *init, dpwa_stream_t stream)
+{
+    if (!n || !n->learner) return set_error(DPWA_ERR_STATE, "dpwa_node_set_resident: node not bound");
+    return dpwa_learner_set_resident(n->learner, init, stream);
+}
+
 int dpwa_node_update_wait_average(dpwa_node *n, void *flat, double loss, const double *loss_dev, int flags,
                                   dpwa_stream_t stream, int *peer)
 {
     if (!n || !n->learner || !peer) return set_error(DPWA_ERR_STATE, "dpwa_node_update_wait_average: node not bound");
     int rc = finish_fetch(n, flags, stream, peer);
-    if (rc || *peer < 0) return rc;
-    if (flags & DPWA_FLAG_WRITE_THROUGH) {
+    if (rc) return rc;
+    const bool resident = resident_slot(n->learner) >= 0;
+    if (*peer < 0) return resident ? relocate(n, stream) : DPWA_OK;
+    if ((flags & DPWA_FLAG_WRITE_THROUGH) || resident) {
         if (n->board) {
             // the average rewrites the slot of the NEXT publish (that of publish v-1): the
             // board's publish rule -- our publish v is visible, no live reader holds v-1 --
@@ -478,15 +511,19 @@ int dpwa_node_update_wait_average_many(dpwa_node *const *nodes, void *const *fla
         if (!n || !n->learner) return set_error(DPWA_ERR_STATE, "dpwa_node_update_wait_average_many: node %d not bound", i);
         int rc = finish_fetch(n, flags, stream, &peers[i]);   // dpwa.py:130-137, node by node
         if (rc) return rc;
-        if (peers[i] < 0) continue;
-        if (through && n->board &&
+        const bool resident = resident_slot(n->learner) >= 0;
+        if (peers[i] < 0) {
+            if (resident && (rc = relocate(n, stream))) return rc;
+            continue;
+        }
+        if ((through || resident) && n->board &&
             (rc = dpwa_board_publish_wait(n->board, learner_version(n->learner) + 1, n->publish_timeout_ms)))
             return rc;
         ls.push_back(n->learner);
         fl.push_back(flats[i]);
         lo.push_back(loss[i]);
         ld.push_back(loss_dev ? loss_dev[i] : nullptr);
-        wt.push_back(through ? 1 : 0);
+        wt.push_back(through || resident ? 1 : 0);
     }
     if (ls.empty()) return DPWA_OK;
     return dpwa_learner_average_many(ls.data(), fl.data(), lo.data(), ld.data(), wt.data(), (int)ls.size(), stream);

@@ -348,6 +348,28 @@ class DpwaConnection:
         return self._result()
 
     # ---------------------------------------------------------------- extensions
+    def make_resident(self, parameters):
+        """Resident parameters (extension, dpwa_learner_set_resident in include/dpwa_hip.h): the
+        parameters move into the learner's own snapshot slots, so a publish moves no bytes and the
+        average reads them in the published slot and writes the next one -- 3*n*s bytes a round,
+        the averaging's own.  Call before the first update_send; returns the tensor the
+        parameters are in now (see ``parameters``).  From then on pass ``conn.parameters`` to
+        update_send / update_wait_average, re-read it after every update_wait_average (it
+        alternates between the two slots), and do not write it between update_send and
+        update_wait_average (it is the served snapshot then)."""
+        learner = self._learner if self._learner is not None else self._bind(parameters)
+        stream = torch.cuda.current_stream(learner.device)
+        learner._ptr(parameters)
+        _lib.call("dpwa_node_set_resident", self._node, ctypes.c_void_p(parameters.data_ptr()),
+                  ctypes.c_void_p(stream.cuda_stream))
+        return learner.resident_params()
+
+    @property
+    def parameters(self):
+        """The resident parameters' tensor now (None unless ``make_resident`` was called): a view
+        of one of the learner's snapshot slots, valid until ``close``."""
+        return self._learner.resident_params() if self._learner is not None else None
+
     @staticmethod
     def update_wait_average_many(conns, parameters, losses, write_through=False):
         """update_wait_average of several connections of this process (the learners of a
@@ -452,6 +474,8 @@ class DpwaConnection:
         return self._peer_node_index[k]
 
     def close(self):
+        """Shuts the node down; tensors from ``make_resident`` / ``parameters`` must not be used
+        afterwards (their memory is the learner's)."""
         group = getattr(self, "_group", None)
         if group is not None:
             group.leave(self)

@@ -49,6 +49,27 @@ class FlatParameters:
             p.data = self.buffer[o:o + p.numel()].view(p.shape)
             self._ptrs.append(p.data_ptr())
 
+    def rehome(self, buffer):
+        """Re-points every parameter into `buffer`, a tensor of this layout that already holds
+        the values (a resident learner's slot, which alternates between two: their views are
+        built once, so a move costs one ``.data`` assignment per parameter)."""
+        if buffer is self.buffer:
+            return
+        if buffer.numel() != self.numel or buffer.dtype != self.dtype or buffer.device != self.device:
+            raise ValueError("rehome: a %s buffer of %d elements on %s is needed" % (self.dtype, self.numel,
+                                                                                     self.device))
+        cache = self.__dict__.setdefault("_homes", {})
+        key = buffer.data_ptr()
+        views = cache.get(key)
+        if views is None:
+            if len(cache) >= 2:
+                cache.clear()
+            views = cache[key] = [buffer[o:o + p.numel()].view(p.shape) for p, o in zip(self.params, self.offsets)]
+        self.buffer = buffer
+        for p, v in zip(self.params, views):
+            p.data = v
+        self._ptrs = [v.data_ptr() for v in views]
+
     def resync(self):
         """Re-homes parameters whose ``.data`` was replaced since the last call (e.g. a
         user assigned ``param.data = ...``); returns the number re-homed."""

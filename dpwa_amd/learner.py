@@ -56,12 +56,17 @@ class Learner:
         self.version = 0                 # publishes so far (mirrors dpwa_learner_version)
         self._keep = None
         self._loss_dtype = _lib.F64      # what device loss pointers point at (native side)
-        self._checked = None             # (id, data_ptr, numel, dtype) of the last validated tensor
+        self._checked = (None, None)     # (id, data_ptr, numel, dtype) of the last two validated tensors
         self._f_publish = lib.dpwa_learner_publish
         self._f_fetch = lib.dpwa_learner_fetch
         self._f_average = lib.dpwa_learner_average
         self._f_factor = lib.dpwa_learner_factor
         self._f_lerp = lib.dpwa_learner_lerp
+        # resident parameters: where they are, read once per round
+        self._f_resident = lib.dpwa_learner_resident_params
+        self._res_ptr, self._res_slot = ctypes.c_void_p(), ctypes.c_int()
+        self._res_args = (ctypes.byref(self._res_ptr), ctypes.byref(self._res_slot))
+        self._res_views = {}             # slot payload address -> tensor over it (two at most)
 
     @property
     def handle(self):
@@ -100,13 +105,14 @@ class Learner:
             raise ValueError("expected a %s tensor on %s, got %s" % (self.dtype, self.device, type(t).__name__))
         # id and address alone can repeat for a new tensor (a freed one's id, the caching
         # allocator's block): size and dtype are part of the key, so such a tensor is checked
+        # (the last two keys: resident parameters alternate between two tensors)
         key = (id(t), t.data_ptr(), t.numel(), t.dtype)
-        if key != self._checked:
+        if key not in self._checked:
             if t.device != self.device or t.dtype != self.dtype:
                 raise ValueError("expected a %s tensor on %s" % (self.dtype, self.device))
             if not t.is_contiguous() or t.numel() != self.numel:
                 raise ValueError("expected a contiguous tensor of %d elements, got %s" % (self.numel, tuple(t.shape)))
-            self._checked = key
+            self._checked = (self._checked[-1], key)
         return key[1]
 
     def _fail(self, name, rc):
@@ -119,6 +125,26 @@ class Learner:
         if rc:
             self._fail("dpwa_learner_publish", rc)
         self.version += 1
+
+    def set_resident(self, init, stream):
+        """dpwa_learner_set_resident: the parameters move into slot 0 (before the first publish)."""
+        _lib.call("dpwa_learner_set_resident", self._h, self._ptr(init), stream.cuda_stream)
+        return self.resident_params()
+
+    def resident_params(self):
+        """The tensor over the slot the resident parameters are in now (None when the learner is
+        not resident); it changes at every average."""
+        rc = self._f_resident(self._h, *self._res_args)
+        if rc:
+            self._fail("dpwa_learner_resident_params", rc)
+        ptr = self._res_ptr.value
+        if not ptr:
+            return None
+        t = self._res_views.get(ptr)
+        if t is None:
+            from .devview import device_tensor
+            t = self._res_views[ptr] = device_tensor(ptr, self.numel, self.dtype, self.device)
+        return t
 
     def native_version(self):
         """dpwa_learner_version: publishes issued so far (no device sync)."""

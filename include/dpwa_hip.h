@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DPWA_ABI_VERSION 5
+#define DPWA_ABI_VERSION 6
 
 #define DPWA_OK 0
 #define DPWA_ERR_ARG (-1)     /* bad argument (API misuse)                          */
@@ -135,6 +135,11 @@ typedef struct dpwa_average_desc {
 } dpwa_average_desc;
 int dpwa_average_many(int32_t dtype, const dpwa_average_desc *descs, int count, const dpwa_interp *cfg,
                       dpwa_stream_t stream, void *start_event, void *stop_event);
+/* The same in the resident form (dpwa_learner_set_resident below): each `param` is read only and the
+ * result goes to its snap_payload (required for n > 0) -- 3*n*s bytes per descriptor.  One
+ * descriptor runs the single-learner kernel, several the batched one. */
+int dpwa_average_many_resident(int32_t dtype, const dpwa_average_desc *descs, int count, const dpwa_interp *cfg,
+                               dpwa_stream_t stream, void *start_event, void *stop_event);
 
 /* Factor + clock on the device (dpwa.py:139-155 + interpolation.py): reads *clock_dev and the
  * peer's header, writes *coef_dev and, unless the status is an error, *clock_dev = new_clock.
@@ -242,6 +247,27 @@ int dpwa_learner_publish_reuse(dpwa_learner *l, const void *flat, double loss, c
  * reuse_guard_hits: how many publishes found a difference (synchronises the device). */
 int dpwa_learner_set_reuse_guard(dpwa_learner *l, int on);
 int dpwa_learner_reuse_guard_hits(dpwa_learner *l, uint32_t *hits);
+
+/* Resident parameters (extension; replaces the snapshot copy of pytorch.py:49-53 and
+ * RxThread.set_current_state, conn.py:73-79, with no copy at all).  The learner's parameters live
+ * in its own two snapshot slots and move between them: a publish writes only the header of the
+ * slot they are in, and the average reads them there -- the published snapshot, which it leaves
+ * untouched -- and stores the result into the other slot, the slot of the next publish.  A round
+ * then moves 3*n*s bytes, the averaging's own (write-through: 4*n*s; publish + in-place average:
+ * 5*n*s), with the same results.
+ *   set_resident      before the first publish: copy `init` (n elements) into slot 0.
+ *   resident_params   where the parameters are now (*params NULL and *slot -1 when not resident):
+ *                     a device pointer valid for the learner's life, which changes at every
+ *                     average -- re-read it after each one.
+ *   relocate          a round without an average: the parameters leave the published slot by one
+ *                     copy into the next publish's slot (no-op when they are there).
+ * Contract: the parameters ARE the served snapshot between a publish and the next average or
+ * relocate, so they must not be written in that window (the reference's loop does not:
+ * update_send, update_wait, then the training step).  A publish is given the resident pointer;
+ * the split factor/lerp form is refused. */
+int dpwa_learner_set_resident(dpwa_learner *l, const void *init, dpwa_stream_t stream);
+int dpwa_learner_resident_params(dpwa_learner *l, void **params, int *slot);
+int dpwa_learner_relocate(dpwa_learner *l, dpwa_stream_t stream);
 
 /* Split form of dpwa_learner_average for the DpwaConnection / adapter seam:
  * factor only (update_wait's return value), then lerp with the learner's coefficients. */
@@ -473,6 +499,11 @@ int dpwa_node_update_wait_average(dpwa_node *n, void *flat, double loss, const d
 int dpwa_node_update_wait_average_many(dpwa_node *const *nodes, void *const *flats, const double *loss,
                                        const double *const *loss_dev, int count, int flags,
                                        dpwa_stream_t stream, int *peers);
+/* Resident parameters for the node's learner (dpwa_learner_set_resident; bound, before the first
+ * publish).  A resident node's update_wait_average always averages in the resident form (flat =
+ * dpwa_learner_resident_params before the call) and relocates the parameters in a round without
+ * an average; its split update_wait is refused. */
+int dpwa_node_set_resident(dpwa_node *n, const void *init, dpwa_stream_t stream);
 /* State of the current/last round: fetching flag, fetched peer (-1: none), its publish
  * number, and the picks the last fetch took. */
 int dpwa_node_info(const dpwa_node *n, int *fetching, int *fetch_peer, uint64_t *fetch_version,

@@ -22,9 +22,12 @@ def add_bf16(param_u16, delta_u16):
 
 
 def simulate(names, init, deltas, send_loss, wait_loss, method, value, threshold, fetch_probability,
-             seeds, lerp=lerp_f32, add=None):
+             seeds, lerp=lerp_f32, add=None, train_after_wait=False):
     """init (G, n) and deltas (T, G, n): fp32 arrays, or raw bf16 bits (uint16) with
-    lerp=lerp_bf16, add=add_bf16."""
+    lerp=lerp_bf16, add=add_bf16.  train_after_wait: round r's training delta is applied after
+    its update_wait instead of between update_send and update_wait (the order a loop with
+    resident parameters must keep: update_send, update_wait, training step); out_params then
+    holds the parameters after the average, before that delta."""
     G, n = init.shape
     T = deltas.shape[0]
     learners = [OracleLearner(names[g], [x for x in names if x != names[g]], fetch_probability,
@@ -41,9 +44,12 @@ def simulate(names, init, deltas, send_loss, wait_loss, method, value, threshold
             states.append(learners[g].update_send(send_loss[r][g]))
             snaps.append(params[g].copy())
             fetching[r, g] = learners[g].fetching
-        for g in range(G):
-            params[g] = (np.add(params[g], deltas[r, g], dtype=params.dtype) if add is None
-                         else add(params[g], deltas[r, g]))
+        def train():
+            for g in range(G):
+                params[g] = (np.add(params[g], deltas[r, g], dtype=params.dtype) if add is None
+                             else add(params[g], deltas[r, g]))
+        if not train_after_wait:
+            train()
         for g in range(G):
             L = learners[g]
             state, payload, attempts = None, None, []
@@ -59,4 +65,6 @@ def simulate(names, init, deltas, send_loss, wait_loss, method, value, threshold
             factors[r, g] = factor
             clocks[r, g] = L.clock
             out_params[r, g] = params[g]
+        if train_after_wait:
+            train()
     return {"params": out_params, "clocks": clocks, "factors": factors, "fetching": fetching, "picks": picks}

@@ -29,13 +29,19 @@ def test_parity_transports_cover_every_trial_and_the_fd_shared_path():
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
     import bench
-    assert bench.parity_transports(1) == ["local"]
+    assert bench.parity_transports(1) == ["local", "local+res"]
     t = bench.parity_transports(8)
     assert "lockstep/relay-avg:32+vmm" in t and "async/copy+vmm" in t
+    assert "lockstep/relay-avg:32+res+vmm" in t and "async/copy+res+vmm" in t
     lockstep = ["copy", "kernel:256", "kernel:1024", "relay:32", "relay:128", "relay:512", "relay-avg:32",
                 "relay-avg:128", "relay-avg:512"]
     trials = lockstep + ["async/%s%s" % (m, wt) for m in lockstep if not m.startswith("relay") for wt in ("", "+wt")]
+    # resident learners (the default publish form): "+res" trial keys, vouched for by "+res" transports
+    trials += [m + "+res" for m in lockstep] + ["async/%s+res" % m for m in lockstep if not m.startswith("relay")]
     assert {bench.parity_key(k) for k in trials} <= set(t)
+    assert bench.parity_key("relay-avg:512+res") == "lockstep/relay-avg:32+res"
+    assert bench.parity_key("async/kernel:1024+res") == "async/kernel:256+res"
+    assert bench.trial_mode("relay-avg:128+res") == "relay-avg:128" and bench.trial_mode("async/copy+wt") == "copy"
     assert all(x.startswith("async/") for x in bench.parity_transports(4, "async"))
     assert all(x.startswith("lockstep/") for x in bench.parity_transports(4, "lockstep"))
 

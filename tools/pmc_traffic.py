@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--numel", type=int, default=11_173_962)
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--publish", choices=["full", "write-through"], default="full",
+    ap.add_argument("--publish", choices=["full", "write-through", "resident"], default="full",
                     help="write-through: the kernel also writes the next snapshot (4*N*s algorithmic bytes)")
     ap.add_argument("--learners", type=int, default=1, help="averages per dispatch (k_lerp_batch)")
     ap.add_argument("--basis", choices=["cold", "in-loop"], default="cold",
