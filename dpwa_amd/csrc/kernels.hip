@@ -565,12 +565,19 @@ static hipError_t launch_oop_policy(void *param, const void *peer, int64_t n, co
     return hipGetLastError();
 }
 
+// (the resident kernel stores only the next slot, so its store policy is the snapshot one: bit 16
+// makes it `nt`, bit 1 loads the parameters with the default policy; tuning variants)
 template <class Ops>
 static hipError_t launch_oop(void *param, const void *peer, int64_t n, const LerpArgs &args, hipStream_t s,
                              const LaunchTiming *timing)
 {
-    if (lerp_policy() == 0) return launch_oop_policy<Ops, 0>(param, peer, n, args, s, timing);
-    return launch_oop_policy<Ops, kProductPolicy>(param, peer, n, args, s, timing);
+    switch (lerp_policy()) {
+    case 0: return launch_oop_policy<Ops, 0>(param, peer, n, args, s, timing);
+    case 1: return launch_oop_policy<Ops, 1>(param, peer, n, args, s, timing);
+    case 16: return launch_oop_policy<Ops, 16>(param, peer, n, args, s, timing);
+    case 17: return launch_oop_policy<Ops, 17>(param, peer, n, args, s, timing);
+    default: return launch_oop_policy<Ops, kProductPolicy>(param, peer, n, args, s, timing);
+    }
 }
 
 hipError_t launch_average(int32_t dtype, void *param, const void *peer, int64_t n, const FusedArgs &fa, void *snap,
@@ -658,8 +665,13 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
     // the resident form: the product policy unless 0 is forced
 #define DPWA_BATCH_LAUNCH_OOP(OPS)                                                                          \
     do {                                                                                                    \
-        if (lerp_policy() == 0) DPWA_BATCH_LAUNCH_P(OPS, true, 0, true);                                    \
-        else DPWA_BATCH_LAUNCH_P(OPS, true, kProductPolicy, true);                                          \
+        switch (lerp_policy()) {                                                                            \
+        case 0: DPWA_BATCH_LAUNCH_P(OPS, true, 0, true); break;                                             \
+        case 1: DPWA_BATCH_LAUNCH_P(OPS, true, 1, true); break;                                             \
+        case 16: DPWA_BATCH_LAUNCH_P(OPS, true, 16, true); break;                                           \
+        case 17: DPWA_BATCH_LAUNCH_P(OPS, true, 17, true); break;                                           \
+        default: DPWA_BATCH_LAUNCH_P(OPS, true, kProductPolicy, true); break;                               \
+        }                                                                                                   \
     } while (0)
     if (dtype == DPWA_F32) {
         if (oop) DPWA_BATCH_LAUNCH_OOP(OpsF32);

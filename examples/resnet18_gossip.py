@@ -70,6 +70,11 @@ def main(argv=None):
                          "(the relays need --gossip lockstep)")
     ap.add_argument("--no-batch-wait", dest="batch_wait", action="store_false",
                     help="co-resident learners: one update_wait per adapter instead of update_wait_many")
+    ap.add_argument("--resident", action="store_true",
+                    help="resident parameters (the adapter's resident=True): the loop runs update_send, "
+                         "update_wait, then the training step -- nothing may write the parameters between "
+                         "update_send and update_wait in this form -- instead of the reference's update_send, "
+                         "step, update_wait")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,21 +115,26 @@ def main(argv=None):
             if gossip:
                 for i, a in enumerate(adapters):
                     a.update_send(losses[i])       # a device tensor: no host sync
-            for i in range(len(mine)):
-                losses[i] = train_step(i)
+            if not args.resident:                  # the reference's order (README.md:18-29)
+                for i in range(len(mine)):
+                    losses[i] = train_step(i)
             if gossip:
                 if len(adapters) > 1 and args.batch_wait:    # co-resident: one averaging dispatch
                     DpwaPyTorchAdapter.update_wait_many(adapters, losses)
                 else:
                     for i, a in enumerate(adapters):
                         a.update_wait(losses[i])
+            if args.resident:                      # resident parameters: the step after update_wait
+                for i in range(len(mine)):
+                    losses[i] = train_step(i)
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
     group = {"group": args.gossip} if world > 1 else {}
     if world > 1 and args.pull:
         group["pull"] = args.pull
-    adapters = [DpwaPyTorchAdapter(nets[i], names[g], cfg, seed=100 + g, **group) for i, g in enumerate(mine)]
+    adapters = [DpwaPyTorchAdapter(nets[i], names[g], cfg, seed=100 + g, resident=args.resident, **group)
+                for i, g in enumerate(mine)]
     run(args.warmup, False)
     run(args.warmup, True, adapters)
     # interleaved phases, the first pair discarded: a run's first phase executes at a higher
@@ -147,6 +157,7 @@ def main(argv=None):
             "train_steps_per_s_per_learner_gossip": round(args.steps / t_gossip, 1),
             "gossip_overhead_pct": round(100 * (t_gossip - t_plain) / t_plain, 2),
             "batched_wait": bool(args.batch_wait and len(adapters) > 1),
+            "resident": bool(args.resident),
             "final_clock": adapters[0].connection.clock,
         }))
     for a in adapters:

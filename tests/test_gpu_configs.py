@@ -218,6 +218,59 @@ def test_gpu_key_moves_the_model_onto_its_device(tmp_path):
         a.connection.close()
 
 
+def test_configs0_resnet18_resident_training(tmp_path):
+    """configs[0]'s four ResNet-18 learners with resident parameters (the adapter's resident=True,
+    62 parameters re-pointed into the slots every round), the resident loop order: update_send,
+    update_wait, then the training step (SGD with momentum and weight decay).  Every average is the
+    oracle lerp of the learner's published parameters with its peer's (constant 0.5, divergence
+    threshold 0.5 crossed from round 3), the peers and clocks are the oracle's, and the optimizer
+    keeps training the re-pointed parameters."""
+    G, T = 4, 6
+    names = ["w%d" % (g + 1) for g in range(G)]
+    cfg = tmp_path / "c0r.yaml"
+    write_cfg(cfg, names, 1, "constant", 0.5, 0.5)
+    torch.manual_seed(0)
+    nets = [resnet18().to(DEV) for _ in range(G)]
+    opts = [torch.optim.SGD(n.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4) for n in nets]
+    group = LocalGroup()
+    adapters = [DpwaPyTorchAdapter(nets[g], names[g], str(cfg), seed=100 + g, group=group, resident=True)
+                for g in range(G)]
+    L = [OracleLearner(names[g], [x for x in names if x != names[g]], 1, "constant", 0.5, 0.5, 100 + g)
+         for g in range(G)]
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    send = [2.3] * G
+    homes = [set() for _ in range(G)]
+    for r in range(T):
+        for g in range(G):
+            adapters[g].update_send(send[g])
+        snaps = [a.flat.buffer.cpu().numpy() for a in adapters]         # what each learner published
+        wait = [s * (0.1 if r >= 3 else 1.0) for s in send]
+        DpwaPyTorchAdapter.update_wait_many(adapters, wait)
+        exp = oracle_round(L, send, wait, names)
+        for g in range(G):
+            q, factor = exp[g]
+            got = torch.cat([p.detach().reshape(-1) for p in nets[g].parameters()]).cpu().numpy()
+            want = olerp.lerp_f32(snaps[g], snaps[q], factor)
+            flat = adapters[g].flat
+            want = np.concatenate([want[o:o + p.numel()] for p, o in zip(flat.params, flat.offsets)])
+            assert adapters[g].connection.last_fetch_peer == names[q], (r, g)
+            assert olerp.bits_equal(got, want), (r, g)
+            assert adapters[g].connection.clock == L[g].clock, (r, g)
+            homes[g].add(adapters[g].flat.buffer.data_ptr())
+        send = []
+        for g in range(G):                                               # the step, after update_wait
+            x = torch.randn(8, 3, 32, 32, device=DEV, generator=gen)
+            y = torch.randint(0, 10, (8,), device=DEV, generator=gen)
+            opts[g].zero_grad(set_to_none=True)
+            loss = F.cross_entropy(nets[g](x), y)
+            loss.backward()
+            opts[g].step()
+            send.append(loss.item())
+    assert all(len(h) == 2 for h in homes)
+    for a in adapters:
+        a.connection.close()
+
+
 def test_resnet18_example_runs(capsys):
     """f1: examples/resnet18_gossip.py (the reference trainer's loop, main.py:122-158) runs end
     to end with gossip every step; the clock advanced every round (fetch_probability 1)."""
@@ -226,10 +279,11 @@ def test_resnet18_example_runs(capsys):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples"))
     import resnet18_gossip
-    resnet18_gossip.main(["--learners", "2", "--steps", "4", "--warmup", "2", "--batch-size", "8"])
-    out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
-    assert out["learners"] == 2 and out["final_clock"] == 2 + 3 * 4   # warmup + three gossip phases
-    assert out["train_steps_per_s_per_learner_gossip"] > 0
+    for extra in ([], ["--resident"]):
+        resnet18_gossip.main(["--learners", "2", "--steps", "4", "--warmup", "2", "--batch-size", "8"] + extra)
+        out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+        assert out["learners"] == 2 and out["final_clock"] == 2 + 3 * 4   # warmup + three gossip phases
+        assert out["train_steps_per_s_per_learner_gossip"] > 0 and out["resident"] == bool(extra)
 
 
 @pytest.mark.parametrize("group", ["lockstep", "async"])

@@ -15,7 +15,6 @@ from dpwa_amd import DpwaConnection, DpwaPyTorchAdapter, _lib
 from dpwa_amd.group import LocalGroup
 from oracle import gossip as ogossip
 from oracle import lerp as olerp
-from tests.test_gpu_gossip import Net
 from tests.test_gpu_kernels import from_u16, to_u16
 
 pytestmark = pytest.mark.gpu
@@ -185,14 +184,14 @@ def test_resident_adapter_matches_write_through(tmp_path, many):
     step (SGD with momentum) after every update_wait, gives bit for bit the parameters and clocks
     of the write-through adapter; the parameters are re-pointed into the slots every round and
     the optimizer keeps working on them."""
-    shapes = [(64, 3, 3, 3), (64,), (10, 64), (10,), (7, 5)]
     names = ["a0", "a1", "a2"]
     cfg = tmp_path / "ad.yaml"
     _write_cfg(cfg, names, 0.8, "clock")
     results = {}
     for mode in ("resident", "write_through"):
         torch.manual_seed(5)
-        nets = [Net(shapes).to(DEV) for _ in names]
+        nets = [torch.nn.Sequential(torch.nn.Linear(7, 33), torch.nn.Tanh(), torch.nn.Linear(33, 5)).to(DEV)
+                for _ in names]
         grp = LocalGroup()
         ads = [DpwaPyTorchAdapter(nets[g], names[g], str(cfg), seed=40 + g, group=grp,
                                   resident=mode == "resident") for g in range(3)]
