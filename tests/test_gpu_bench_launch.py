@@ -35,15 +35,18 @@ def test_self_launched_two_ranks_print_one_line():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0
     parity = {k: v for k, v in out["parity"].items() if k != "workload"}
-    assert len(parity) == 10 and all(parity.values()), parity
+    sys.path.insert(0, ROOT)
+    import bench
+    assert set(parity) == set(bench.parity_transports(2)) and all(parity.values()), parity
     assert out["parity_of_timed_transport"]["ok"]
 
 
 def test_injected_transport_failure_is_isolated():
-    rc, lines, err = _bench({"DPWA_BENCH_INJECT": "lockstep/kernel:256@1:end"})
+    # the timed rounds run resident learners (the default publish form): their transport fails
+    rc, lines, err = _bench({"DPWA_BENCH_INJECT": "lockstep/kernel:256+res@1:end"})
     assert rc == 1, err[-3000:]
     assert len(lines) == 1, lines
     out = json.loads(lines[0])
-    assert out["parity"]["lockstep/kernel:256"] is False
-    assert all(v for k, v in out["parity"].items() if k not in ("workload", "lockstep/kernel:256"))
+    assert out["parity"]["lockstep/kernel:256+res"] is False
+    assert all(v for k, v in out["parity"].items() if k not in ("workload", "lockstep/kernel:256+res"))
     assert out["value"] > 0 and not any(k.startswith("kernel") for k in out["pull_trials_gbs"])
