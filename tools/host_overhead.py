@@ -3,7 +3,9 @@
 host-bound training loop pays on the CPU): two learners in one process, a ResNet-18-shaped
 parameter list (62 tensors) scaled down so the GPU work is negligible, timed per call with
 time.perf_counter over many rounds.  Prints one JSON line (microseconds per call and learner;
-connection_batched: both learners' update_wait in one update_wait_average_many call)."""
+connection_batched: both learners' update_wait in one update_wait_average_many call; the
+_resident modes: resident learners -- the adapter re-points its 62 parameters every round, the
+connection re-reads conn.parameters)."""
 import json
 import os
 import sys
@@ -31,14 +33,32 @@ def main(rounds=2000):
                 self.register_parameter("p%d" % i, torch.nn.Parameter(torch.zeros(min(64, int(torch.tensor(s).prod())))))
 
     out = {}
-    for mode in ("adapter", "connection", "connection_batched"):
+    for mode in ("adapter", "connection", "connection_batched", "adapter_resident", "adapter_resident_batched",
+                 "connection_batched_resident"):
         group = LocalGroup()
-        if mode == "adapter":
+        if mode.startswith("adapter"):
             nets = [Net().to(dev), Net().to(dev)]
-            ads = [DpwaPyTorchAdapter(n, nm, cfg, seed=i, group=group) for i, (n, nm) in enumerate(zip(nets, "ab"))]
+            ads = [DpwaPyTorchAdapter(n, nm, cfg, seed=i, group=group, resident="resident" in mode)
+                   for i, (n, nm) in enumerate(zip(nets, "ab"))]
             send = [a.update_send for a in ads]
             wait = [a.update_wait for a in ads]
+            if mode.endswith("batched"):
+                wait = [lambda l: DpwaPyTorchAdapter.update_wait_many(ads, [l, l])]
             conns = [a.connection for a in ads]
+        elif mode == "connection_batched_resident":
+            conns = [DpwaConnection(nm, cfg, seed=i, group=group) for i, nm in enumerate("ab")]
+            for i, c in enumerate(conns):
+                c.make_resident(torch.full((4096,), float(i), device=dev))
+            cur = [c.parameters for c in conns]
+
+            def _send(l, i):
+                conns[i].update_send(cur[i], l)
+
+            def _wait(l):
+                DpwaConnection.update_wait_average_many(conns, cur, [l, l])
+                cur[:] = [c.parameters for c in conns]
+            send = [lambda l: _send(l, 0), lambda l: _send(l, 1)]
+            wait = [_wait]
         else:
             flats = [torch.zeros(4096, device=dev), torch.ones(4096, device=dev)]
             conns = [DpwaConnection(nm, cfg, seed=i, group=group) for i, nm in enumerate("ab")]
