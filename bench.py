@@ -25,8 +25,8 @@ fetch_probability 1.
 averaging) summed over all learners / the max-over-ranks wall time of the
 K timed steps, from a pass with no instrumentation.  ``roofline`` prices the averaging
 kernel alone, cold, per launch (dispatch begin/end events); ``roofline.in_loop`` times the same
-kernel inside the gossip loop in a separate sampled pass.  ``parity`` (at N>1 before the
-trials, so only verified transports are timed) checks every transport bit for bit against the
+kernel inside the gossip loop in a separate sampled pass.  ``parity`` (before the timed
+rounds; at N>1 before the trials, so only verified transports are timed) checks every transport bit for bit against the
 oracle, each transport isolated (an error becomes ``false``, not a teardown), with a watchdog
 that prints a partial line and exits non-zero if a phase overruns.  ``cpu_baseline`` times the
 reference's own CPU round restated (oracle/ref_round.py: two learner processes on localhost
@@ -1121,11 +1121,12 @@ def main(argv=None):
         write_config(cfg, names, args.interpolation, args.fetch_probability, args.divergence_threshold)
         mine = [(names[rank], rank)]
 
-    # At N>1 the parity leg runs first: a transport that fails it on this node's devices is
+    # The parity leg runs first: at N>1 a transport that fails it on this node's devices is
     # reported (parity: false) and left out of the trials, so the timed run always uses a
-    # transport whose results matched the oracle.
+    # transport whose results matched the oracle; at N=1 it checks both local forms (and gives
+    # the GPU a second of work between the CPU baseline and the timed rounds).
     parity = None
-    if world > 1 and not args.no_parity:
+    if not args.no_parity:
         parity = parity_leg(world, rank, local_rank, device, tmp, parity_transports(world, args.gossip),
                             args.dist_backend, ctl=ctl, watchdog=wd)
 
@@ -1525,8 +1526,6 @@ def main(argv=None):
         if o_trials:
             overlap["trials_ms_per_step"] = {m: round(1e3 * t / o_steps, 4) for m, t in o_trials.items()}
 
-    if world == 1 and not args.no_parity:      # one transport (local): checked after the timed region
-        parity = parity_leg(1, 0, 0, device, tmp, parity_transports(1), args.dist_backend, watchdog=wd)
     if parity is not None:
         parity["workload"] = ("%d-element fp32 vector per learner, %d lock-step rounds (clock interpolation, "
                               "fetch_probability %g, seeded training-step deltas, write-through and split rounds "
