@@ -1601,6 +1601,15 @@ def main(argv=None):
                 "learners_per_gpu": len(mine),
                 "numel": args.numel,
                 "publish": variant,
+                "publish_note": ("resident: each learner's parameters live in its two snapshot slots; the average "
+                                 "reads the published slot and writes the other (3*N*s), the publish moves nothing. "
+                                 "Valid for rounds that write nothing to the parameters between update_send and "
+                                 "update_wait, as these synthetic rounds (no training step); the reference's own loop "
+                                 "trains in that window and needs the write-through form (at N=1 timed in "
+                                 "secondary_publish; --publish write-through times it as the main run)"
+                                 if resident_main else
+                                 "write-through: the average also writes the next snapshot (4*N*s)" if wt_main else
+                                 "full: every publish copies the 2*N*s snapshot"),
                 "averaging_dispatch": ("one batched dispatch per round for the %d co-resident learners" % per_launch
                                        if per_launch > 1 else "one dispatch per learner per round"),
                 "transport": "in-place HBM read (co-resident peer)" if world == 1 else
