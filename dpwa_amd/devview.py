@@ -3,9 +3,11 @@
 The resident form keeps a learner's parameters in its own snapshot slots
 (``dpwa_learner_set_resident``, include/dpwa_hip.h); the training loop needs them as a torch
 tensor.  ``device_tensor`` wraps a device pointer through DLPack (``torch.from_dlpack`` of a
-``dltensor`` capsule built here with ctypes): no copy, no allocation, and torch never frees the
-memory -- the capsule's deleter only drops this module's reference to the descriptor.  The
-tensor must not outlive the learner that owns the memory.
+``dltensor`` capsule built here with ctypes): no copy, and torch never frees the memory -- the
+descriptor has no deleter.  Each descriptor (80 bytes) lives in malloc'd memory that is never
+freed, so torch may read it whenever it lets go of the tensor, interpreter shutdown included,
+without calling back into Python (a learner makes two such views for its life).  The tensor
+must not outlive the learner that owns the memory.
 """
 import ctypes
 
@@ -38,13 +40,11 @@ _DELETER = ctypes.CFUNCTYPE(None, ctypes.POINTER(DLManagedTensor))
 DLManagedTensor._fields_ = [("dl_tensor", DLTensor), ("manager_ctx", ctypes.c_void_p), ("deleter", _DELETER)]
 
 _DTYPES = {torch.float32: (_KDL_FLOAT, 32), torch.bfloat16: (_KDL_BFLOAT, 16), torch.uint8: (1, 8)}
-_live = {}                # address of a DLManagedTensor -> (struct, shape array): kept until torch lets go
-
-
-@_DELETER
-def _release(managed):
-    _live.pop(ctypes.addressof(managed.contents), None)
-
+_libc = ctypes.CDLL(None)
+_libc.malloc.restype = ctypes.c_void_p
+_libc.malloc.argtypes = [ctypes.c_size_t]
+_DESC_BYTES = ctypes.sizeof(DLManagedTensor) + ctypes.sizeof(ctypes.c_int64)
+made = [0]                # descriptors made (never freed)
 
 _capsule_new = ctypes.pythonapi.PyCapsule_New
 _capsule_new.restype = ctypes.py_object
@@ -59,12 +59,16 @@ def device_tensor(ptr, numel, dtype, device, device_type=KDL_ROCM):
     if not ptr and numel:
         raise ValueError("device_tensor: NULL pointer")
     index = device.index if isinstance(device, torch.device) else int(device)
-    shape = (ctypes.c_int64 * 1)(int(numel))
-    m = DLManagedTensor()
+    addr = _libc.malloc(_DESC_BYTES)
+    if not addr:
+        raise MemoryError("device_tensor: no memory for a DLPack descriptor")
+    shape = ctypes.c_int64.from_address(addr + ctypes.sizeof(DLManagedTensor))
+    shape.value = int(numel)
+    m = DLManagedTensor.from_address(addr)
     code, bits = _DTYPES[dtype]
     m.dl_tensor = DLTensor(ctypes.c_void_p(ptr), DLDevice(device_type, index or 0), 1, DLDataType(code, bits, 1),
-                           shape, None, 0)
+                           ctypes.pointer(shape), None, 0)
     m.manager_ctx = None
-    m.deleter = _release
-    _live[ctypes.addressof(m)] = (m, shape)
-    return torch.utils.dlpack.from_dlpack(_capsule_new(ctypes.addressof(m), b"dltensor", None))
+    m.deleter = _DELETER()          # NULL: torch frees nothing and calls nothing
+    made[0] += 1
+    return torch.utils.dlpack.from_dlpack(_capsule_new(addr, b"dltensor", None))

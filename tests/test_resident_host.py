@@ -13,7 +13,7 @@ from dpwa_amd.flat import FlatParameters
 from oracle import gossip as ogossip
 
 
-def test_device_tensor_shares_memory_and_releases_its_descriptor():
+def test_device_tensor_shares_memory_and_calls_nothing_when_freed():
     a = np.arange(1000, dtype=np.float32)
     t = devview.device_tensor(a.ctypes.data, 1000, torch.float32, 0, device_type=devview.KDL_CPU)
     assert t.dtype == torch.float32 and t.shape == (1000,) and t.data_ptr() == a.ctypes.data
@@ -23,10 +23,12 @@ def test_device_tensor_shares_memory_and_releases_its_descriptor():
     tb = devview.device_tensor(b.ctypes.data, 64, torch.bfloat16, 0, device_type=devview.KDL_CPU)
     tb.fill_(1.0)
     assert b[0] == 0x3F80                                # bf16 1.0
-    live = len(devview._live)
+    made = devview.made[0]
     del t, tb
-    gc.collect()
-    assert len(devview._live) == live - 2               # the deleter dropped both descriptors
+    gc.collect()                                        # no deleter: torch drops the views quietly
+    assert devview.made[0] == made
+    t2 = devview.device_tensor(a.ctypes.data, 1000, torch.float32, 0, device_type=devview.KDL_CPU)
+    assert t2[7].item() == -3.0 and devview.made[0] == made + 1
 
 
 def test_device_tensor_refuses_what_it_cannot_describe():
