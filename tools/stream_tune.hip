@@ -114,6 +114,25 @@ __global__ __launch_bounds__(BLOCK) void k_avg(Args a)
     }
 }
 
+// The resident (out-of-place) average: reads param and peer, stores ONLY into snap (2R:1W to a
+// third buffer: the learner reads the published slot and writes the other one).
+template <int BLOCK, int U, int AUXS = SC1>
+__global__ __launch_bounds__(BLOCK) void k_oop(Args a)
+{
+    const int64_t span = (int64_t)BLOCK * 16 * U;
+    const int64_t off = (int64_t)blockIdx.x * span;
+    auto rq = rsrc(a.peer, off, a.bytes, (int)span);
+    auto rp = rsrc(a.param, off, a.bytes, (int)span);
+    f32x4 q[U], p[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) q[u] = ld<NT>(rq, threadIdx.x * 16 + u * BLOCK * 16);
+#pragma unroll
+    for (int u = 0; u < U; ++u) p[u] = ld<NT>(rp, threadIdx.x * 16 + u * BLOCK * 16);
+    auto rs = rsrc(a.snap, off, a.bytes, (int)span);
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<AUXS>(rs, threadIdx.x * 16 + u * BLOCK * 16, lerp4(0.5f, 0.5f, q[u], p[u]));
+}
+
 // Persistent grid, software-pipelined: the next span's loads are issued before this span's
 // stores, so the in-order vmcnt wait for them never waits on a store.
 template <int BLOCK, bool DUAL>
@@ -232,6 +251,18 @@ int main(int argc, char **argv)
              launch(k_pipe<64, false>, std::min(grid_of(a.bytes, 64 * 16), cus * 32), 64, a, s, e0, e1); }},
         {"avg  xcd-slab 64", 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
              launch(k_avg_xcdslab<64, false>, (grid_of(a.bytes, 64 * 16) + 7) / 8 * 8, 64, a, s, e0, e1); }},
+        {"oop  64x1 (resident, 2R1W')", 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+             launch(k_oop<64, 1>, grid_of(a.bytes, 64 * 16), 64, a, s, e0, e1); }},
+        {"oop  64x2", 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+             launch(k_oop<64, 2>, grid_of(a.bytes, 64 * 16 * 2), 64, a, s, e0, e1); }},
+        {"oop  64x4", 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+             launch(k_oop<64, 4>, grid_of(a.bytes, 64 * 16 * 4), 64, a, s, e0, e1); }},
+        {"oop 128x1", 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+             launch(k_oop<128, 1>, grid_of(a.bytes, 128 * 16), 128, a, s, e0, e1); }},
+        {"oop 256x1", 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+             launch(k_oop<256, 1>, grid_of(a.bytes, 256 * 16), 256, a, s, e0, e1); }},
+        {"oop  64x1 nt+sc1 store", 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+             launch(k_oop<64, 1, SC1 | NT>, grid_of(a.bytes, 64 * 16), 64, a, s, e0, e1); }},
         avg<64, 1, true>("dual 64x1 (product WT, 2R2W)"),
         avg<64, 2, true>("dual 64x2"),
         avg<64, 4, true>("dual 64x4"),
