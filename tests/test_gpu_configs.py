@@ -197,6 +197,66 @@ def test_full_size_configs_with_their_settings(tmp_path, cfgname, n, dtype, G, i
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("cfgname,n,dtype,G,interp,fp,thr,T", [
+    ("configs[2]", 100_000_000, torch.float32, 3, "clock", 1, 0.0, 5),
+    ("configs[3]", 1_000_000_000, torch.bfloat16, 2, "loss", 1, 0.5, 8),
+    ("configs[4]", 7_000_000_000, torch.bfloat16, 3, "constant", 0.7, 0.0, 6),
+])
+def test_full_size_configs_resident(tmp_path, cfgname, n, dtype, G, interp, fp, thr, T):
+    """The same configs at full size with resident learners (the bench's form), their averages
+    batched: sampled windows of every learner's parameters after every round against the oracle
+    lerp of the published windows (a learner without a fetch keeps its parameters: relocated);
+    peers, clocks and flow-control scores against the oracle policy; the served snapshot untouched
+    by the round's averages."""
+    names = ["w%d" % (g + 1) for g in range(G)]
+    cfg = tmp_path / "bigres.yaml"
+    write_cfg(cfg, names, fp, interp, thr, 0.5)
+    group = LocalGroup()
+    conns = [DpwaConnection(names[g], str(cfg), seed=300 + g, group=group) for g in range(G)]
+    for g in range(G):
+        conns[g].make_resident(_fill(n, dtype, 10 + g))
+    torch.cuda.empty_cache()
+    L = [OracleLearner(names[g], [x for x in names if x != names[g]], fp, interp, 0.5, thr, 300 + g)
+         for g in range(G)]
+    win = [slice(0, 1 << 16), slice(n // 2 - 7, n // 2 + 4099), slice(n - (1 << 16) - 3, n)]
+    lerp = olerp.lerp_bf16 if dtype == torch.bfloat16 else olerp.lerp_f32
+    rng = np.random.default_rng(9)
+    crossed, relocated = False, 0
+    for r in range(T):
+        send = [2.0 * float(np.exp(-r / 3.0)) + 0.05 * float(rng.random()) for _ in range(G)]
+        wait = [2.0 * float(np.exp(-(r + 0.5) / 3.0)) + 0.05 * float(rng.random()) for _ in range(G)]
+        crossed |= min(wait) < thr
+        for g in range(G):
+            conns[g].update_send(conns[g].parameters, send[g])
+        published = [c.parameters for c in conns]
+        snaps = [[_bits(f[w]) for w in win] for f in published]
+        exp = oracle_round(L, send, wait, names)
+        res = DpwaConnection.update_wait_average_many(conns, published, wait)
+        for g in range(G):
+            payload, _ = res[g]
+            q, factor = exp[g]
+            assert (payload.peer if payload is not None else None) == (names[q] if q is not None else None), (r, g)
+            now = conns[g].parameters
+            assert now.data_ptr() != published[g].data_ptr()
+            relocated += q is None
+            for k, w in enumerate(win):
+                want = lerp(snaps[g][k], snaps[q][k], factor) if q is not None else snaps[g][k]
+                assert olerp.bits_equal(_bits(now[w]), want), (cfgname, r, g, k)
+                assert olerp.bits_equal(_bits(published[g][w]), snaps[g][k]), (cfgname, r, g, k)
+            assert conns[g].clock == L[g].clock, (cfgname, r, g)
+        assert [conns[g].flow_control_scores() for g in range(G)] == \
+               [dict(zip([x for x in names if x != names[g]], L[g].scores([x for x in names if x != names[g]])))
+                for g in range(G)]
+    if thr > 0:
+        assert crossed
+    if fp < 1:
+        assert relocated > 0
+    for c in conns:
+        c.close()
+    del published
+    torch.cuda.empty_cache()
+
+
 def test_gpu_key_moves_the_model_onto_its_device(tmp_path):
     """f4: a node's gpu: key places its learner -- the adapter re-homes a model built on the
     CPU into a flat buffer on that GPU (before the optimizer exists, as main.py:109-116)."""
