@@ -55,9 +55,11 @@ def write_cfg(path, names, fp, interp, thr):
 
 
 def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of_rank, pull="copy", dtype="f32",
-                  digest=False):
+                  digest=False, resident=False):
     """Lock-step rounds through DistGroup; saves every round's parameters (or, with
-    `digest`, their sha1 -- for full-size vectors), clock and peer."""
+    `digest`, their sha1 -- for full-size vectors), clock and peer.  `resident`: the parameters
+    live in the learner's slots, every round averages fused and the training delta comes after
+    update_wait (the saved parameters are those right after the average)."""
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -75,7 +77,16 @@ def gossip_worker(rank, world, port, cfg_path, out_dir, n, T, backend, device_of
     params = [] if digest else np.zeros((T, n), init.dtype)
     clocks = np.zeros(T)
     peers = []
-    for r in range(T):
+    if resident:
+        conn.make_resident(flat)
+        for r in range(T):
+            conn.update_send(conn.parameters, send[r][rank])
+            payload, _ = conn.update_wait_average(conn.parameters, wait[r][rank])
+            peers.append(payload.peer if payload is not None else None)
+            params[r] = to_host(conn.parameters)
+            clocks[r] = conn.clock
+            conn.parameters.add_(to_device(deltas[r, rank], dev))      # the step, after update_wait
+    for r in range(0 if not resident else T, T):
         conn.update_send(flat, send[r][rank])
         flat.add_(to_device(deltas[r, rank], dev))
         if r % 2:

@@ -65,6 +65,36 @@ def test_ipc_gossip_bf16_matches_oracle(tmp_path, world, interp, fp, thr, pull):
     test_ipc_gossip_matches_oracle(tmp_path, world, interp, fp, thr, pull, n=100_003, dtype="bf16")
 
 
+@pytest.mark.parametrize("world,interp,fp,thr,pull,dtype", [(2, "clock", 1.0, 0.0, "copy", "f32"),
+                                                             (3, "loss", 0.7, 0.5, "kernel:64", "bf16"),
+                                                             (3, "clock", 0.7, 0.0, "relay:8", "f32"),
+                                                             (3, "clock", 0.8, 0.0, "relay-avg:8", "bf16"),
+                                                             (2, "constant", 1.0, 0.0, "relay-avg:8", "f32")])
+def test_ipc_gossip_resident_matches_oracle(tmp_path, world, interp, fp, thr, pull, dtype, n=100_003):
+    """Resident learners (parameters in their IPC-exported slots; the average reads the published
+    slot and writes the other) in separate processes through every pull, the relay's fused
+    out-of-place average included, f32 and bf16 with a ragged payload, rounds without a fetch
+    relocating: parameters, clocks and peers bit-exact with oracle/gossip.py in the resident loop
+    order (the step after update_wait)."""
+    T = 10
+    names = ["r%d" % i for i in range(world)]
+    cfg = str(tmp_path / "res.yaml")
+    dist_worker.write_cfg(cfg, names, fp, interp, thr)
+    mp.spawn(dist_worker.gossip_worker,
+             args=(world, free_port(), cfg, str(tmp_path), n, T, "gloo", 0, pull, dtype, False, True),
+             nprocs=world, join=True)
+    init, deltas, send, wait = dist_worker.inputs(world, n, T, dtype=dtype)
+    kw = dict(lerp=olerp.lerp_bf16, add=ogossip.add_bf16) if dtype == "bf16" else {}
+    exp = ogossip.simulate(names, init, deltas, send, wait, interp, 0.5, thr, fp, [500 + r for r in range(world)],
+                           train_after_wait=True, **kw)
+    for r in range(world):
+        got = np.load(tmp_path / ("rank%d.npz" % r))
+        want_peers = [p[0] if p else "" for p in (exp["picks"][t][r] for t in range(T))]
+        assert list(got["peers"]) == want_peers, r
+        assert np.array_equal(got["clocks"], exp["clocks"][:, r]), r
+        assert olerp.bits_equal(got["params"], exp["params"][:, r]), r
+
+
 @pytest.mark.parametrize("pull", ["copy", "relay:64", "relay-avg:64"])
 def test_ipc_gossip_configs2_full_size(tmp_path, pull):
     """BASELINE configs[2] at its own size and interpolation through the multi-process path:
