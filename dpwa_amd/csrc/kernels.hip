@@ -783,6 +783,36 @@ __global__ __launch_bounds__(BLOCK) void k_publish(char *__restrict__ slot, cons
     }
 }
 
+// Local streaming copy of a payload (a resident learner's relocation: the parameters leave the
+// published slot for the next one), the publish's span shape without the header.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_copy_payload(char *__restrict__ dst, const char *__restrict__ src,
+                                                        int64_t nbytes)
+{
+    constexpr int SPAN = BLOCK * 16;
+    const int64_t n16 = nbytes >> 4;
+    const int64_t span_off = (int64_t)blockIdx.x * SPAN;
+    const int lane_off = threadIdx.x * 16;
+    span_store(span_rsrc<SPAN>(dst, span_off, n16 * 16), lane_off,
+               span_load<u32x4>(span_rsrc<SPAN>(src, span_off, n16 * 16), lane_off));
+    if (blockIdx.x == 0 && threadIdx.x < (nbytes & 15)) {
+        const int64_t j = (n16 << 4) + threadIdx.x;
+        dst[j] = src[j];
+    }
+}
+
+hipError_t launch_copy_payload(void *dst, const void *src, int64_t nbytes, hipStream_t s)
+{
+    if (nbytes <= 0) return hipSuccess;
+    if (!aligned16(dst) || !aligned16(src))
+        return hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDevice, s);
+    const int64_t g = (nbytes >> 4) / kStreamBlock + 1;
+    if (g > 0x7fffffffLL) return hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDevice, s);
+    hipLaunchKernelGGL(k_copy_payload<kStreamBlock>, dim3((uint32_t)g), dim3(kStreamBlock), 0, s, (char *)dst,
+                       (const char *)src, nbytes);
+    return hipGetLastError();
+}
+
 // Pull: copy a peer's snapshot (header + payload, IPC-mapped in another GPU's HBM) into the
 // local staging buffer.  The loads travel over the xGMI link to the owner; each lane keeps
 // four 16-byte loads in flight and the grid is capped (grid-stride) so the pull occupies a

@@ -82,6 +82,8 @@ hipError_t launch_factor(const FusedArgs &fa, hipStream_t s);
 hipError_t launch_publish(char *slot, const void *flat, int64_t nbytes, int64_t n, int32_t dtype,
                           double *clock, double loss, const double *loss_dev, bool loss_f32, uint64_t version,
                           bool system_release, hipStream_t s);
+// Local streaming copy of `nbytes` (a resident learner's relocation between its slots).
+hipError_t launch_copy_payload(void *dst, const void *src, int64_t nbytes, hipStream_t s);
 // Pull of `nbytes` (multiple of 16, 16-B aligned) from a peer's slot into local staging with
 // a copy kernel of at most `max_blocks` workgroups.  `remote`: the source is another GPU's
 // memory -- the kernel is preceded by a system-scope acquire on every XCD, so no L2 line of

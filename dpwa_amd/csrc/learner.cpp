@@ -1295,9 +1295,7 @@ static int relocate_impl(dpwa_learner *l, hipStream_t s)
     if (!l->resident || l->res_slot == k) return DPWA_OK;
     int rc = wait_slot_readers(l, k, s);
     if (rc) return rc;
-    if (l->payload_bytes)
-        HIP_TRY(hipMemcpyAsync(slot_payload(l, k), slot_payload(l, l->res_slot), l->payload_bytes,
-                               hipMemcpyDeviceToDevice, s));
+    HIP_TRY(launch_copy_payload(slot_payload(l, k), slot_payload(l, l->res_slot), (int64_t)l->payload_bytes, s));
     l->res_slot = k;
     l->wt_valid = true;
     l->wt_header = false;     // the publish writes the header (the clock did not move)
