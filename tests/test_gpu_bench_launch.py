@@ -50,3 +50,22 @@ def test_injected_transport_failure_is_isolated():
     assert out["parity"]["lockstep/kernel:256+res"] is False
     assert all(v for k, v in out["parity"].items() if k not in ("workload", "lockstep/kernel:256+res"))
     assert out["value"] > 0 and not any(k.startswith("kernel") for k in out["pull_trials_gbs"])
+
+
+def test_resident_parity_failure_falls_back_to_write_through():
+    """If no resident transport passes the parity check (here an injected failure in the N=1 leg's
+    `local+res`), the timed run uses the verified write-through form, says so in the line, and the
+    run still exits 1 for the failed transport."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["DPWA_BENCH_INJECT"] = "local+res@0:end"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2",
+                        "--no-cpu-baseline", "--no-sweep", "--compute-us", "0", "--no-secondary", "--no-cold"],
+                       cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=280)
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert p.returncode == 1, p.stderr[-3000:]
+    assert len(lines) == 1, lines
+    out = json.loads(lines[0])
+    assert out["parity"]["local+res"] is False and out["parity"]["local"] is True
+    assert "publish_fallback" in out and out["config"]["publish"] == "write-through"
+    assert out["value"] > 0 and out["parity_of_timed_transport"] == {"transport": "local", "ok": True}
