@@ -126,11 +126,6 @@ class Learner:
             self._fail("dpwa_learner_publish", rc)
         self.version += 1
 
-    def set_resident(self, init, stream):
-        """dpwa_learner_set_resident: the parameters move into slot 0 (before the first publish)."""
-        _lib.call("dpwa_learner_set_resident", self._h, self._ptr(init), stream.cuda_stream)
-        return self.resident_params()
-
     def resident_params(self):
         """The tensor over the slot the resident parameters are in now (None when the learner is
         not resident); it changes at every average."""
