@@ -574,6 +574,7 @@ static hipError_t launch_oop(void *param, const void *peer, int64_t n, const Ler
     switch (lerp_policy()) {
     case 0: return launch_oop_policy<Ops, 0>(param, peer, n, args, s, timing);
     case 1: return launch_oop_policy<Ops, 1>(param, peer, n, args, s, timing);
+    case 2: return launch_oop_policy<Ops, 2>(param, peer, n, args, s, timing);
     case 16: return launch_oop_policy<Ops, 16>(param, peer, n, args, s, timing);
     case 17: return launch_oop_policy<Ops, 17>(param, peer, n, args, s, timing);
     default: return launch_oop_policy<Ops, kProductPolicy>(param, peer, n, args, s, timing);
@@ -668,6 +669,7 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
         switch (lerp_policy()) {                                                                            \
         case 0: DPWA_BATCH_LAUNCH_P(OPS, true, 0, true); break;                                             \
         case 1: DPWA_BATCH_LAUNCH_P(OPS, true, 1, true); break;                                             \
+        case 2: DPWA_BATCH_LAUNCH_P(OPS, true, 2, true); break;                                             \
         case 16: DPWA_BATCH_LAUNCH_P(OPS, true, 16, true); break;                                           \
         case 17: DPWA_BATCH_LAUNCH_P(OPS, true, 17, true); break;                                           \
         default: DPWA_BATCH_LAUNCH_P(OPS, true, kProductPolicy, true); break;                               \
