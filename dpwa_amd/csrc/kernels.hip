@@ -33,6 +33,10 @@
 
 #include <hip/hip_ext.h>
 
+#ifndef DPWA_FACTOR_LDS
+#define DPWA_FACTOR_LDS 0     // 1: one-wave workgroups hand the factor over through LDS too (A/B builds)
+#endif
+
 namespace dpwa {
 
 constexpr int kBlock = 256;   // 4 waves of 64
@@ -313,21 +317,37 @@ __device__ __forceinline__ void lerp_span(uint32_t blk, typename Ops::V *__restr
         a = args.coef->a;
         b = args.coef->b;
     } else {
-        __shared__ float s_a, s_b;
-        __shared__ int s_ok;
-        if (threadIdx.x < 64) {  // wave 0: fp64 factor while the loads are in flight
+        bool ok;
+        if (BLOCK == 64 && !DPWA_FACTOR_LDS) {
+            // one-wave workgroup: every lane evaluates the (uniform) fp64 factor while the loads
+            // are in flight and keeps it in registers -- no LDS hand-off, no barrier
             const FusedArgs &fa = args.fused;
             const double loss = read_loss(fa.loss_d, fa.loss_f32, fa.loss_h);
             const dpwa_coef c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, loss);
-            if (threadIdx.x == 0) {
-                s_a = c.a;
-                s_b = c.b;
-                s_ok = c.status == DPWA_STATUS_OK;
-                if (blk == 0) factor_commit(fa, c);
+            if (blk == 0 && threadIdx.x == 0) factor_commit(fa, c);
+            a = c.a;
+            b = c.b;
+            ok = c.status == DPWA_STATUS_OK;
+        } else {
+            __shared__ float s_a, s_b;
+            __shared__ int s_ok;
+            if (threadIdx.x < 64) {  // wave 0: fp64 factor while the loads are in flight
+                const FusedArgs &fa = args.fused;
+                const double loss = read_loss(fa.loss_d, fa.loss_f32, fa.loss_h);
+                const dpwa_coef c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, loss);
+                if (threadIdx.x == 0) {
+                    s_a = c.a;
+                    s_b = c.b;
+                    s_ok = c.status == DPWA_STATUS_OK;
+                    if (blk == 0) factor_commit(fa, c);
+                }
             }
+            __syncthreads();
+            a = s_a;
+            b = s_b;
+            ok = s_ok != 0;
         }
-        __syncthreads();
-        if (!s_ok) {          // no-op round; a write-through snapshot still gets the parameters
+        if (!ok) {            // no-op round; a write-through snapshot still gets the parameters
             if (DUAL)
                 span_store<V, LerpPolicy<POLICY>::snap_store>(span_rsrc<SPAN>(args.snap, span_off, nv * 16), lane_off, p);
             if (DUAL && blk == 0 && threadIdx.x < n - nv * Ops::PER) {
@@ -336,8 +356,6 @@ __device__ __forceinline__ void lerp_span(uint32_t blk, typename Ops::V *__restr
             }
             return;
         }
-        a = s_a;
-        b = s_b;
     }
     {
         const V r = Ops::lerp(a, b, q, p);
