@@ -13,8 +13,9 @@
 //             changes up to ~30% of results near cancellation), so contraction is
 //             switched off for this whole file.
 //  * fused average: the same pass with the factor of dpwa/dpwa.py:139-155 computed in
-//             the kernel: wave 0 of every workgroup evaluates it in fp64 while the
-//             workgroup's loads are in flight and shares (a, b) through LDS; block 0
+//             the kernel: every workgroup evaluates it in fp64 while its loads are in flight
+//             (one-wave workgroups keep the uniform (a, b) in registers; wider ones have wave 0
+//             share them through LDS); block 0
 //             also writes the new clock (into the other half of a double-buffered clock,
 //             so no workgroup ever reads a clock another one is writing) and dpwa_coef.
 //  * factor:  the same fp64 math as a one-thread kernel for the split API.
