@@ -97,6 +97,8 @@ class DpwaPyTorchAdapter:
         """pytorch.py:55-68: wait for the fetch and average in place (resident: into the other
         slot, where the parameters are re-pointed)."""
         if self._resident:
+            if self._conn.parameters is None:         # no update_send yet: nothing to average
+                return
             self._conn.update_wait_average(self._flat.buffer, loss)
             self._flat.rehome(self._conn.parameters)
             return
@@ -124,7 +126,7 @@ class DpwaPyTorchAdapter:
                                                       [a._flat.buffer for a in adapters], list(losses),
                                                       write_through=wt)
         for a, (payload, _) in zip(adapters, res):
-            if resident:
+            if resident and a._conn.parameters is not None:
                 a._flat.rehome(a._conn.parameters)
             elif wt and payload is not None:
                 a._versions = a._param_versions()

@@ -81,3 +81,21 @@ def test_oracle_train_after_wait_is_the_resident_order():
     c = ogossip.simulate(names, init, deltas, send, wait, "clock", None, 0.0, 0.7, seeds, train_after_wait=True)
     assert np.array_equal(c["clocks"], a["clocks"])      # the policy does not see the parameters
     assert not np.array_equal(c["params"], a["params"])
+
+
+def test_resident_adapter_update_wait_before_any_update_send_is_a_noop(tmp_path):
+    """As in the reference (update_wait without a fetch returns (None, 0) and the adapter leaves
+    the parameters alone), a resident adapter's update_wait before its first update_send does
+    nothing -- no binding, no GPU call."""
+    from dpwa_amd import DpwaPyTorchAdapter
+    from dpwa_amd.launch import write_config
+    from dpwa_amd.group import LocalGroup
+    cfg = write_config(str(tmp_path / "r.yaml"), ["a", "b"], interpolation="constant")
+    net = torch.nn.Linear(3, 2)
+    before = [p.detach().clone() for p in net.parameters()]
+    ad = DpwaPyTorchAdapter(net, "a", cfg, seed=1, group=LocalGroup(), resident=True)
+    ad.update_wait(1.0)
+    DpwaPyTorchAdapter.update_wait_many([ad], [1.0])
+    assert ad.connection.parameters is None
+    assert all(torch.equal(p.detach(), b) for p, b in zip(net.parameters(), before))
+    ad.connection.close()
