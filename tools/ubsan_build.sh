@@ -3,6 +3,7 @@
 # Sanitizer in trap mode (a check that fails executes a trap instruction: no sanitizer runtime
 # to load, so it runs inside python as is).  Device code is not instrumented.  Use it with
 #   DPWA_HIP_LIB=$PWD/build_san/libdpwa_hip.so python -m pytest tests ...
+# (build_san is listed in .gpurunignore: take that line out before a GPU run that loads it)
 set -e
 cd "$(dirname "$0")/../dpwa_amd/csrc"
 mkdir -p ../../build_san
