@@ -50,7 +50,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-XGMI_LINK_GBS = 153.6          # MI355X xGMI per link (spec, both directions)
+XGMI_LINK_GBS = 153.6          # MI355X xGMI per link (spec, both directions together)
+XGMI_LINK_DIR_GBS = XGMI_LINK_GBS / 2   # one direction of one link: what a pull of a peer's snapshot uses
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_MEASURED_GBS = 6290.0      # the guide's measured HBM ceiling (float4 copy, MI355X_MICROARCH.md)
 RESNET18_NUMEL = 11_173_962    # examples/pytorch-cifar/models/resnet.py ResNet18
@@ -1130,6 +1131,8 @@ def main(argv=None):
         parity = parity_leg(world, rank, local_rank, device, tmp, parity_transports(world, args.gossip),
                             args.dist_backend, ctl=ctl, watchdog=wd)
 
+    # rehearsals run several ranks on one GPU: their pulls never cross an xGMI link
+    shared_device = world > 1 and world > torch.cuda.device_count()
     wd.enter("learners", 300.0)
     group = LocalGroup() if world == 1 else None
     learners = []
@@ -1327,26 +1330,31 @@ def main(argv=None):
                 torch.matmul(a, b, out=c)
         return compute, k, per_us
 
-    def run_overlap(steps, warmup, compute, gossip):
-        """Training-loop shape (main.py:122-158): update_send, the step, update_wait."""
+    def run_overlap(steps, warmup, compute, gossip, wt, update):
+        """The reference's training loop (main.py:130-145): update_send, the step (`compute`, then
+        `update` -- an SGD-style write of every learner's parameters), update_wait.  The step
+        writes the parameters while peers read the snapshot taken at update_send, so the learners
+        are write-through (or full-publish) ones: a resident learner's update_wait refuses
+        parameters written in that window."""
         def step():
             done = 0
             losses = [loss_of(i) for i in range(len(learners))]
             loss_t[0] += 1
             if gossip:
                 for i, (conn, flat) in enumerate(learners):
-                    conn.update_send(params_of(conn, flat), losses[i], reuse_snapshot=wt_main)
-            for _ in learners:
+                    conn.update_send(flat, losses[i], reuse_snapshot=wt)
+            for _, flat in learners:
                 compute()
+                update(flat)
             if gossip:
                 if batched:
                     res = DpwaConnection.update_wait_average_many([c for c, _ in learners],
-                                                                  [params_of(c, f) for c, f in learners], losses,
-                                                                  write_through=wt_main)
+                                                                  [f for _, f in learners], losses,
+                                                                  write_through=wt)
                     done += sum(p is not None for p, _ in res)
                 else:
                     for i, (conn, flat) in enumerate(learners):
-                        payload, _ = conn.update_wait_average(params_of(conn, flat), losses[i], write_through=wt_main)
+                        payload, _ = conn.update_wait_average(flat, losses[i], write_through=wt)
                         done += payload is not None
             return done
 
@@ -1481,46 +1489,61 @@ def main(argv=None):
         dist.all_gather_object(got, float(np.mean(pull_us)) if pull_us else float("nan"), group=ctl)
         pull_us = [float(np.mean(got))]
     secondary = None
-    if not args.no_secondary and not resident_main:   # the other publish form, same learners and transport
+    main_set = list(learners)
+    wt_set = None           # write-through learners: the reference loop's form (secondary, overlap)
+    wt_key = None           # the parity transport that vouches for them
+    if not resident_main:
+        wt_set = main_set
+    elif not args.no_secondary or args.compute_us > 0:
+        # resident learners cannot leave their slots: the write-through form runs on a second set
+        # of learners (same initial parameters, same transport; at N>1 every rank makes its own in
+        # the same order, the binding is collective)
+        wt_key = ("local" if world == 1 else
+                  parity_key(("async/" + sel_mode + "+wt") if sel_async else sel_mode))
+        if parity is None or parity.get(wt_key, False):
+            wd.enter("write-through learners", 300.0)
+            grp2 = LocalGroup() if world == 1 else ("async" if sel_async else "lockstep")
+            wt_set = [(DpwaConnection(name, cfg, seed=1000 + seed, group=grp2, pull=None if world == 1 else sel_mode),
+                       f0.clone()) for (name, seed), (_, f0) in zip(mine, main_set)]
+        else:
+            progress("write-through form not timed: %s did not pass the parity check" % wt_key)
+    if not args.no_secondary and wt_set is not None:
         wd.enter("secondary publish form", 600.0)
-        s2 = run(args.steps, args.warmup, not wt_main)
-        s2_k = run(s_steps, 2, not wt_main, args.sample_every)
-        secondary = ("write-through" if not wt_main else "full", s2, s2_k[3])
-    elif not args.no_secondary and world == 1:
-        # resident learners cannot leave their slots: the write-through form runs on a second pair
-        # of learners (same initial parameters, same rounds)
-        wd.enter("secondary publish form", 600.0)
-        main_set = list(learners)
-        grp2 = LocalGroup()
-        learners[:] = [(DpwaConnection(name, cfg, seed=1000 + seed, group=grp2), flat.clone())
-                       for (name, seed), (_, flat) in zip(mine, main_set)]
-        s2 = run(args.steps, args.warmup, True)
-        s2_k = run(s_steps, 2, True, args.sample_every)
-        secondary = ("write-through", s2, s2_k[3])
-        for conn, _ in learners:
-            conn.close()
+        learners[:] = wt_set
+        s_wt = True if resident_main else not wt_main    # the form the main run did not time
+        s2 = run(args.steps, args.warmup, s_wt)
+        s2_k = run(s_steps, 2, s_wt, args.sample_every)
+        secondary = ("write-through" if s_wt else "full", s2, s2_k[3])
         learners[:] = main_set
     overlap = None
-    if args.compute_us > 0:
+    if args.compute_us > 0 and wt_set is not None:
         wd.enter("overlap", 600.0)
         compute, k_gemm, gemm_us = make_compute(args.compute_us)
+        upd = torch.randn(args.numel, device=device, dtype=torch.float32).mul_(1e-4).to(dtype)
+
+        def update(flat):
+            flat.sub_(upd)      # the optimizer's write of the parameters (3*N*s of HBM traffic)
+
         o_steps = max(20, args.steps // 4)
-        progress("overlap: %d GEMMs per step" % k_gemm)
-        t_compute = run_overlap(o_steps, 3, compute, gossip=False)
+        o_wt = True if resident_main else wt_main
+        progress("overlap: %d GEMMs per step, %s learners" % (k_gemm, "write-through" if o_wt else "full"))
+        learners[:] = wt_set
+        t_compute = run_overlap(o_steps, 3, compute, False, o_wt, update)
         o_trials = {}
         o_mode = sel_mode
         if world > 1 and o_mode != "copy" and args.pull == "auto":
             # the copy engine leaves every CU to the training step: try it beside the
             # pure-loop winner and keep the cheaper overlap
             for m in [m for m in (o_mode, "copy")
-                      if verified((m + res_sfx) if not sel_async else "async/" + m + ("+wt" if wt_main else res_sfx))]:
+                      if verified(("async/" + m + ("+wt" if o_wt else "")) if sel_async else m)]:
                 set_pull(m)
-                o_trials[m] = run_overlap(o_steps, 3, compute, gossip=True)
+                o_trials[m] = run_overlap(o_steps, 3, compute, True, o_wt, update)
             o_mode = min(o_trials, key=o_trials.get)
             t_both = o_trials[o_mode]
             set_pull(sel_mode)
         else:
-            t_both = run_overlap(o_steps, 3, compute, gossip=True)
+            t_both = run_overlap(o_steps, 3, compute, True, o_wt, update)
+        learners[:] = main_set
         overlap = {
             "compute": "%d x bf16 GEMM 4096^3 per learner per step (%.1f us each)" % (k_gemm, gemm_us),
             "steps": o_steps,
@@ -1528,15 +1551,25 @@ def main(argv=None):
             "ms_per_step": round(1e3 * t_both / o_steps, 4),
             "gossip_overhead_frac": round(t_both / t_compute - 1.0, 4),
             "rounds_per_s_per_learner": round(o_steps / t_both, 1),
-            "gossip_rounds_per_s": round(o_steps * len(learners) * world / t_both, 1),   # all learners, all ranks
+            "gossip_rounds_per_s": round(o_steps * len(wt_set) * world / t_both, 1),   # all learners, all ranks
             "transport": o_mode if world > 1 else "in-place HBM read (co-resident peer)",
-            "note": "update_send -> synthetic training step -> update_wait_average (SURVEY §8d C4 "
-                    "weak scaling): the overhead the gossip round adds to a step of this length. Scaling "
-                    "definition: per-learner compute is fixed, so gossip_rounds_per_s (all learners) "
-                    "compared across N is the weak-scaling figure; value above is the raw bandwidth loop",
+            "publish": "write-through" if o_wt else "full",
+            "loop_order": "update_send -> step (GEMMs, then a write of every parameter) -> update_wait",
+            "note": "the reference's loop order (main.py:130-145; SURVEY §8d C4 weak scaling) with a synthetic "
+                    "step that writes the parameters while peers read the update_send snapshot, so the learners "
+                    "publish write-through (%s): the overhead the gossip round adds to a step of this length. "
+                    "Scaling definition: per-learner compute is fixed, so gossip_rounds_per_s (all learners) "
+                    "compared across N is the weak-scaling figure; value above is the raw bandwidth loop"
+                    % ("a second set of learners: the timed run's are resident, which refuses this order"
+                       if resident_main else "the timed run's learners"),
         }
         if o_trials:
             overlap["trials_ms_per_step"] = {m: round(1e3 * t / o_steps, 4) for m, t in o_trials.items()}
+    if resident_main and wt_set is not None:
+        hbarrier()      # every rank's pulls of these learners' slots are done
+        for conn, _ in wt_set:
+            conn.close()
+        wt_set = None
 
     if parity is not None:
         parity["workload"] = ("%d-element fp32 vector per learner, %d lock-step rounds (clock interpolation, "
@@ -1555,11 +1588,21 @@ def main(argv=None):
     # the same kernel alone, cold (rotating buffers, per-launch dispatch events): the roofline's basis
     cold = None
     cold_plain = None
+    cold_ref = {}           # the reference loop's (write-through) kernels and the single resident one, cold
     if not args.no_cold:
         wd.enter("cold kernel", 300.0)
         cold = cold_kernel(args.numel, dtype, device, wt_kernel, learners=per_launch, resident=resident_main)
         if wt_kernel:   # BASELINE's target kernel: the same dispatch without the snapshot write
             cold_plain = cold_kernel(args.numel, dtype, device, False, learners=per_launch)
+        for key, wt_, n_, res_ in (("write_through_x%d" % per_launch, True, per_launch, False),
+                                   ("write_through_single", True, 1, False), ("resident_single", False, 1, True)):
+            if key == "write_through_single" and per_launch == 1:
+                continue
+            same = (n_ == per_launch and res_ == resident_main and wt_ == wt_kernel)
+            c = cold if same else cold_kernel(args.numel, dtype, device, wt_, learners=n_, resident=res_)
+            b = n_ * (4 if wt_ else 3) * args.numel * esize
+            cold_ref[key] = {"avg_launch_us": round(c["avg_launch_us"], 2),
+                             "frac": round(b / (c["avg_launch_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
     wd.enter("report", 120.0)
     out = None
     if rank == 0:
@@ -1615,10 +1658,12 @@ def main(argv=None):
                 "publish": variant,
                 "publish_note": ("resident: each learner's parameters live in its two snapshot slots; the average "
                                  "reads the published slot and writes the other (3*N*s), the publish moves nothing. "
-                                 "Valid for rounds that write nothing to the parameters between update_send and "
-                                 "update_wait, as these synthetic rounds (no training step); the reference's own loop "
-                                 "trains in that window and needs the write-through form (at N=1 timed in "
-                                 "secondary_publish; --publish write-through times it as the main run)"
+                                 "This value assumes the loop order update_send -> update_wait -> step (nothing "
+                                 "writes the parameters between update_send and update_wait; these synthetic rounds "
+                                 "have no step, and update_wait raises if the window was written). The reference's "
+                                 "own order update_send -> step -> update_wait needs the write-through form: "
+                                 "reference_loop (last key) and secondary_publish; --publish write-through times "
+                                 "it as the main run"
                                  if resident_main else
                                  "write-through: the average also writes the next snapshot (4*N*s)" if wt_main else
                                  "full: every publish copies the 2*N*s snapshot"),
@@ -1717,23 +1762,30 @@ def main(argv=None):
         if world > 1:
             pull_bytes = 256 + args.numel * esize
             p_us = pull_us[0] if pull_us and np.isfinite(pull_us[0]) else None
+            p_gbs = pull_bytes / (p_us * 1e-6) / 1e9 if p_us else None
             out["xgmi"] = {
                 "bytes_per_pull": pull_bytes,
                 "avg_pull_us": round(p_us, 2) if p_us else None,
-                "achieved_gbs_per_pull": round(pull_bytes / (p_us * 1e-6) / 1e9, 1) if p_us else None,
-                "peak_link_gbs": XGMI_LINK_GBS,
-                "note": "one pull = one peer snapshot over the direct link between the two GPUs, timed by "
-                        "side-stream events around each copying fetch (mean over ranks; null for the relay); "
-                        "peak = MI355X xGMI spec per link, both directions together",
+                "achieved_gbs_per_pull": round(p_gbs, 1) if p_gbs else None,
+                "peak_gbs": XGMI_LINK_DIR_GBS,
+                "frac": round(p_gbs / XGMI_LINK_DIR_GBS, 4) if p_gbs and not shared_device else None,
+                "ranks_share_device": shared_device,
+                "note": "one pull = one peer snapshot, one direction of the direct link between the two GPUs, timed "
+                        "by side-stream events around each copying fetch (mean over ranks; null for the relay); peak "
+                        "= MI355X xGMI spec per link and direction (%.1f GB/s both ways)%s"
+                        % (XGMI_LINK_GBS, "; ranks share a device here (a rehearsal): the pulls never cross a link, "
+                           "so the rate is an HBM copy rate and frac is null" if shared_device else ""),
             }
             if sel_mode.startswith("relay"):
                 # every directed link carries at most one stripe per phase, two per round
                 link_bytes = 2 * ((args.numel * esize + 15) // 16 * 16) // world
+                l_gbs = link_bytes / (elapsed / args.steps) / 1e9
                 out["xgmi"]["relay"] = {
                     "bytes_per_link_per_round": link_bytes,
                     "round_us": round(1e6 * elapsed / args.steps, 2),
-                    "achieved_gbs_per_link_direction": round(link_bytes / (elapsed / args.steps) / 1e9, 1),
-                    "peak_link_gbs_per_direction": XGMI_LINK_GBS / 2,
+                    "achieved_gbs_per_link_direction": round(l_gbs, 1),
+                    "peak_gbs": XGMI_LINK_DIR_GBS,
+                    "frac": round(l_gbs / XGMI_LINK_DIR_GBS, 4) if not shared_device else None,
                     "note": "the relay's busiest directed link per round over the whole round's time "
                             "(barriers and the average included): a lower bound on the link rate",
                 }
@@ -1772,6 +1824,22 @@ def main(argv=None):
         if world == 1:
             out["roofline"]["size_sweep"] = size_rows
         out["round_sweep"] = round_rows
+    if out is not None:
+        # last key, so it stays in the tail of the output a driver keeps: the drop-in form's numbers
+        # (the reference's own loop order) beside the headline's
+        ref = {"order": "update_send -> step -> update_wait (README.md:18-29, main.py:130-145)",
+               "publish": "write-through"}
+        sp = out.get("secondary_publish")
+        if sp is not None and sp["publish"] == "write-through":
+            ref.update(value=sp["value"], ms_per_step=sp["ms_per_step"])
+        elif not resident_main and wt_main:
+            ref.update(value=out["value"], ms_per_step=out["ms_per_step"])
+        else:
+            ref.update(value=None, ms_per_step=None)
+        ref["kernel_cold"] = cold_ref or None
+        if resident_main:
+            ref["headline"] = "resident (update_send -> update_wait -> step): %.1f GB/s" % out["value"]
+        out["reference_loop"] = ref
     wd.hold(out, 1 if parity_failed else 0)
     if world == 1 and not args.no_sweep:
         wd.enter("size sweep", 900.0)

@@ -40,13 +40,20 @@ class DpwaPyTorchAdapter:
 
     resident (extension, off by default): the parameters live in the learner's own two snapshot
     slots (``DpwaConnection.make_resident``) and every ``param.data`` is re-pointed to the slot
-    they are in after each update_wait -- a publish moves no bytes and an average moves 3*N*s
-    (the write-through form 4*N*s), for one ``.data`` assignment per parameter per round on the
-    host.  Writes through ``param.data`` are then always part of the next snapshot (no reuse
-    guard is needed); what must hold is the reference loop's order: nothing writes the
-    parameters between update_send and update_wait (they are the served snapshot then).  Code
-    that keeps raw data pointers of the parameters across rounds (a captured HIP graph of the
-    training step) must not use it."""
+    they are in after each update_send and update_wait -- a publish moves no bytes and an
+    average moves 3*N*s (the write-through form 4*N*s), for one ``.data`` assignment per
+    parameter per round on the host.  Writes through ``param.data`` are then always part of the
+    next snapshot (no reuse guard is needed).  The price is the loop order: between update_send
+    and update_wait the parameters ARE the snapshot peers read, so nothing may write them
+    there.  The reference's loop trains exactly there (README.md:18-29,
+    examples/pytorch-cifar/main.py:130-145: update_send, step, update_wait) and keeps the
+    default write-through form; a resident adapter needs update_send, update_wait, step (each
+    step then comes after the round's average instead of before it).  update_wait raises
+    DpwaError when a parameter's (or the flat buffer's) version counter moved since update_send
+    -- an optimizer step, ``param.add_``, ``load_state_dict`` in the window.  Writes through
+    ``param.data`` bypass version counters and are not caught.  Code that keeps raw data
+    pointers of the parameters across rounds (a captured HIP graph of the training step) must
+    not use it."""
 
     def __init__(self, net, name, config_file, write_through=True, transport="device", reuse_guard=True,
                  resident=False, **connection_kwargs):
@@ -71,9 +78,21 @@ class DpwaPyTorchAdapter:
         self._reuse_guard = bool(reuse_guard)
         self._guard_set = False
         self._versions = None
+        self._sent = None           # resident: the version counters at the last update_send
 
     def _param_versions(self):
         return [p._version for p in self._flat.params] + [self._flat.buffer._version]
+
+    def _check_window(self):
+        """Resident form: nothing may have written the parameters since update_send (they are
+        the snapshot peers read until the average)."""
+        if self._sent is not None and self._param_versions() != self._sent:
+            raise _lib.DpwaError(
+                "DpwaPyTorchAdapter.update_wait", _lib.ERR_STATE,
+                "the parameters were modified between update_send and update_wait (an optimizer step?); "
+                "with resident=True they are the snapshot peers read in that window, so the loop must run "
+                "update_send -> update_wait -> step.  The reference's order update_send -> step -> "
+                "update_wait (README.md, main.py:130-145) needs resident=False (the write-through default)")
 
     def update_send(self, loss):
         """pytorch.py:42-53: publish the parameters and maybe start a fetch."""
@@ -83,6 +102,10 @@ class DpwaPyTorchAdapter:
                 self._flat.rehome(self._conn.make_resident(self._flat.buffer))
             self._flat.resync()                        # a parameter re-homed by the caller
             self._conn.update_send(self._flat.buffer, loss)
+            # a publish with no average since the last one moved the parameters into the slot it
+            # published (dpwa_learner_relocate): the views follow them
+            self._flat.rehome(self._conn.parameters)
+            self._sent = self._param_versions()
             return
         moved = self._flat.resync()
         reuse = (self._write_through and moved == 0 and self._versions is not None
@@ -99,8 +122,10 @@ class DpwaPyTorchAdapter:
         if self._resident:
             if self._conn.parameters is None:         # no update_send yet: nothing to average
                 return
+            self._check_window()
             self._conn.update_wait_average(self._flat.buffer, loss)
             self._flat.rehome(self._conn.parameters)
+            self._sent = None
             return
         payload, _ = self._conn.update_wait_average(self._flat.buffer, loss, write_through=self._write_through)
         if self._write_through and payload is not None:
@@ -122,12 +147,16 @@ class DpwaPyTorchAdapter:
                 a.update_wait(loss)
             return
         wt, resident = wts.pop()
+        if resident:
+            for a in adapters:
+                a._check_window()
         res = DpwaConnection.update_wait_average_many([a._conn for a in adapters],
                                                       [a._flat.buffer for a in adapters], list(losses),
                                                       write_through=wt)
         for a, (payload, _) in zip(adapters, res):
             if resident and a._conn.parameters is not None:
                 a._flat.rehome(a._conn.parameters)
+                a._sent = None
             elif wt and payload is not None:
                 a._versions = a._param_versions()
 

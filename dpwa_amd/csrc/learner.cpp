@@ -300,6 +300,28 @@ static void close_endpoint(Endpoint &ep)
     ep.base = nullptr;
 }
 
+// A rescue lane: where a fetch re-selected after a timed-out pull goes (conn.py:304-309) -- a
+// buffer and a stream of the greatest priority (a hardware queue no stalled normal-priority stream
+// shares), so no stalled pull ahead of it can hold it up.
+constexpr int kRescueLanes = 3;
+struct RescueLane {
+    char *buf = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_landed = nullptr;     // its last pull landed
+    hipEvent_t ev_done = nullptr;       // the last reader of its buffer is done
+    bool used = false;                  // a pull was issued into it
+    bool read = false;                  // ev_done recorded
+};
+
+void destroy_lane(RescueLane &r)
+{
+    if (r.buf) (void)hipFree(r.buf);
+    if (r.stream) (void)hipStreamDestroy(r.stream);
+    if (r.ev_landed) (void)hipEventDestroy(r.ev_landed);
+    if (r.ev_done) (void)hipEventDestroy(r.ev_done);
+    r = RescueLane();
+}
+
 struct dpwa_learner {
     int device = 0;
     int64_t n = 0;
@@ -332,18 +354,16 @@ struct dpwa_learner {
     // the average that last read its buffer (ev_stage_done), so a pull starts at update_send
     // instead of after the caller's queued work, and a peer's read mark is released sooner.
     char *staging_alt = nullptr;        // second staging buffer, allocated at the first such fetch
-    // [2]: the rescue buffer (a fetch re-selected after a timed-out pull, conn.py:304-309),
-    // pulled on its own stream so a stalled pull ahead of it cannot hold it up
-    hipEvent_t ev_stage_done[3] = {nullptr, nullptr, nullptr};
-    bool stage_read[3] = {false, false, false};
-    char *rescue_buf = nullptr;
-    hipStream_t rescue_stream = nullptr;
-    hipEvent_t ev_rescue = nullptr;     // the last rescue pull landed
-    bool rescue_used = false;
+    hipEvent_t ev_stage_done[2] = {nullptr, nullptr};
+    bool stage_read[2] = {false, false};
+    // rescue lanes (RescueLane), allocated at first use: a lane whose pull has not landed stays
+    // taken and the next re-selected pull takes another, as TxThread keeps re-selecting
+    RescueLane rescue[kRescueLanes];
+    int rescue_lanes = 0;
     int64_t fetch_issue_ns = 0;         // host time the fetch in flight was issued (its timeout clock)
     hipStream_t fetch_stream = nullptr; // stream the fetch in flight moves its bytes on
     int stage_next = 0;
-    int src_stage = -1;                 // staging buffer (0 / 1) l->src points into, -1: none
+    int src_stage = -1;                 // buffer l->src points into: staging 0 / 1, rescue lane 2 + j; -1: none
     hipEvent_t ev_factor = nullptr;     // last factor computation done
     // write-through snapshot: the last average also wrote its result into the slot of the
     // next publish (for the flat buffer `wt_flat`, on stream `wt_stream`)
@@ -575,9 +595,7 @@ int dpwa_learner_destroy(dpwa_learner *l)
     for (auto ev : l->ev_stage_done)
         if (ev) (void)hipEventDestroy(ev);
     if (l->staging_alt) (void)hipFree(l->staging_alt);
-    if (l->rescue_buf) (void)hipFree(l->rescue_buf);
-    if (l->rescue_stream) (void)hipStreamDestroy(l->rescue_stream);
-    if (l->ev_rescue) (void)hipEventDestroy(l->ev_rescue);
+    for (auto &r : l->rescue) destroy_lane(r);
     if (l->ev_factor) (void)hipEventDestroy(l->ev_factor);
     if (l->ev_wt) (void)hipEventDestroy(l->ev_wt);
     if (l->ev_read) (void)hipEventDestroy(l->ev_read);
@@ -828,6 +846,42 @@ int dpwa_learner_attach_fds(dpwa_learner *l, int peer_id, const void *handle, in
     return DPWA_OK;
 }
 
+// A free rescue lane (its last pull landed, or none issued), allocating one when every lane is
+// taken and fewer than kRescueLanes exist; *lane = -1 when all kRescueLanes are still pulling.
+// A new lane is built in a local and counted only once every resource exists.
+static int rescue_lane(dpwa_learner *l, int *lane)
+{
+    *lane = -1;
+    for (int j = 0; j < l->rescue_lanes; ++j) {
+        RescueLane &r = l->rescue[j];
+        const hipError_t e = r.used ? hipEventQuery(r.ev_landed) : hipSuccess;
+        if (e == hipSuccess) {
+            *lane = j;
+            return DPWA_OK;
+        }
+        if (e != hipErrorNotReady) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(e));
+    }
+    if (l->rescue_lanes == kRescueLanes) return DPWA_OK;
+    RescueLane r;
+    int least = 0, greatest = 0;
+    hipError_t e;
+    do {
+        if ((e = hipMalloc(&r.buf, l->slot_stride)) != hipSuccess) break;
+        if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) break;
+        if ((e = hipStreamCreateWithPriority(&r.stream, hipStreamNonBlocking, greatest)) != hipSuccess) break;
+        if ((e = hipEventCreateWithFlags(&r.ev_landed, hipEventDisableTiming)) != hipSuccess) break;
+        e = hipEventCreateWithFlags(&r.ev_done, hipEventDisableTiming);
+    } while (0);
+    if (e != hipSuccess) {
+        destroy_lane(r);
+        return set_error(DPWA_ERR_HIP, "rescue lane %d: %s (%zu bytes)", l->rescue_lanes, hipGetErrorString(e),
+                         l->slot_stride);
+    }
+    l->rescue[l->rescue_lanes] = r;
+    *lane = l->rescue_lanes++;
+    return DPWA_OK;
+}
+
 int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int flags, dpwa_stream_t stream)
 {
     const int zero_copy = flags & DPWA_FETCH_ZERO_COPY;
@@ -857,36 +911,33 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
     l->fetch_issue_ns = now_ns();
     l->fetch_stream = l->side;
     if (flags & DPWA_FETCH_RESCUE) {
-        // re-selected after a timed-out pull: its own stream and buffer, ordered after the
-        // publish of the snapshot (above, local peers) and after the last reader of the buffer
-        if (!l->rescue_buf) {
-            HIP_TRY(hipMalloc(&l->rescue_buf, l->slot_stride));
-            // the greatest priority: a hardware queue of its own, not one a stalled normal-priority
-            // stream (the side stream, or any other of the process's streams) may share
-            int least = 0, greatest = 0;
-            HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-            HIP_TRY(hipStreamCreateWithPriority(&l->rescue_stream, hipStreamNonBlocking, greatest));
-            HIP_TRY(hipEventCreateWithFlags(&l->ev_rescue, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&l->ev_stage_done[2], hipEventDisableTiming));
-        }
+        // re-selected after a timed-out pull: a free lane (its own stream and buffer), ordered
+        // after the publish of the snapshot (above, local peers) and after the last reader of the
+        // lane's buffer
+        int j = -1;
+        const int rc = rescue_lane(l, &j);
+        if (rc) return rc;
+        if (j < 0)
+            return set_error(DPWA_ERR_STATE, "dpwa_learner_fetch: all %d rescue lanes are still pulling", kRescueLanes);
+        RescueLane &r = l->rescue[j];
         if (!(flags & DPWA_FETCH_PUBLISHED)) {
             HIP_TRY(hipEventRecord(l->ev_issue, s));
-            HIP_TRY(hipStreamWaitEvent(l->rescue_stream, l->ev_issue, 0));
+            HIP_TRY(hipStreamWaitEvent(r.stream, l->ev_issue, 0));
         }
-        if (l->stage_read[2]) HIP_TRY(hipStreamWaitEvent(l->rescue_stream, l->ev_stage_done[2], 0));
+        if (r.read) HIP_TRY(hipStreamWaitEvent(r.stream, r.ev_done, 0));
         const size_t nbytes = kPayloadOff + round_up(l->payload_bytes, 16);
         if (l->pull_mode == DPWA_PULL_KERNEL)
-            HIP_TRY(launch_pull(l->rescue_buf, peer_slot, (int64_t)nbytes, l->pull_blocks,
-                                ep.kind == 2 || ep.device != l->device, l->rescue_stream));
+            HIP_TRY(launch_pull(r.buf, peer_slot, (int64_t)nbytes, l->pull_blocks,
+                                ep.kind == 2 || ep.device != l->device, r.stream));
         else
-            HIP_TRY(hipMemcpyAsync(l->rescue_buf, peer_slot, nbytes, hipMemcpyDefault, l->rescue_stream));
-        HIP_TRY(hipEventRecord(l->ev_rescue, l->rescue_stream));
-        HIP_TRY(hipEventRecord(l->ev_fetched, l->rescue_stream));
-        l->rescue_used = true;
-        l->fetch_stream = l->rescue_stream;
-        l->src = l->rescue_buf;
+            HIP_TRY(hipMemcpyAsync(r.buf, peer_slot, nbytes, hipMemcpyDefault, r.stream));
+        HIP_TRY(hipEventRecord(r.ev_landed, r.stream));
+        HIP_TRY(hipEventRecord(l->ev_fetched, r.stream));
+        r.used = true;
+        l->fetch_stream = r.stream;
+        l->src = r.buf;
         l->src_copied = true;
-        l->src_stage = 2;
+        l->src_stage = 2 + j;
     } else if (zero_copy && ep.kind == 1 && ep.device == l->device) {
         l->src = peer_slot;             // read in place; stream order covers the rest
         l->src_copied = false;
@@ -986,6 +1037,11 @@ int dpwa_learner_factor(dpwa_learner *l, double loss, const double *loss_dev, dp
 static hipError_t staging_read(dpwa_learner *l, hipStream_t s)
 {
     if (l->src_stage < 0 || !l->src_copied) return hipSuccess;
+    if (l->src_stage >= 2) {
+        RescueLane &r = l->rescue[l->src_stage - 2];
+        r.read = true;
+        return hipEventRecord(r.ev_done, s);
+    }
     l->stage_read[l->src_stage] = true;
     return hipEventRecord(l->ev_stage_done[l->src_stage], s);
 }
@@ -1776,11 +1832,14 @@ int dpwa_learner_rescue_free(dpwa_learner *l, int *free_out)
 {
     if (!l || !free_out) return set_error(DPWA_ERR_ARG, "dpwa_learner_rescue_free: NULL argument");
     *free_out = 1;
-    if (!l->rescue_used) return DPWA_OK;
+    if (l->rescue_lanes < kRescueLanes) return DPWA_OK;     // a lane can still be made
     DeviceGuard dg(l->device);
-    const hipError_t e = hipEventQuery(l->ev_rescue);
-    if (e != hipSuccess && e != hipErrorNotReady) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(e));
-    *free_out = e == hipSuccess ? 1 : 0;
+    for (int j = 0; j < l->rescue_lanes; ++j) {
+        const hipError_t e = hipEventQuery(l->rescue[j].ev_landed);
+        if (e == hipSuccess) return DPWA_OK;
+        if (e != hipErrorNotReady) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(e));
+    }
+    *free_out = 0;
     return DPWA_OK;
 }
 

@@ -273,8 +273,9 @@ static int fetch_loop(dpwa_node *n, int flags, dpwa_stream_t stream, bool rescue
                                 (p.kind == PEER_LOCAL || via_board);
             int state = DPWA_FETCH_LANDED;
             if (rescue && judged) {
-                // the rescue buffer must be free: its last pull landed (else our own transport is
-                // stalled: wait up to the timeout, then this request times out and the round ends)
+                // a rescue lane must be free: its last pull landed, or another lane can be made
+                // (with every lane's pull stalled our own transport is stuck: wait up to the
+                // timeout, then this request times out and the round ends)
                 int free_ = 1;
                 const int64_t t0 = now_ms();
                 while ((rc = dpwa_learner_rescue_free(n->learner, &free_)) == DPWA_OK && !free_ &&

@@ -238,6 +238,8 @@ class DpwaConnection:
         _lib.call("dpwa_node_handles", self._node, None, ctypes.byref(sched))
         self._sched = Scheduler(len(self.peers), handle=sched.value)
         self._learner = None
+        self._resident = False      # make_resident was called
+        self._sent = None           # resident: (parameters tensor, its version) at update_send
         # transport of copying fetches: "copy" (hipMemcpyAsync) or "kernel[:blocks]"
         self._pull = pull if pull is not None else os.environ.get("DPWA_PULL", "copy")
         self._out = ctypes.c_int()
@@ -307,6 +309,9 @@ class DpwaConnection:
             self._fail("dpwa_node_update_send", rc)
         learner.version += 1
         self.fetching = bool(self._out.value)
+        if self._resident:      # the served snapshot: its version counter, checked at update_wait
+            t = learner.resident_params()
+            self._sent = (t, t._version)
         if not self._eager and getattr(self._group, "prefetch", False):
             self._group.after_update_send(self)
 
@@ -338,6 +343,8 @@ class DpwaConnection:
             return None, 0
         if learner.take_status():
             self._zero_division()
+        if self._sent is not None:
+            self._check_window()
         p = learner._ptr(parameters)
         h, d, learner._keep = learner.loss_args(loss)
         flags = self._flags | (_lib.FLAG_WRITE_THROUGH if write_through else 0)
@@ -345,6 +352,7 @@ class DpwaConnection:
         if rc:
             self._fail("dpwa_node_update_wait_average", rc)
         self.fetching = False
+        self._sent = None
         return self._result()
 
     # ---------------------------------------------------------------- extensions
@@ -354,14 +362,20 @@ class DpwaConnection:
         average reads them in the published slot and writes the next one -- 3*n*s bytes a round,
         the averaging's own.  Call before the first update_send; returns the tensor the
         parameters are in now (see ``parameters``).  From then on pass ``conn.parameters`` to
-        update_send / update_wait_average, re-read it after every update_wait_average (it
-        alternates between the two slots), and do not write it between update_send and
-        update_wait_average (it is the served snapshot then)."""
+        update_send / update_wait_average, re-read it after every update_send and
+        update_wait_average (it alternates between the two slots), and do not write it between
+        update_send and update_wait_average: it is the served snapshot then.  So the loop is
+        update_send, update_wait_average, step -- not the reference's update_send, step,
+        update_wait (README.md:18-29, main.py:130-145), which needs the write-through or full
+        form.  update_wait_average raises DpwaError when the tensor's version counter moved in
+        that window (an in-place op on it or on a view of it; writes through ``.data`` are not
+        counted)."""
         learner = self._learner if self._learner is not None else self._bind(parameters)
         stream = torch.cuda.current_stream(learner.device)
         learner._ptr(parameters)
         _lib.call("dpwa_node_set_resident", self._node, ctypes.c_void_p(parameters.data_ptr()),
                   ctypes.c_void_p(stream.cuda_stream))
+        self._resident = True
         return learner.resident_params()
 
     @property
@@ -401,6 +415,9 @@ class DpwaConnection:
             if len(calls) > 64:
                 calls.clear()
             calls[key] = cache
+        for c in conns:         # resident learners: nothing wrote the served snapshots (before any call)
+            if c._sent is not None:
+                c._check_window()
         out = [(None, 0)] * len(conns)
         keep = []
         for bound, dev_index, nodes, flats, hs, ds, peers, lib in cache:
@@ -420,6 +437,7 @@ class DpwaConnection:
                                                          torch._C._cuda_getCurrentRawStream(dev_index), peers)
             for i in bound:
                 conns[i].fetching = False
+                conns[i]._sent = None
             if rc:
                 raise _lib.DpwaError("dpwa_node_update_wait_average_many", rc,
                                      lib.dpwa_last_error().decode(errors="replace"))
@@ -566,6 +584,16 @@ class DpwaConnection:
         self._flags &= ~_lib.FLAG_PICK_ONLY
         _lib.call("dpwa_learner_set_pull", learner.handle, _lib.PULL_KERNEL if kind == "kernel" else
                   _lib.PULL_COPY_ENGINE, int(blocks or 512))
+
+    def _check_window(self):
+        t, v = self._sent
+        if t._version != v:
+            raise _lib.DpwaError(
+                "DpwaConnection.update_wait_average", _lib.ERR_STATE,
+                "the resident parameters were modified between update_send and update_wait (version %d -> %d); "
+                "they are the snapshot peers read in that window, so a resident loop runs update_send -> "
+                "update_wait -> step.  The reference's order update_send -> step -> update_wait (README.md, "
+                "main.py:130-145) needs the write-through or full form" % (v, t._version))
 
     def _zero_division(self):
         raise ZeroDivisionError("float division by zero (interpolation factor, dpwa.py:143-147)")

@@ -196,8 +196,10 @@ int dpwa_learner_attach_fds(dpwa_learner *l, int peer_id, const void *handle, in
 #define DPWA_FETCH_ZERO_COPY 1
 #define DPWA_FETCH_PUBLISHED 2
 /* DPWA_FETCH_RESCUE: the fetch re-selected after a timed-out pull (conn.py:304-309 reconnects and
- * picks again): it copies into a separate rescue buffer on a separate stream, so the stalled pull
- * ahead of it on the side stream cannot hold it up. */
+ * picks again): it copies into a rescue lane -- a buffer and a stream of the greatest priority of
+ * its own -- so the stalled pull ahead of it on the side stream cannot hold it up.  A lane whose
+ * pull has not landed stays taken and the next re-selected pull takes another (up to 3 lanes,
+ * allocated at first use, one snapshot each); DPWA_ERR_STATE when all are still pulling. */
 #define DPWA_FETCH_RESCUE 4
 int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int flags,
                        dpwa_stream_t stream);
@@ -205,8 +207,13 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
  * timeout_ms from the YAML, and its handling at conn.py:304-309).  fetch_state polls the copying
  * fetch in flight without blocking: DPWA_FETCH_LANDED (landed, or nothing to wait for),
  * DPWA_FETCH_IN_FLIGHT, or DPWA_FETCH_TIMED_OUT (still in flight timeout_ms after it was issued).
- * rescue_free: *free_out = 1 when the rescue buffer's last pull has landed.  fetch_stream: the
- * stream the fetch in flight moves its bytes on (side or rescue stream). */
+ * The clock starts when the host issues the pull, so for a pull ordered after the caller's
+ * stream (a local peer's snapshot, not through the board) a device backlog queued on that stream
+ * before update_send counts toward timeout_ms -- the reference's socket timeout measures only the
+ * reply; judged pulls are LocalGroup copying pulls and board pulls (which wait for nothing of
+ * the caller's).  rescue_free: *free_out = 1 when a rescue lane is free (its pull landed) or can
+ * still be allocated.  fetch_stream: the stream the fetch in flight moves its bytes on (side
+ * stream or a rescue lane's). */
 #define DPWA_FETCH_LANDED 0
 #define DPWA_FETCH_IN_FLIGHT 1
 #define DPWA_FETCH_TIMED_OUT 2
@@ -262,9 +269,14 @@ int dpwa_learner_reuse_guard_hits(dpwa_learner *l, uint32_t *hits);
  *   relocate          a round without an average: the parameters leave the published slot by one
  *                     copy into the next publish's slot (no-op when they are there).
  * Contract: the parameters ARE the served snapshot between a publish and the next average or
- * relocate, so they must not be written in that window (the reference's loop does not:
- * update_send, update_wait, then the training step).  A publish is given the resident pointer;
- * the split factor/lerp form is refused. */
+ * relocate, so they must not be written in that window.  The reference's own loop DOES write
+ * there (README.md:18-29, examples/pytorch-cifar/main.py:130-145: update_send, the training
+ * step, update_wait) and must use the write-through or full form; a resident learner needs the
+ * reordered loop update_send, update_wait, step (the same gossip with each step applied after
+ * the round's average instead of before it).  The Python layer records the parameters' version
+ * counters at update_send and raises at update_wait when any moved (DpwaConnection,
+ * DpwaPyTorchAdapter).  A publish is given the resident pointer; the split factor/lerp form is
+ * refused. */
 int dpwa_learner_set_resident(dpwa_learner *l, const void *init, dpwa_stream_t stream);
 int dpwa_learner_resident_params(dpwa_learner *l, void **params, int *slot);
 int dpwa_learner_relocate(dpwa_learner *l, dpwa_stream_t stream);
@@ -468,8 +480,11 @@ int dpwa_node_set_board(dpwa_node *n, dpwa_board *board, const int32_t *peer_ran
  * less than timeout_ms ago -> the reply with data (score +10, conn.py:301-302; a pull still in
  * flight is then waited for on the device); still in flight after timeout_ms -> a socket timeout
  * (score -100, reconnect, conn.py:304-309) and the loop picks again, the re-selected pull going
- * to the rescue buffer (DPWA_FETCH_RESCUE) and being polled on the host up to timeout_ms like
- * the reference's blocking receive.  Lock-step (DistGroup) pulls wait for the round's barrier,
+ * to a rescue lane (DPWA_FETCH_RESCUE) and being polled on the host up to timeout_ms like the
+ * reference's blocking receive; a rescue pull that times out too is followed by the next pick on
+ * another lane, until data, no peer, or every lane stalled (then the request times out and the
+ * round ends without data -- the reference would keep picking; the learner's own transport is
+ * what is stuck).  Lock-step (DistGroup) pulls wait for the round's barrier,
  * i.e. for the slowest learner, not for the peer, and are not judged. */
 int dpwa_node_set_timeout(dpwa_node *n, int timeout_ms);
 

@@ -417,10 +417,10 @@ def resnet_worker(rank, world, port, cfg_path, out_dir, T, group):
 
 def async_timeout_worker(rank, world, port, cfg_path, out_dir, n, T, hold_round, pull="copy"):
     """Free-running rounds (the gossip board) where rank 0's pull of round `hold_round` is held
-    on its side stream behind a ~0.6 s spin kernel and its update_wait comes 0.3 s later, past
-    the config's timeout_ms (100): that request times out (conn.py:304-309), the loop picks
-    again and the re-selected pull goes to the rescue buffer.  Records what async_worker
-    records plus the fetch attempts and scores."""
+    on its side stream behind a spin kernel (tests.helpers.Hold: HOLD_S from the measured spin
+    rate) and its update_wait comes HOST_WAIT_S later, past the config's timeout_ms (TIMEOUT_MS):
+    that request times out (conn.py:304-309), the loop picks again and the re-selected pull goes
+    to a rescue lane.  Records what async_worker records plus the fetch attempts and scores."""
     import ctypes
     import time
     import torch
@@ -431,6 +431,7 @@ def async_timeout_worker(rank, world, port, cfg_path, out_dir, n, T, hold_round,
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     from dpwa_amd import DpwaConnection, _lib
+    from tests.helpers import HOST_WAIT_S, Hold
     names = ["r%d" % i for i in range(world)]
     conn = DpwaConnection(names[rank], cfg_path, seed=710 + rank, group="async", pull=pull)
     flat = torch.empty(n, device=dev, dtype=torch.float32)
@@ -438,15 +439,14 @@ def async_timeout_worker(rank, world, port, cfg_path, out_dir, n, T, hold_round,
     params, clocks, peers, versions, scores, attempts = np.zeros((T, n), np.float32), np.zeros(T), [], [], [], []
     for r in range(T):
         flat.copy_(bases[r])
-        held = rank == 0 and r == hold_round
-        if held:
+        held = None
+        if rank == 0 and r == hold_round:
             s = ctypes.c_void_p()
             _lib.call("dpwa_learner_side_stream", conn._learner.handle, ctypes.byref(s))
-            with torch.cuda.stream(torch.cuda.ExternalStream(s.value, device=dev)):
-                torch.cuda._sleep(1_500_000_000)        # this round's pull queues behind it
+            held = Hold(torch.cuda.ExternalStream(s.value, device=dev))   # this round's pull queues behind it
         conn.update_send(flat, async_loss(rank, r))
         if held:
-            time.sleep(0.3)                             # past timeout_ms
+            time.sleep(HOST_WAIT_S)                     # past timeout_ms
         payload, _ = conn.update_wait_average(flat, async_loss(rank, r, wait=True))
         peers.append(payload.peer if payload is not None else "")
         versions.append(conn._info()[2] if payload is not None else 0)
@@ -456,6 +456,7 @@ def async_timeout_worker(rank, world, port, cfg_path, out_dir, n, T, hold_round,
         scores.append([conn.flow_control_scores()[p] for p in names if p != names[rank]])
         if held:
             torch.cuda.synchronize()                    # the stalled pull has landed
+            held.check(HOST_WAIT_S)
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), params=params, clocks=clocks, peers=np.array(peers),
              versions=np.array(versions, dtype=np.int64), attempts=np.array(attempts),

@@ -25,6 +25,7 @@ Outputs (all small; see tests/golden/README.md):
   peer_select.json      TxThread peer choice + flow control under scripted faults (conn.py:224-317)
   peer_add.json         the same with removed peers put back by add_peer (dpwa.py:95-96, conn.py:208-213)
   gossip.npz/.json      lock-step G-learner gossip through the real adapter + connection + TxThread
+  gossip_step_after_wait.npz/.json   the same with the step after update_wait (the resident order)
   wire.json             <HLL + pickle frames (dpwa/messaging.py:24-94)
   config.json           YAML parsing (dpwa/dpwa.py:29-93)
 
@@ -547,24 +548,40 @@ def gen_peer_add(tmp):
 GOSSIP_SHAPES = [(8, 5), (8,), (4, 2, 3, 3), (4,), (4,), (3, 17), (3,)]
 
 
-def gen_gossip(tmp):
+GOSSIP_CASES = [("constant", 0.5, 0.0, 1.0, 4), ("clock", None, 0.0, 1.0, 4),
+                ("loss", None, 0.5, 0.7, 4), ("constant", 0.25, 0.5, 0.7, 3), ("clock", None, 0.5, 1.0, 8)]
+# the loop order resident parameters need (update_send -> update_wait -> step): G = 3 and 4,
+# clock and loss interpolation, fetch_probability 0.7
+GOSSIP_STEP_AFTER_WAIT_CASES = [("clock", None, 0.0, 0.7, 3), ("loss", None, 0.5, 0.7, 4),
+                                ("clock", None, 0.5, 0.7, 4), ("loss", None, 0.0, 0.7, 3)]
+
+
+def gen_gossip(tmp, step_after_wait=False):
+    """Lock-step rounds through the real adapter.  README order (README.md:18-29,
+    main.py:130-145): update_send, training step, update_wait.  step_after_wait: the same
+    adapter calls with the step after update_wait (update_send, update_wait, step -- the
+    reference runs either order: pytorch.py:42-68 and dpwa.py:104-156 never look at what
+    happened in between); the recorded parameters are then the ones update_wait left, before
+    the round's step."""
     npz = {}
-    meta = {"shapes": GOSSIP_SHAPES, "cases": []}
-    cases = [("constant", 0.5, 0.0, 1.0, 4), ("clock", None, 0.0, 1.0, 4),
-             ("loss", None, 0.5, 0.7, 4), ("constant", 0.25, 0.5, 0.7, 3), ("clock", None, 0.5, 1.0, 8)]
+    meta = {"shapes": GOSSIP_SHAPES, "cases": [],
+            "order": "update_send, update_wait, step" if step_after_wait else "update_send, step, update_wait"}
+    cases = GOSSIP_STEP_AFTER_WAIT_CASES if step_after_wait else GOSSIP_CASES
+    base_port = 50000 if step_after_wait else 49000
+    seed_base = 300 if step_after_wait else 100
     n = sum(int(np.prod(s)) for s in GOSSIP_SHAPES)
     T = 8
     for ci, (interp, val, thr, fp, G) in enumerate(cases):
-        nodes = make_nodes(G, base_port=49000 + 32 * ci)
+        nodes = make_nodes(G, base_port=base_port + 32 * ci)
         for nd in nodes:
             ADDR2NAME[(nd["host"], nd["port"])] = nd["name"]
         cfg = os.path.join(tmp, "gossip_%d.yaml" % ci)
         write_config(cfg, nodes, fp, interp, thr, extra=val)
-        rng = np.random.default_rng(100 + ci)
+        rng = np.random.default_rng(seed_base + ci)
         names = [nd["name"] for nd in nodes]
         init = rng.standard_normal((G, n)).astype(np.float32)
         deltas = (0.01 * rng.standard_normal((T, G, n))).astype(np.float32)
-        lrng = random.Random(55 + ci)
+        lrng = random.Random(seed_base - 45 + ci)
         send_loss = [[2 * math.exp(-r / 3.0) + 0.05 * lrng.random() for _ in range(G)] for r in range(T)]
         wait_loss = [[2 * math.exp(-(r + 0.5) / 3.0) + 0.05 * lrng.random() for _ in range(G)] for r in range(T)]
         nets, adapters, conns = [], [], []
@@ -572,7 +589,7 @@ def gen_gossip(tmp):
         for g, name in enumerate(names):
             net = Net(GOSSIP_SHAPES)
             load_flat(net, init[g])
-            conn = new_connection(cfg, name, 1000 + g, real_tx=True)
+            conn = new_connection(cfg, name, 10 * seed_base + g, real_tx=True)
             nets.append(net)
             conns.append(conn)
             adapters.append(adapter_for(net, conn))
@@ -598,13 +615,17 @@ def gen_gossip(tmp):
                 adapters[g].update_send(send_loss[r][g])          # publish + Bernoulli + fetch_send
                 fetching[r, g] = conns[g].fetching
             ENV.gate.set()                                       # every learner has published round r
-            for g in range(G):
-                with torch.no_grad():                            # the "training step"
-                    off = 0
-                    for _, p in nets[g].named_parameters():
-                        k = p.numel()
-                        p.data.add_(torch.from_numpy(deltas[r, g, off:off + k]).view(p.shape))
-                        off += k
+
+            def train():
+                for g in range(G):
+                    with torch.no_grad():                        # the "training step"
+                        off = 0
+                        for _, p in nets[g].named_parameters():
+                            k = p.numel()
+                            p.data.add_(torch.from_numpy(deltas[r, g, off:off + k]).view(p.shape))
+                            off += k
+            if not step_after_wait:
+                train()
             for g in range(G):
                 RNG.set_current(names[g])
                 c = conns[g]
@@ -625,6 +646,8 @@ def gen_gossip(tmp):
                 params[r, g] = flat_params(nets[g])
             for g in range(G):
                 picks[r][g] = [a["peer"] for a in ENV.logs[names[g]]]
+            if step_after_wait:
+                train()
         for c in conns:
             c.tx._queue.put(False)
         ENV.gate = None
@@ -637,12 +660,17 @@ def gen_gossip(tmp):
         npz[key + "_fetching"] = fetching
         meta["cases"].append({"key": key, "interpolation": interp, "value": val,
                               "divergence_threshold": thr, "fetch_probability": fp, "G": G,
-                              "names": names, "seeds": [1000 + g for g in range(G)],
+                              "names": names, "seeds": [10 * seed_base + g for g in range(G)],
                               "send_loss": send_loss, "wait_loss": wait_loss, "picks": picks})
-    np.savez_compressed(os.path.join(OUT, "gossip.npz"), **npz)
-    with open(os.path.join(OUT, "gossip.json"), "wt") as f:
+    stem = "gossip_step_after_wait" if step_after_wait else "gossip"
+    np.savez_compressed(os.path.join(OUT, stem + ".npz"), **npz)
+    with open(os.path.join(OUT, stem + ".json"), "wt") as f:
         json.dump(meta, f, indent=0)
-    print("gossip: %d cases" % len(meta["cases"]))
+    print("%s: %d cases" % (stem, len(meta["cases"])))
+
+
+def gen_gossip_step_after_wait(tmp):
+    gen_gossip(tmp, step_after_wait=True)
 
 
 # ----------------------------------------------------------------------------
@@ -800,6 +828,7 @@ def main():
         gen_peer_select(tmp)
         gen_peer_add(tmp)
         gen_gossip(tmp)
+        gen_gossip_step_after_wait(tmp)
         gen_wire()
         gen_wire_adapter()
         gen_config(tmp)

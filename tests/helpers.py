@@ -60,3 +60,52 @@ class AttemptReplay:
 
     def done(self):
         return self.i == len(self.attempts)
+
+
+# ---- measured holds for the fetch-timeout tests (test_gpu_timeout.py, dist_worker.py) ----------
+TIMEOUT_MS = 100                 # the YAML's timeout_ms in the timed-out rounds
+HOST_WAIT_S = 0.3                # the host waits this long after update_send: 3 x timeout_ms
+HOLD_S = 0.9                     # a held pull's spin: 3 x the host wait
+assert HOST_WAIT_S >= 3 * TIMEOUT_MS / 1e3 and HOLD_S >= 3 * HOST_WAIT_S
+
+
+def sleep_rate():
+    """torch.cuda._sleep cycles per second on this box: two spins of different length timed by
+    events, the rate from their difference (launch overhead cancels)."""
+    import torch
+
+    def timed(cycles):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        torch.cuda._sleep(cycles)
+        b.record()
+        b.synchronize()
+        return a.elapsed_time(b) * 1e-3
+    timed(10_000_000)
+    short, long_ = timed(20_000_000), timed(220_000_000)
+    return 200_000_000 / max(long_ - short, 1e-6)
+
+
+class Hold:
+    """A spin of `seconds` (from the measured rate) on `stream`, timed by events, so the test can
+    state afterwards how long the pull behind it was really held."""
+    rate = None
+
+    def __init__(self, stream, seconds=HOLD_S):
+        import torch
+        if Hold.rate is None:
+            Hold.rate = sleep_rate()
+        self.seconds = seconds
+        self.a, self.b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(stream):
+            self.a.record()
+            torch.cuda._sleep(int(seconds * Hold.rate))
+            self.b.record()
+
+    def check(self, waited_s):
+        """After the round: the hold outlasted the host's wait past the deadline by >= 2x."""
+        held = self.a.elapsed_time(self.b) * 1e-3
+        assert held >= 2 * waited_s, ("the hold lasted %.0f ms, under 2 x the host's %.0f ms wait past the %d ms "
+                                      "deadline (spin rate %.3g cycles/s): the held pull may have landed before it "
+                                      "was judged" % (1e3 * held, 1e3 * waited_s, TIMEOUT_MS, Hold.rate))
+        return held

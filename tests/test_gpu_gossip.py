@@ -101,6 +101,59 @@ def test_gossip_matches_reference_trajectories(tmp_path):
         assert olerp.bits_equal(got["params"], z[k + "_params"]), k
 
 
+@pytest.mark.parametrize("form", ["resident", "resident-many", "write-through"])
+def test_step_after_wait_matches_reference_trajectories(tmp_path, form):
+    """The reference driven update_send -> update_wait -> step (tests/golden/gossip_step_after_wait.*:
+    G = 3 and 4, clock and loss interpolation, fetch_probability 0.7): the resident adapter (one by
+    one and batched) and the write-through adapter replay it bit for bit -- parameters after every
+    update_wait, clocks, factors, fetch gates and peers."""
+    meta = load_json("gossip_step_after_wait.json")
+    z = load_npz("gossip_step_after_wait.npz")
+    shapes = [tuple(s) for s in meta["shapes"]]
+    for case in meta["cases"]:
+        k, names, G = case["key"], case["names"], case["G"]
+        cfg = tmp_path / ("%s_%s.yaml" % (k, form))
+        write_cfg(cfg, names, case["fetch_probability"], case["interpolation"], case["divergence_threshold"],
+                  case["value"])
+        init, deltas = z[k + "_init"], z[k + "_deltas"]
+        group = LocalGroup()
+        nets, ads = [], []
+        for g in range(G):
+            net = Net(shapes).to(DEV)
+            load_flat(net, init[g])
+            nets.append(net)
+            ads.append(DpwaPyTorchAdapter(net, names[g], str(cfg), seed=case["seeds"][g], group=group,
+                                          resident=form.startswith("resident")))
+        for r in range(deltas.shape[0]):
+            fetching = []
+            for g in range(G):
+                ads[g].update_send(case["send_loss"][r][g])
+                fetching.append(ads[g].connection.fetching)
+            assert fetching == list(z[k + "_fetching"][r]), (k, r)
+            if form == "resident-many":
+                DpwaPyTorchAdapter.update_wait_many(ads, case["wait_loss"][r])
+            else:
+                for g in range(G):
+                    ads[g].update_wait(case["wait_loss"][r][g])
+            for g in range(G):
+                c = ads[g].connection
+                fetched = fetching[g] and c.last_fetch_peer is not None
+                assert ([c.last_fetch_peer] if fetched else []) == case["picks"][r][g], (k, r, g)
+                factor = float(c._learner.read_coef().factor) if fetched else 0.0
+                assert factor == z[k + "_factors"][r, g], (k, r, g)
+                assert c.clock == z[k + "_clocks"][r, g], (k, r, g)
+                assert olerp.bits_equal(flat_params(nets[g]), z[k + "_params"][r, g]), (k, r, g)
+            for g in range(G):          # the training step, after update_wait
+                with torch.no_grad():
+                    off = 0
+                    for _, p in nets[g].named_parameters():
+                        n = p.numel()
+                        p.add_(torch.from_numpy(deltas[r, g, off:off + n]).to(DEV).view(p.shape))
+                        off += n
+        for a in ads:
+            a.connection.close()
+
+
 def test_gossip_longer_run_matches_oracle(tmp_path):
     """A longer synthetic run (loss interpolation, divergence threshold, p<1) against the
     oracle's lock-step simulation."""

@@ -1,10 +1,13 @@
 """Resident parameters (dpwa_learner_set_resident, include/dpwa_hip.h): a learner's parameters
 live in its own two snapshot slots, publishes move no bytes and every average reads the
-published slot and writes the other one.  The rounds must stay exactly the reference's
-(README.md:18-29 loop order: update_send, update_wait, training step) -- parameters, clocks and
-peers bit-exact with oracle/gossip.py, snapshots served as they were at update_send -- whether
-the averages run one by one or batched, with rounds that have no fetch (fetch_probability < 1),
-and through the adapter."""
+published slot and writes the other one.  That needs the loop order update_send, update_wait,
+training step -- NOT the reference's README order (README.md:18-29, main.py:130-145: update_send,
+step, update_wait), which trains while peers read the snapshot and keeps the write-through form.
+In the resident order the rounds must match the reference driven that way
+(tests/golden/gossip_step_after_wait.*, via oracle/gossip.py train_after_wait) -- parameters,
+clocks and peers bit-exact, snapshots served as they were at update_send -- whether the averages
+run one by one or batched, with rounds that have no fetch (fetch_probability < 1), and through
+the adapter; a write in the send -> wait window is refused."""
 import ctypes
 
 import numpy as np
@@ -263,3 +266,106 @@ def test_resident_pointer_api():
     del got
     for h in ls:
         _lib.call("dpwa_learner_destroy", h)
+
+
+def test_resident_refuses_a_write_between_send_and_wait(tmp_path):
+    """The reference's own order (update_send, optimizer step, update_wait; main.py:130-145) under
+    resident=True would serve peers a snapshot being trained: update_wait raises DpwaError naming
+    the order instead -- through the adapter (SGD step), the batched adapter call, and the
+    connection (an in-place op on conn.parameters) -- and nothing was averaged.  The resident
+    order (step after update_wait) keeps working, and so does the write-through adapter in the
+    reference order."""
+    names = ["v0", "v1"]
+    cfg = tmp_path / "win.yaml"
+    _write_cfg(cfg, names, 1.0, "constant")
+    torch.manual_seed(3)
+    for many in (False, True):
+        nets = [torch.nn.Sequential(torch.nn.Linear(6, 9), torch.nn.Linear(9, 2)).to(DEV) for _ in names]
+        grp = LocalGroup()
+        ads = [DpwaPyTorchAdapter(nets[g], names[g], str(cfg), seed=80 + g, group=grp, resident=True)
+               for g in range(2)]
+        opts = [torch.optim.SGD(n.parameters(), lr=0.1) for n in nets]
+
+        def sgd_step(g):
+            opts[g].zero_grad()
+            nets[g](torch.randn(3, 6, device=DEV)).sum().backward()
+            opts[g].step()
+
+        for r in range(2):      # the resident order works
+            for ad in ads:
+                ad.update_send(1.0)
+            if many:
+                DpwaPyTorchAdapter.update_wait_many(ads, [1.0, 1.0])
+            else:
+                for ad in ads:
+                    ad.update_wait(1.0)
+            for g in range(2):
+                sgd_step(g)
+        for ad in ads:
+            ad.update_send(1.0)
+        before = ads[1].connection.parameters.clone()
+        sgd_step(1)                                             # the reference's step position
+        with pytest.raises(_lib.DpwaError, match="update_send -> update_wait -> step"):
+            if many:
+                DpwaPyTorchAdapter.update_wait_many(ads, [1.0, 1.0])
+            else:
+                ads[0].update_wait(1.0)                          # untouched: averages
+                ads[1].update_wait(1.0)
+        assert not torch.equal(ads[1].connection.parameters, before)  # the step's write, not an average
+        torch.cuda.synchronize()
+        for ad in ads:
+            ad.connection.close()
+    # the connection-level form: an in-place write of the resident tensor in the window
+    group = LocalGroup()
+    conns = [DpwaConnection(names[g], str(cfg), seed=90 + g, group=group) for g in range(2)]
+    for g in range(2):
+        conns[g].make_resident(torch.full((5000,), float(g), device=DEV))
+    for c in conns:
+        c.update_send(c.parameters, 1.0)
+    conns[0].parameters[7:9].mul_(2.0)                         # a view shares the version counter
+    with pytest.raises(_lib.DpwaError, match="modified between update_send and update_wait"):
+        DpwaConnection.update_wait_average_many(conns, [c.parameters for c in conns], [1.0, 1.0])
+    with pytest.raises(_lib.DpwaError):
+        conns[0].update_wait_average(conns[0].parameters, 1.0)
+    conns[1].update_wait_average(conns[1].parameters, 1.0)     # its own window is clean
+    torch.cuda.synchronize()
+    for c in conns:
+        c.close()
+
+
+def test_resident_adapter_second_publish_without_wait_follows_the_parameters(tmp_path):
+    """Two update_sends with no update_wait between them: the second publish relocates the
+    parameters into the slot it publishes (dpwa_learner_relocate), and the adapter re-points
+    every parameter there, so the next update_wait averages them where they are and the
+    optimizer keeps training the live tensor."""
+    names = ["q0", "q1"]
+    cfg = tmp_path / "twice.yaml"
+    _write_cfg(cfg, names, 1.0, "constant")
+    torch.manual_seed(4)
+    nets = [torch.nn.Linear(5, 3).to(DEV) for _ in names]
+    grp = LocalGroup()
+    ads = [DpwaPyTorchAdapter(nets[g], names[g], str(cfg), seed=95 + g, group=grp, resident=True) for g in range(2)]
+    for ad in ads:
+        ad.update_send(1.0)
+    for ad in ads:
+        ad.update_wait(1.0)
+    ads[0].update_send(1.0)
+    home = ads[0].connection.parameters.data_ptr()
+    ads[0].update_send(1.0)                                     # again, no average in between
+    moved = ads[0].connection.parameters
+    assert moved.data_ptr() != home
+    for p in nets[0].parameters():
+        assert moved.data_ptr() <= p.data_ptr() < moved.data_ptr() + moved.numel() * 4
+    ads[1].update_send(1.0)
+    peer = ads[1].connection.parameters.clone()
+    mine = moved.clone()
+    for ad in ads:
+        ad.update_wait(1.0)
+    want = (0.5 * peer) + (0.5 * mine)                          # pytorch.py:68, fp32
+    assert torch.equal(ads[0].connection.parameters, want)
+    w = next(nets[0].parameters())
+    lo = ads[0].connection.parameters.data_ptr()
+    assert lo <= w.data_ptr() < lo + want.numel() * 4
+    torch.cuda.synchronize()
+    for ad in ads:
+        ad.connection.close()

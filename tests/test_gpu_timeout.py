@@ -3,9 +3,15 @@ YAML's timeout_ms; conn.py:304-309 handles it: score -100, disconnect, pick agai
 
 A pull is held back on the learner's side stream by a long spin kernel queued ahead of it, and
 update_wait polls it after the deadline: the round must score that peer -100, pick again, pull
-the re-selected peer into the rescue buffer and average with it -- peers, scores, clocks and
+the re-selected peer into a rescue lane and average with it -- peers, scores, clocks and
 parameters against the oracle policy with that request scripted as a timeout.  A pull that is
-merely slower than the host (the normal case) is never judged a timeout."""
+merely slower than the host (the normal case) is never judged a timeout.
+
+The margins come from a measurement, not from an assumed clock: the spin kernel's rate
+(torch.cuda._sleep cycles per second) is measured on the box first, a hold is sized in seconds
+from it, and every held round checks afterwards, from events around the spin, that the hold
+outlasted the host's wait past the deadline by the stated factor (so a held pull was still in
+flight when it was judged)."""
 import ctypes
 
 import numpy as np
@@ -20,7 +26,7 @@ from oracle.policy import OracleLearner
 pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda", 0)
-HOLD_CYCLES = 1_500_000_000      # ~0.6 s of spinning on the side stream (torch.cuda._sleep)
+from tests.helpers import HOLD_S, HOST_WAIT_S, TIMEOUT_MS, Hold  # noqa: E402  (measured spin holds)
 
 
 def write_cfg(path, names, timeout_ms, interp="clock"):
@@ -73,7 +79,7 @@ def expected(names, init, send, wait, seeds, timeouts):
 def test_held_pull_times_out_and_the_loop_picks_again(tmp_path, pull, G):
     names = ["t%d" % g for g in range(G)]
     cfg = tmp_path / "to.yaml"
-    write_cfg(cfg, names, timeout_ms=100)
+    write_cfg(cfg, names, timeout_ms=TIMEOUT_MS)
     rng = np.random.default_rng(3)
     n, T = 100_003, 4
     init = rng.standard_normal((G, n)).astype(np.float32)
@@ -87,16 +93,15 @@ def test_held_pull_times_out_and_the_loop_picks_again(tmp_path, pull, G):
     flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
     import time
     for r in range(T):
-        for g in range(G):
-            if (r, g) in held:
-                with torch.cuda.stream(side_stream(conns[g])):
-                    torch.cuda._sleep(HOLD_CYCLES)       # the next pull of learner g queues behind this
+        holds = [Hold(side_stream(conns[g])) for g in range(G) if (r, g) in held]   # the next pull queues behind it
         for g in range(G):
             conns[g].update_send(flats[g], send[r][g])
-        if any(h[0] == r for h in held):
-            time.sleep(0.3)                              # past the 100 ms deadline
+        if holds:
+            time.sleep(HOST_WAIT_S)                      # past the deadline
         got = [conns[g].update_wait_average(flats[g], wait[r][g]) for g in range(G)]
         torch.cuda.synchronize()                         # (the held pull has landed before the next round)
+        for h in holds:
+            h.check(HOST_WAIT_S)
         params, clocks, scores, row = exp[r]
         for g in range(G):
             assert (got[g][0].peer if got[g][0] is not None else "") == row[g][0], (r, g)
@@ -128,14 +133,16 @@ def test_slow_but_in_time_pull_is_data(tmp_path):
     conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group) for g in range(G)]
     flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
     for r in range(T):
-        if r > 0:
-            for g in range(G):
-                with torch.cuda.stream(side_stream(conns[g])):
-                    torch.cuda._sleep(50_000_000)        # ~20 ms: slower than the host, inside the timeout
+        # ~20 ms: slower than the host, well inside the 5 s timeout
+        holds = [Hold(side_stream(conns[g]), 0.02) for g in range(G)] if r > 0 else []
         for g in range(G):
             conns[g].update_send(flats[g], send[r][g])
         for g in range(G):
             conns[g].update_wait_average(flats[g], wait[r][g])
+        torch.cuda.synchronize()
+        for h in holds:
+            held = h.a.elapsed_time(h.b)
+            assert held < 5000 / 10, "the hold lasted %.0f ms, not well inside the 5000 ms timeout" % held
         params, clocks, scores, _ = exp[r]
         for g in range(G):
             assert olerp.bits_equal(flats[g].cpu().numpy(), params[g]), (r, g)
@@ -169,7 +176,7 @@ def test_board_pull_times_out_and_the_rescue_pull_reads_a_whole_snapshot(tmp_pat
     names = ["r%d" % i for i in range(world)]
     cfg = str(tmp_path / "to_board.yaml")
     dist_worker.write_cfg(cfg, names, 1.0, "constant", 0.0)
-    text = open(cfg).read().replace("- timeout_ms: 2500", "- timeout_ms: 100")
+    text = open(cfg).read().replace("- timeout_ms: 2500", "- timeout_ms: %d" % TIMEOUT_MS)
     open(cfg, "w").write(text)
     mp.spawn(dist_worker.async_timeout_worker, args=(world, _free_port(), cfg, str(tmp_path), n, T, hold, pull),
              nprocs=world, join=True)
@@ -197,88 +204,97 @@ def test_board_pull_times_out_and_the_rescue_pull_reads_a_whole_snapshot(tmp_pat
 
 
 def _stalled_rescue(_rank, tmp):
+    """See test_stalled_rescue_pulls_take_the_next_lane.  Rounds (learner 0): 1: its side stream
+    held -> timeout, the re-selected pull on rescue lane 0 -> data; 2: side stream and lane 0 held
+    -> two timeouts, lane 1 -> data; 3: side, lanes 0 and 1 held -> three timeouts, lane 2 ->
+    data; 4: side and all three lanes held -> four timeouts, then no lane is free within the
+    timeout: that request times out and the round ends without data (five timeouts)."""
     import pathlib
+    import time
     tmp_path = pathlib.Path(tmp)
     G = 3
     names = ["x%d" % g for g in range(G)]
     cfg = tmp_path / "stall.yaml"
-    write_cfg(cfg, names, timeout_ms=100)
+    write_cfg(cfg, names, timeout_ms=TIMEOUT_MS)
     rng = np.random.default_rng(5)
-    n, T = 50_003, 3
+    n, T = 50_003, 5
     init = rng.standard_normal((G, n)).astype(np.float32)
     send = [[1.0 + g + r for g in range(G)] for r in range(T)]
     wait = [[2.0 + g + r for g in range(G)] for r in range(T)]
     seeds = [90 + g for g in range(G)]
-    # the oracle: round 1 of learner 0 -> one timeout then data; round 2 -> three timeouts, no data
+    timeouts = {1: 1, 2: 2, 3: 3, 4: 5}        # learner 0: its first k requests of round r time out
     idx = {nm: i for i, nm in enumerate(names)}
     L = [OracleLearner(names[g], [x for x in names if x != names[g]], 1.0, "clock", None, 0.0, seeds[g])
          for g in range(G)]
     params = init.copy()
-    exp, picks = [], []
+    exp = []
     for r in range(T):
         states = [L[g].update_send(send[r][g]) for g in range(G)]
         snaps = [params[g].copy() for g in range(G)]
+        picks = []
         for g in range(G):
             n_req = [0]
 
             def request(peer, g=g, r=r, n_req=n_req):
                 n_req[0] += 1
-                if g == 0 and ((r == 1 and n_req[0] == 1) or r == 2):
+                if g == 0 and n_req[0] <= timeouts.get(r, 0):
                     return "timeout", None, None
                 return "payload", states[idx[peer]], snaps[idx[peer]]
 
             state, payload, attempts = L[g].fetch(lambda p: "ok", request,
-                                                  max_attempts=3 if (g == 0 and r == 2) else None)
+                                                  max_attempts=5 if (g == 0 and r == 4) else None)
             averaged, factor = L[g].update_wait(wait[r][g], state, payload is not None)
             if averaged:
                 params[g] = olerp.lerp_f32(params[g], payload, factor)
             picks.append([a["peer"] for a in attempts])
         exp.append((params.copy(), [L[g].clock for g in range(G)],
-                    [L[g].scores([x for x in names if x != names[g]]) for g in range(G)], picks[-G:]))
+                    [L[g].scores([x for x in names if x != names[g]]) for g in range(G)], picks))
     group = LocalGroup(prefetch=True, zero_copy=False)
     conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group) for g in range(G)]
     flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
-    import time
-    rescue = None
+    lanes = []                                      # rescue lane streams, in the order they appear
     for r in range(T):
-        if r in (1, 2):
-            with torch.cuda.stream(side_stream(conns[0])):
-                torch.cuda._sleep(HOLD_CYCLES)
-        if r == 2:
-            with torch.cuda.stream(rescue):
-                torch.cuda._sleep(2 * HOLD_CYCLES)       # the rescue pull queues behind this
+        holds = []
+        if r >= 1:
+            holds.append(Hold(side_stream(conns[0])))
+            # lane j's pull is judged after the side pull's HOST_WAIT_S and j earlier rescue polls
+            holds += [Hold(s, HOLD_S + (j + 1) * 0.3) for j, s in enumerate(lanes[:r - 1])]
         for g in range(G):
             conns[g].update_send(flats[g], send[r][g])
-        if r in (1, 2):
-            time.sleep(0.3)
+        if r >= 1:
+            time.sleep(HOST_WAIT_S)
         got = [conns[g].update_wait_average(flats[g], wait[r][g]) for g in range(G)]
-        if r == 1:   # the stream the rescue pull ran on
+        if 1 <= r <= 3:   # the stream the rescue pull that delivered ran on: a new lane
             s = ctypes.c_void_p()
             _lib.call("dpwa_learner_fetch_stream", conns[0]._learner.handle, ctypes.byref(s))
-            rescue = torch.cuda.ExternalStream(s.value, device=DEV)
-            assert rescue.cuda_stream != side_stream(conns[0]).cuda_stream
+            assert s.value not in [x.cuda_stream for x in lanes] + [side_stream(conns[0]).cuda_stream], r
+            lanes.append(torch.cuda.ExternalStream(s.value, device=DEV))
         torch.cuda.synchronize()
+        if holds:
+            holds[0].check(HOST_WAIT_S)
+            for j, h in enumerate(holds[1:]):       # lane j's pull is judged HOST_WAIT_S + (j+1) timeouts in
+                h.check(HOST_WAIT_S + (j + 1) * TIMEOUT_MS / 1e3)
         p_exp, c_exp, s_exp, pk_exp = exp[r]
-        if r == 2:
-            assert got[0][0] is None and conns[0].last_fetch_attempts == 3
         for g in range(G):
             peer = got[g][0].peer if got[g][0] is not None else ""
-            assert (peer, conns[g].last_fetch_attempts) == ((pk_exp[g][-1] if g or r != 2 else ""), len(pk_exp[g])), \
+            want = pk_exp[g][-1] if (g or r != 4) else ""
+            assert (peer, conns[g].last_fetch_attempts) == (want, len(pk_exp[g])), \
                 (r, g, peer, conns[g].last_fetch_attempts, pk_exp[g])
             assert conns[g].flow_control_scores() == dict(zip([x for x in names if x != names[g]], s_exp[g])), (r, g)
             assert olerp.bits_equal(flats[g].cpu().numpy(), p_exp[g]), (r, g)
             assert conns[g].clock == c_exp[g], (r, g)
-            assert conns[g].flow_control_scores() == dict(zip([x for x in names if x != names[g]], s_exp[g])), (r, g)
+    assert len(lanes) == 3
     for c in conns:
         c.close()
 
 
-def test_stalled_rescue_pull_ends_the_round_without_data(tmp_path):
-    """Both the side stream and the rescue stream stalled: the first pull times out, the
-    re-selected rescue pull times out too, and the next pick finds the rescue buffer still
-    taken -- that request times out and the round ends without data (the learner's own
-    transport is stuck; the reference would keep picking).  Three timeouts, -100 each, no average
-    -- the oracle policy with three scripted timeouts and the loop cut after them.  Runs in a
-    fresh process (a stream map of its own).""" 
+def test_stalled_rescue_pulls_take_the_next_lane(tmp_path):
+    """TxThread keeps re-selecting after a timeout until data, no peer, or every peer removed
+    (conn.py:286-313).  Here a re-selected pull whose rescue lane is stalled times out too and the
+    next pick goes to another lane: with the side stream and one, then two rescue lanes held, the
+    round still ends with data from the next pick -- peers, attempts, scores, clocks and parameters
+    as the oracle policy with those requests scripted as timeouts.  Only with all three lanes held
+    (the learner's own transport stuck) does the next request time out and the round end without
+    data: five timeouts, -100 each.  Runs in a fresh process (a stream map of its own)."""
     import torch.multiprocessing as mp
     mp.spawn(_stalled_rescue, args=(str(tmp_path),), nprocs=1, join=True)

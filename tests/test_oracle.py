@@ -127,6 +127,31 @@ def test_gossip_trajectories_match_reference():
         assert olerp.bits_equal(res["params"], z[k + "_params"]), k
 
 
+def test_gossip_step_after_wait_trajectories_match_reference():
+    """The resident loop order (update_send, update_wait, step) from reference runs
+    (make_golden.py gen_gossip_step_after_wait: the real adapter, connection and TxThread driven
+    in that order, pytorch.py:42-68, dpwa.py:104-156) against oracle/gossip.py
+    train_after_wait=True, bit for bit; and the README-order oracle does not reproduce it."""
+    meta = load_json("gossip_step_after_wait.json")
+    z = load_npz("gossip_step_after_wait.npz")
+    assert meta["order"] == "update_send, update_wait, step"
+    assert {c["G"] for c in meta["cases"]} == {3, 4}
+    assert {c["interpolation"] for c in meta["cases"]} == {"clock", "loss"}
+    for case in meta["cases"]:
+        k = case["key"]
+        args = (case["names"], z[k + "_init"], z[k + "_deltas"], case["send_loss"], case["wait_loss"],
+                case["interpolation"], case["value"], case["divergence_threshold"], case["fetch_probability"],
+                case["seeds"])
+        res = ogossip.simulate(*args, train_after_wait=True)
+        assert res["picks"] == case["picks"], k
+        assert np.array_equal(res["fetching"], z[k + "_fetching"]), k
+        assert np.array_equal(res["factors"], z[k + "_factors"]), k
+        assert np.array_equal(res["clocks"], z[k + "_clocks"]), k
+        assert olerp.bits_equal(res["params"], z[k + "_params"]), k
+        other = ogossip.simulate(*args)
+        assert not olerp.bits_equal(other["params"], z[k + "_params"]), k
+
+
 def test_fixture_files_are_data_only():
     """Fixtures are inputs/outputs (json/npz), never reference source."""
     import os
