@@ -93,7 +93,7 @@ __global__ __launch_bounds__(BLOCK) void k_copy(Args a)
 
 // ---- averaging shapes ------------------------------------------------------------------
 // U items per lane, block span BLOCK*16*U, all loads first; DUAL also stores into snap.
-template <int BLOCK, int U, bool DUAL, int AUXP = NT, int AUXS = SC1>
+template <int BLOCK, int U, bool DUAL, int AUXP = NT, int AUXS = SC1, int AUXN = AUXS>
 __global__ __launch_bounds__(BLOCK) void k_avg(Args a)
 {
     const int64_t span = (int64_t)BLOCK * 16 * U;
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(BLOCK) void k_avg(Args a)
     for (int u = 0; u < U; ++u) {
         const f32x4 r = lerp4(0.5f, 0.5f, q[u], p[u]);
         st<AUXS>(rp, threadIdx.x * 16 + u * BLOCK * 16, r);
-        if (DUAL) st<AUXS>(rs, threadIdx.x * 16 + u * BLOCK * 16, r);
+        if (DUAL) st<AUXN>(rs, threadIdx.x * 16 + u * BLOCK * 16, r);
     }
 }
 
@@ -194,11 +194,11 @@ static void launch(K k, int grid, int block, const Args &a, hipStream_t s, hipEv
 
 static int grid_of(int64_t bytes, int64_t span) { return (int)((bytes + span - 1) / span); }
 
-template <int B, int U, bool D, int AP = NT, int AS = SC1>
+template <int B, int U, bool D, int AP = NT, int AS = SC1, int AN = AS>
 static Variant avg(const char *name)
 {
     return {name, D ? 4.0 : 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-                launch(k_avg<B, U, D, AP, AS>, grid_of(a.bytes, (int64_t)B * 16 * U), B, a, s, e0, e1);
+                launch(k_avg<B, U, D, AP, AS, AN>, grid_of(a.bytes, (int64_t)B * 16 * U), B, a, s, e0, e1);
             }};
 }
 
@@ -263,11 +263,22 @@ int main(int argc, char **argv)
              launch(k_oop<256, 1>, grid_of(a.bytes, 256 * 16), 256, a, s, e0, e1); }},
         {"oop  64x1 nt+sc1 store", 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
              launch(k_oop<64, 1, SC1 | NT>, grid_of(a.bytes, 64 * 16), 64, a, s, e0, e1); }},
+        // round 4: system-scope (sc0 sc1) stores, written through past the XCD L2, so the kernel's
+        // end-of-launch L2 write-back finds nothing dirty
+        {"oop  64x1 sc0+sc1 store", 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+             launch(k_oop<64, 1, SC1 | 1>, grid_of(a.bytes, 64 * 16), 64, a, s, e0, e1); }},
+        {"oop  64x1 nt+sc0+sc1 store", 3.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+             launch(k_oop<64, 1, SC1 | 1 | NT>, grid_of(a.bytes, 64 * 16), 64, a, s, e0, e1); }},
         avg<64, 1, true>("dual 64x1 (product WT, 2R2W)"),
         avg<64, 2, true>("dual 64x2"),
         avg<64, 4, true>("dual 64x4"),
         avg<256, 1, true>("dual 256x1"),
         avg<64, 1, true, NT, SC1 | NT>("dual 64x1 nt+sc1 stores"),
+        avg<64, 1, true, NT, SC1 | 1>("dual 64x1 sc0+sc1 stores"),
+        avg<64, 1, true, NT, SC1 | NT, SC1>("dual 64x1 param nt+sc1, snap sc1 (policy 8)"),
+        avg<64, 1, true, NT, SC1 | NT, SC1 | 1>("dual 64x1 param nt+sc1, snap sc0+sc1"),
+        avg<64, 1, true, NT, SC1 | 1, SC1>("dual 64x1 param sc0+sc1, snap sc1"),
+        avg<64, 1, false, NT, SC1 | 1>("avg  64x1 sc0+sc1 store (full)"),
         {"dual pipe 64, 16 WG/CU", 4.0, [cus](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
              launch(k_pipe<64, true>, std::min(grid_of(a.bytes, 64 * 16), cus * 16), 64, a, s, e0, e1); }},
         {"dual xcd-slab 64", 4.0, [](const Args &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
