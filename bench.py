@@ -648,6 +648,16 @@ def parity_key(trial):
     return "%s/%s%s" % (kind or "lockstep", pull, form)
 
 
+def write_through_key(world, chosen):
+    """The parity transport that vouches for the write-through learners a resident run times
+    beside its own (secondary_publish, reference_loop, overlap): the chosen trial's pull in the
+    write-through form ("local" at N=1)."""
+    if world == 1:
+        return "local"
+    mode = trial_mode(chosen)
+    return parity_key(("async/" + mode + "+wt") if chosen.startswith("async/") else mode)
+
+
 def trial_mode(key):
     """The pull mode of a trial key: "async/copy+wt" -> "copy", "relay-avg:32+res" -> "relay-avg:32"."""
     return key.split("/")[-1].replace("+wt", "").replace("+res", "")
@@ -1498,8 +1508,7 @@ def main(argv=None):
         # resident learners cannot leave their slots: the write-through form runs on a second set
         # of learners (same initial parameters, same transport; at N>1 every rank makes its own in
         # the same order, the binding is collective)
-        wt_key = ("local" if world == 1 else
-                  parity_key(("async/" + sel_mode + "+wt") if sel_async else sel_mode))
+        wt_key = write_through_key(world, pull)
         if parity is None or parity.get(wt_key, False):
             wd.enter("write-through learners", 300.0)
             grp2 = LocalGroup() if world == 1 else ("async" if sel_async else "lockstep")

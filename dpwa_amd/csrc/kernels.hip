@@ -246,8 +246,9 @@ template <int POLICY> struct LerpPolicy {
     static constexpr int base_store = kAuxStore | ((POLICY & 2) ? 1 : 0) | ((POLICY & 4) ? kAuxStream : 0);
     // bit 16: only the next snapshot is stored `nt` (a co-resident peer reads it two averages
     // later; this learner's parameters, re-read by its next average one average later, keep
-    // the Infinity Cache)
-    static constexpr int snap_store = base_store | ((POLICY & 16) ? kAuxStream : 0);
+    // the Infinity Cache); bit 32: only the next snapshot is stored `sc0 sc1` (system scope:
+    // written through the XCD L2, so the launch's end-of-kernel L2 write-back finds it clean)
+    static constexpr int snap_store = base_store | ((POLICY & 16) ? kAuxStream : 0) | ((POLICY & 32) ? 1 : 0);
     // bit 8: the parameters are stored `nt`, leaving the Infinity Cache to the snapshot a peer
     // reads next (the product policy)
     static constexpr int store = base_store | ((POLICY & 8) ? kAuxStream : 0);
@@ -522,6 +523,8 @@ static hipError_t launch_mode(void *param, const void *peer, int64_t n, const Le
             case 8: return launch_blocks<Ops, MODE, DUAL, 64, 8>(param, peer, n, args, s, timing);
             case 9: return launch_blocks<Ops, MODE, DUAL, 64, 9>(param, peer, n, args, s, timing);
             case 16: return launch_blocks<Ops, MODE, DUAL, 64, 16>(param, peer, n, args, s, timing);
+            case 10: return launch_blocks<Ops, MODE, DUAL, 64, 10>(param, peer, n, args, s, timing);
+            case 40: return launch_blocks<Ops, MODE, DUAL, 64, 40>(param, peer, n, args, s, timing);
             default: return launch_blocks<Ops, MODE, DUAL, 64>(param, peer, n, args, s, timing);
             }
         case 128: return launch_blocks<Ops, MODE, DUAL, 128>(param, peer, n, args, s, timing);
@@ -676,9 +679,12 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
     do {                                                                                                    \
         switch (lerp_policy()) {                                                                            \
         case 1: DPWA_BATCH_LAUNCH_P(OPS, DL, 1, false); break;                                              \
+        case 2: DPWA_BATCH_LAUNCH_P(OPS, DL, 2, false); break;                                              \
         case 8: DPWA_BATCH_LAUNCH_P(OPS, DL, 8, false); break;                                              \
         case 9: DPWA_BATCH_LAUNCH_P(OPS, DL, 9, false); break;                                              \
         case 16: DPWA_BATCH_LAUNCH_P(OPS, DL, 16, false); break;                                            \
+        case 10: DPWA_BATCH_LAUNCH_P(OPS, DL, 10, false); break;                                            \
+        case 40: DPWA_BATCH_LAUNCH_P(OPS, DL, 40, false); break;                                            \
         default: DPWA_BATCH_LAUNCH_P(OPS, DL, 0, false); break;                                             \
         }                                                                                                   \
     } while (0)

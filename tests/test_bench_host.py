@@ -46,6 +46,23 @@ def test_parity_transports_cover_every_trial_and_the_fd_shared_path():
     assert all(x.startswith("lockstep/") for x in bench.parity_transports(4, "lockstep"))
 
 
+def test_write_through_learners_are_vouched_for():
+    """A resident run times the reference loop's write-through form on a second set of learners
+    with the chosen pull: the parity transport checked for it exists for every possible choice."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    assert bench.write_through_key(1, "auto") == "local"
+    lockstep = ["copy", "kernel:256", "kernel:1024", "relay:32", "relay:128", "relay-avg:512"]
+    chosen = [m + "+res" for m in lockstep] + ["async/%s+res" % m for m in lockstep if not m.startswith("relay")]
+    t = set(bench.parity_transports(8))
+    for c in chosen:
+        k = bench.write_through_key(8, c)
+        assert k in t and "+res" not in k, (c, k)
+    assert bench.write_through_key(8, "async/kernel:1024+res") == "async/kernel:256+wt"
+    assert bench.write_through_key(8, "relay-avg:512+res") == "lockstep/relay-avg:32"
+
+
 def test_injection_hook_parsing(monkeypatch):
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
