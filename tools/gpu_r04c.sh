@@ -12,7 +12,7 @@ done
 timeout -k 10 300 tools/stream_tune 100000000 6 > gpurun_out/stream_tune_${TAG}_100m.log 2>&1 || exit 1
 grep -E "oop|dual|avg  64x1" gpurun_out/stream_tune_${TAG}_11m_2.log
 for pass in 1 2 3; do
-  for P in 8 2 40; do
+  for P in 8 2 40 0; do
     DPWA_LERP_POLICY=$P timeout -k 10 300 python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --compute-us 0 \
         > gpurun_out/ab_${TAG}_p${P}_$pass.json 2> gpurun_out/ab_${TAG}_p${P}_$pass.err || { tail gpurun_out/ab_${TAG}_p${P}_$pass.err; exit 1; }
     python3 -c "
