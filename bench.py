@@ -648,6 +648,26 @@ def parity_key(trial):
     return "%s/%s%s" % (kind or "lockstep", pull, form)
 
 
+TRAFFIC_ROUNDS = ("r04", "r03")     # profiles/traffic_<round>_<publish>[_x<learners>].json, newest first
+
+
+def pmc_traffic(path, publish, learners, numel, dtype, basis):
+    """(HBM bytes per launch, source) of a kernel from a committed PMC summary (tools/pmc_traffic.py
+    over rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/cold_sweep.py), if one matches this
+    workload; else (None, None)."""
+    name = "%s%s.json" % (publish, "_x%d" % learners if learners > 1 else "")
+    paths = [path] if path else [os.path.join(ROOT, "profiles", "traffic_%s_%s" % (r, name)) for r in TRAFFIC_ROUNDS]
+    for tpath in paths:
+        if not os.path.exists(tpath):
+            continue
+        with open(tpath) as f:
+            tr = json.load(f)
+        if (tr.get("numel") == numel and tr.get("dtype") == dtype and tr.get("publish", "full") == publish and
+                tr.get("learners_per_launch", 1) == learners and tr.get("basis", "in-loop") == basis):
+            return tr.get("hbm_bytes_per_launch"), os.path.relpath(tpath, ROOT)
+    return None, None
+
+
 def write_through_key(world, chosen):
     """The parity transport that vouches for the write-through learners a resident run times
     beside its own (secondary_publish, reference_loop, overlap): the chosen trial's pull in the
@@ -1612,6 +1632,9 @@ def main(argv=None):
             b = n_ * (4 if wt_ else 3) * args.numel * esize
             cold_ref[key] = {"avg_launch_us": round(c["avg_launch_us"], 2),
                              "frac": round(b / (c["avg_launch_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+            tb, _ = pmc_traffic(None, "write-through" if wt_ else "resident", n_, args.numel, args.dtype, "cold")
+            if tb:
+                cold_ref[key]["traffic_x"] = round(tb / b, 4)     # PMC HBM bytes / algorithmic bytes
     wd.enter("report", 120.0)
     out = None
     if rank == 0:
@@ -1624,17 +1647,8 @@ def main(argv=None):
         k_us = cold["avg_launch_us"] if cold else lerp_us
         achieved = kbytes / (k_us * 1e-6) / 1e9
         variant = form
-        traffic, traffic_src = None, None
-        tname = "traffic_r03_%s%s.json" % (variant, "_x%d" % per_launch if per_launch > 1 else "")
-        tpath = args.traffic or os.path.join(ROOT, "profiles", tname)
-        if os.path.exists(tpath):
-            with open(tpath) as f:
-                tr = json.load(f)
-            if (tr.get("numel") == args.numel and tr.get("dtype") == args.dtype and
-                    tr.get("publish", "full") == variant and tr.get("learners_per_launch", 1) == per_launch and
-                    tr.get("basis", "in-loop") == ("cold" if cold else "in-loop")):
-                traffic = tr.get("hbm_bytes_per_launch")
-                traffic_src = os.path.relpath(tpath, ROOT)
+        traffic, traffic_src = pmc_traffic(args.traffic, variant, per_launch, args.numel, args.dtype,
+                                           "cold" if cold else "in-loop")
         if resident_main:
             kname = ("dpwa::k_lerp_batch<Ops%s, true, 8, true> (%d resident learners' fused device factor + lerp "
                      "in one dispatch: each reads its published slot and writes the other)" % (args.dtype.upper(),

@@ -41,6 +41,30 @@ def test_self_launched_two_ranks_print_one_line():
     assert out["parity_of_timed_transport"]["ok"]
 
 
+def test_two_ranks_report_the_reference_loop_and_a_shared_device_xgmi_line():
+    """The driver's N>1 line with the write-through learner set on (secondary publish form and the
+    overlap leg, which run the reference's loop order beside the resident timed run): the line's
+    last key is `reference_loop` with a write-through value, the overlap names its publish form,
+    and with both ranks on one GPU the xGMI block says so and leaves `frac` null."""
+    args = [a for a in ARGS if a not in ("--no-secondary",)]
+    i = args.index("--compute-us")
+    args[i + 1] = "300"
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=280)
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert list(out)[-1] == "reference_loop"
+    ref = out["reference_loop"]
+    assert ref["publish"] == "write-through" and ref["value"] > 0 and "resident" in ref["headline"]
+    assert out["secondary_publish"]["publish"] == "write-through"
+    assert out["overlap"]["publish"] == "write-through" and out["overlap"]["ms_per_step"] > 0
+    x = out["xgmi"]
+    assert x["peak_gbs"] == 76.8 and x["ranks_share_device"] is True and x["frac"] is None
+
+
 def test_injected_transport_failure_is_isolated():
     # the timed rounds run resident learners (the default publish form): their transport fails
     rc, lines, err = _bench({"DPWA_BENCH_INJECT": "lockstep/kernel:256+res@1:end"})
