@@ -906,11 +906,12 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
             "rotating_buffer_sets": sets, "learners_per_launch": learners, "batch_bracket_us": float(batch_us)}
 
 
-def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None, publish="resident"):
+def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None, publish="resident", min_s=0.25):
     """Whole gossip rounds (two co-resident learners, `publish` form -- resident or write-through --,
     constant 0.5, fetch_probability 1, both averages in one dispatch) at every north_star size in
     its config's dtype: the averaged GB/s and rounds/s the north star asks for at 11M/100M/1B/7B
-    on one GPU."""
+    on one GPU.  Each size runs at least `steps` rounds and at least `min_s` seconds (sized from
+    one probe round), so the 11.17M row is a longer window than the driver's 20-step timed run."""
     from dpwa_amd import DpwaConnection
     from dpwa_amd.group import LocalGroup
     rows = [] if rows is None else rows
@@ -950,13 +951,17 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None, publ
         for _ in range(warmup):
             step()
         torch.cuda.synchronize()
+        t0 = time.perf_counter()       # one more round sizes the timed run: >= min_s, at least `steps`
+        step()
+        torch.cuda.synchronize()
+        n_steps = int(max(steps, min(20000, np.ceil(min_s / max(time.perf_counter() - t0, 1e-6)))))
         t0 = time.perf_counter()
-        averaged = sum(step() for _ in range(steps))
+        averaged = sum(step() for _ in range(n_steps))
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         rows.append({"numel": numel, "dtype": dt, "value": round(averaged * 3 * numel * esize / el / 1e9, 1),
-                     "ms_per_step": round(1e3 * el / steps, 4), "gossip_rounds_per_s": round(2 * steps / el, 1),
-                     "steps": steps, "batched": batch, "publish": publish})
+                     "ms_per_step": round(1e3 * el / n_steps, 4), "gossip_rounds_per_s": round(2 * n_steps / el, 1),
+                     "steps": n_steps, "seconds": round(el, 3), "batched": batch, "publish": publish})
         for c in conns:
             c.close()
         del flats, conns
