@@ -838,7 +838,8 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
     # > 1.2 GB of other traffic between two uses of a buffer; a set that large by itself is its
     # own rotation (7B bf16: 42 GB per learner, HBM holds the learners' slots too)
     sets = 1 if per_set >= 1.2e9 else max(2, int(np.ceil(1.2e9 / per_set)))
-    launches = max(2 * sets, min(launches, int(np.ceil(64 * 134e6 / (3 * learners * numel * esize)))))
+    # at least 4 timed launches (a 1B / 7B launch is 1-9 ms: one slow launch of two moved a mean by 50 %)
+    launches = max(2 * sets, 4, min(launches, int(np.ceil(64 * 134e6 / (3 * learners * numel * esize)))))
     hdr = _lib.SLOT_PAYLOAD_OFFSET // esize
     bufs = []       # per set: [(param, slot, snap)] * learners
     for _ in range(sets):
