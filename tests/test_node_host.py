@@ -1,0 +1,95 @@
+"""node.cpp's per-round logic on the CPU, under AddressSanitizer + UndefinedBehaviorSanitizer:
+DpwaConnection.update_send / update_wait (dpwa.py:104-156) and TxThread's fetch loop
+(conn.py:277-315) with the device path's timeout judging and rescue lanes, built with g++ over a
+host-only stand-in for the learner runtime (tests/native/fake_learner.cpp: a "pull" is a record
+whose stalling is scripted) and the real scheduler (sched.cpp).  tests/native/node_stress.cpp
+runs G lock-step learners whose first k pulls of a round stall (k drawn per learner and round,
+0-5) and prints what every node did; here each learner's rounds are replayed in the oracle policy
+(oracle/policy.py, pinned to the reference's TxThread by tests/golden/peer_select.json) with its
+first k requests scripted as timeouts: the node re-selects after every timeout -- the side pull,
+then rescue lanes, one after another while their pulls stall too -- exactly as TxThread keeps
+re-selecting, and with the side stream and all three lanes stalled (k >= 4) the next request times
+out for want of a free lane and the round ends without data.  Peers, attempts and
+flow-control scores must match round by round."""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from oracle.policy import OracleLearner
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"]
+LANES = 3
+
+
+@pytest.fixture(scope="module")
+def node_stress(tmp_path_factory):
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    exe = str(tmp_path_factory.mktemp("node") / "node_stress")
+    srcs = ["dpwa_amd/csrc/node.cpp", "dpwa_amd/csrc/sched.cpp", "tests/native/fake_learner.cpp",
+            "tests/native/node_stress.cpp"]
+    cmd = [gxx, "-std=c++17", "-O1", "-g", *SAN, "-I", os.path.join(ROOT, "include"),
+           *[os.path.join(ROOT, s) for s in srcs], "-o", exe, "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0 and ("asan" in r.stderr or "ubsan" in r.stderr):
+        pytest.skip("sanitizer runtime not installed: " + r.stderr[-200:])
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def _run(exe, G, rounds, seed, fp):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([exe, str(G), str(rounds), str(seed), repr(fp)], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "node stress ok" in r.stderr
+    return json.loads(r.stdout)
+
+
+@pytest.mark.parametrize("G,fp,seed", [(2, 1.0, 100), (4, 1.0, 200), (5, 0.7, 300), (8, 1.0, 400)])
+def test_node_fetch_loop_with_rescue_lanes_matches_oracle(node_stress, G, fp, seed):
+    rounds = 40
+    recs = _run(node_stress, G, rounds, seed, fp)
+    assert len(recs) == G * rounds
+    names = ["n%d" % g for g in range(G)]
+    L = [OracleLearner(names[g], [x for x in names if x != names[g]], fp, "constant", 0.5, 0.0, seed + g)
+         for g in range(G)]
+    by = {(x["round"], x["learner"]): x for x in recs}
+    seen = {"data after a stalled rescue pull": 0, "lanes exhausted": 0}
+    for r in range(rounds):
+        for g in range(G):
+            L[g].update_send(1.0)
+        for g in range(G):
+            rec = by[(r, g)]
+            stall = rec["stall"]
+            # the side pull and up to LANES rescue pulls stall; with all of them stalled the next
+            # request finds no free lane and times out too
+            timeouts = stall if stall <= LANES else LANES + 2
+            n_req = [0]
+
+            def request(peer, n_req=n_req, timeouts=timeouts):
+                n_req[0] += 1
+                return ("timeout", None, None) if n_req[0] <= timeouts else ("payload", {"clock": 1, "loss": 1.0}, b"x")
+
+            assert rec["fetching"] == int(L[g].fetching), (r, g)
+            if L[g].fetching:
+                _, payload, attempts = L[g].fetch(lambda p: "ok", request,
+                                                  max_attempts=LANES + 2 if stall > LANES else None)
+                others = [x for x in names if x != names[g]]
+                want_peer = others.index(attempts[-1]["peer"]) if payload is not None else -1
+                assert (rec["peer"], rec["attempts"]) == (want_peer, len(attempts)), (r, g, rec, attempts)
+                L[g].update_wait(1.0, {"clock": 1, "loss": 1.0}, payload is not None)
+                if payload is not None and stall >= 2:
+                    seen["data after a stalled rescue pull"] += 1
+                if stall > LANES:
+                    seen["lanes exhausted"] += 1
+                    assert rec["pulls"] == LANES + 1 and rec["peer"] == -1
+            else:
+                assert rec["peer"] == -1 and rec["attempts"] == 0
+            assert rec["scores"] == L[g].scores([x for x in names if x != names[g]]), (r, g, rec)
+    assert seen["data after a stalled rescue pull"] > 0 and seen["lanes exhausted"] > 0, seen
