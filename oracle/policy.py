@@ -90,8 +90,11 @@ class OracleLearner:
         return peer
 
     # -- conn.py:274-317 (one queue item) ----------------------------------------
-    def fetch(self, connect_fn, request_fn, max_attempts=None):
-        """Returns (state, payload, attempts); state/payload None when no data."""
+    def fetch(self, connect_fn, request_fn, max_attempts=None, stop=None):
+        """Returns (state, payload, attempts); state/payload None when no data.  stop (not the
+        reference's): called after each request's outcome is applied; True ends the loop there
+        without data -- this implementation's one divergence, a round whose every rescue lane is
+        stalled."""
         attempts = []
         while True:
             if max_attempts is not None and len(attempts) >= max_attempts:
@@ -110,6 +113,8 @@ class OracleLearner:
                 peer.connected = False
             else:  # unrecoverable request error: conn.py:311-313
                 del self.peers[peer.name]
+            if stop is not None and stop():
+                return None, None, attempts
 
     # -- dpwa.py:125-156 --------------------------------------------------------
     def update_wait(self, loss, peer_state, have_payload):

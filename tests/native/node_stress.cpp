@@ -51,6 +51,7 @@ int main(int argc, char **argv)
     const int rounds = argc > 2 ? atoi(argv[2]) : 40;
     const uint32_t seed0 = argc > 3 ? (uint32_t)atoi(argv[3]) : 100;
     const double fp = argc > 4 ? atof(argv[4]) : 1.0;
+    const int fault_pct = argc > 5 ? atoi(argv[5]) : 0;     // % of (round, learner, peer) with a fault
     g_rng = seed0 * 7919ULL + (uint64_t)G;
     if (G < 2 || G > 16 || rounds < 1) return 1;
     const dpwa_interp cfg{DPWA_INTERP_CONSTANT, 0, 0.5, 0.0};
@@ -71,10 +72,30 @@ int main(int argc, char **argv)
     bool first = true;
     for (int r = 0; r < rounds; ++r) {
         std::vector<int> stall(G), fetching(G);
+        std::vector<std::vector<int>> fault(G, std::vector<int>(G - 1, -1));
         for (int g = 0; g < G; ++g) {
             const uint64_t u = next_u64() % 100;
             stall[g] = u < 70 ? 0 : u < 80 ? 1 : u < 87 ? 2 : u < 92 ? 3 : u < 96 ? 4 : 5;
             CHECK(fake_stall(learners[g], stall[g]));
+            for (int k = 0; k < G - 1; ++k) {   // what a request to peer k meets this round
+                if ((int)(next_u64() % 100) < fault_pct) {
+                    const uint64_t v = next_u64() % 100;
+                    fault[g][k] = v < 15 ? DPWA_PEER_DOWN : v < 55 ? DPWA_PEER_SLOW : v < 98 ? DPWA_PEER_NO_STATE
+                                                                                      : DPWA_PEER_DEAD;
+                }
+            }
+            // at least one live peer answers normally (a round in which every live peer is slow or
+            // has no state spins for ever in the reference's TxThread, conn.py:286-313)
+            int live_ok = 0, first_live = -1;
+            for (int k = 0; k < G - 1; ++k) {
+                int sc = 0;
+                CHECK(dpwa_sched_score(scheds[g], k, &sc));
+                if (sc < 0) continue;
+                if (first_live < 0) first_live = k;
+                live_ok += fault[g][k] < 0;
+            }
+            if (!live_ok && first_live >= 0) fault[g][first_live] = -1;
+            for (int k = 0; k < G - 1; ++k) CHECK(dpwa_node_set_fault(nodes[g], k, fault[g][k]));
         }
         for (int g = 0; g < G; ++g)
             CHECK(dpwa_node_update_send(nodes[g], nullptr, 1.0, nullptr, 0, nullptr, &fetching[g]));
@@ -102,6 +123,8 @@ int main(int argc, char **argv)
                 EXPECT(sc == -1 || (sc >= 10 && sc <= 1000));
                 printf("%s%d", k ? ", " : "", sc);
             }
+            printf("], \"faults\": [");
+            for (int k = 0; k < G - 1; ++k) printf("%s%d", k ? ", " : "", fault[g][k]);
             printf("]}");
         }
         for (int g = 0; g < G; ++g) CHECK(fake_land_all(learners[g]));

@@ -42,54 +42,72 @@ def node_stress(tmp_path_factory):
     return exe
 
 
-def _run(exe, G, rounds, seed, fp):
+def _run(exe, G, rounds, seed, fp, fault_pct=0):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0", UBSAN_OPTIONS="print_stacktrace=1")
-    r = subprocess.run([exe, str(G), str(rounds), str(seed), repr(fp)], capture_output=True, text=True, timeout=300,
-                       env=env)
+    r = subprocess.run([exe, str(G), str(rounds), str(seed), repr(fp), str(fault_pct)], capture_output=True, text=True,
+                       timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert "node stress ok" in r.stderr
     return json.loads(r.stdout)
 
 
-@pytest.mark.parametrize("G,fp,seed", [(2, 1.0, 100), (4, 1.0, 200), (5, 0.7, 300), (8, 1.0, 400)])
-def test_node_fetch_loop_with_rescue_lanes_matches_oracle(node_stress, G, fp, seed):
+READY, NO_STATE, DOWN, SLOW, DEAD = 0, 1, 2, 3, 4     # DPWA_PEER_*; -1 = no fault
+
+
+@pytest.mark.parametrize("G,fp,seed,fault_pct", [(2, 1.0, 100, 0), (4, 1.0, 200, 0), (5, 0.7, 300, 0),
+                                                 (8, 1.0, 400, 0), (4, 1.0, 500, 12), (6, 0.8, 600, 8)])
+def test_node_fetch_loop_with_rescue_lanes_matches_oracle(node_stress, G, fp, seed, fault_pct):
+    """With fault_pct > 0 some requests also meet a faulted peer (refused or reset when down,
+    empty with no state, timed out when slow, removed when dead; conn.py:246-313), mixed with the
+    stalled pulls."""
     rounds = 40
-    recs = _run(node_stress, G, rounds, seed, fp)
+    recs = _run(node_stress, G, rounds, seed, fp, fault_pct)
     assert len(recs) == G * rounds
     names = ["n%d" % g for g in range(G)]
     L = [OracleLearner(names[g], [x for x in names if x != names[g]], fp, "constant", 0.5, 0.0, seed + g)
          for g in range(G)]
     by = {(x["round"], x["learner"]): x for x in recs}
-    seen = {"data after a stalled rescue pull": 0, "lanes exhausted": 0}
+    seen = {"data after a stalled rescue pull": 0, "lanes exhausted": 0, "faulted requests": 0}
     for r in range(rounds):
         for g in range(G):
             L[g].update_send(1.0)
         for g in range(G):
             rec = by[(r, g)]
+            others = [x for x in names if x != names[g]]
+            fault = dict(zip(others, rec["faults"]))
             stall = rec["stall"]
-            # the side pull and up to LANES rescue pulls stall; with all of them stalled the next
-            # request finds no free lane and times out too
-            timeouts = stall if stall <= LANES else LANES + 2
-            n_req = [0]
+            pulls = [0]      # requests to a ready peer (each is a pull; the first `stall` stall)
 
-            def request(peer, n_req=n_req, timeouts=timeouts):
-                n_req[0] += 1
-                return ("timeout", None, None) if n_req[0] <= timeouts else ("payload", {"clock": 1, "loss": 1.0}, b"x")
+            def connect(peer, fault=fault):
+                return {DOWN: "refused", DEAD: "error"}.get(fault[peer], "ok")
+
+            def request(peer, fault=fault, stall=stall, pulls=pulls):
+                f = fault[peer]
+                if f in (-1, READY):
+                    pulls[0] += 1
+                    # the side pull and up to LANES rescue pulls stall; with all of them stalled the
+                    # next pull finds no free lane and times out too
+                    if pulls[0] <= min(stall, LANES + 1) or (stall > LANES and pulls[0] == LANES + 2):
+                        return "timeout", None, None
+                    return "payload", {"clock": 1, "loss": 1.0}, b"x"
+                seen["faulted requests"] += 1
+                return {NO_STATE: ("empty", None, None), SLOW: ("timeout", None, None)}.get(f, ("error", None, None))
 
             assert rec["fetching"] == int(L[g].fetching), (r, g)
             if L[g].fetching:
-                _, payload, attempts = L[g].fetch(lambda p: "ok", request,
-                                                  max_attempts=LANES + 2 if stall > LANES else None)
-                others = [x for x in names if x != names[g]]
+                _, payload, attempts = L[g].fetch(connect, request, max_attempts=100_000,   # node.cpp's bound
+                                                  stop=lambda pulls=pulls: pulls[0] >= LANES + 2)
                 want_peer = others.index(attempts[-1]["peer"]) if payload is not None else -1
                 assert (rec["peer"], rec["attempts"]) == (want_peer, len(attempts)), (r, g, rec, attempts)
                 L[g].update_wait(1.0, {"clock": 1, "loss": 1.0}, payload is not None)
-                if payload is not None and stall >= 2:
+                if payload is not None and pulls[0] >= 3:
                     seen["data after a stalled rescue pull"] += 1
-                if stall > LANES:
+                if pulls[0] >= LANES + 2:
                     seen["lanes exhausted"] += 1
                     assert rec["pulls"] == LANES + 1 and rec["peer"] == -1
             else:
                 assert rec["peer"] == -1 and rec["attempts"] == 0
-            assert rec["scores"] == L[g].scores([x for x in names if x != names[g]]), (r, g, rec)
+            want_scores = [-1 if x is None else x for x in L[g].scores(others)]
+            assert rec["scores"] == want_scores, (r, g, rec)
     assert seen["data after a stalled rescue pull"] > 0 and seen["lanes exhausted"] > 0, seen
+    assert (seen["faulted requests"] > 0) == (fault_pct > 0), seen
