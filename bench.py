@@ -818,7 +818,7 @@ def _async_verdict(t, names, world, rank, check, err, ctl):
 
 
 # ---------------------------------------------------------------- kernel measurements
-def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners=1, resident=False):
+def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners=1, resident=False, pair=False):
     """The product averaging kernel alone over rotating buffers (> 1.2 GB of other traffic
     between two uses of a buffer, so nothing is served from the 256 MiB Infinity Cache).  With
     learners == 1 it is dpwa_average (k_lerp<Ops, COEF_FUSED, write_through>: fp64 device
@@ -829,12 +829,15 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
     gaps of a back-to-back batch are not counted.  Also returns the rate of one event pair
     around the whole batch (which does include the gaps).  `resident`: the resident form
     (dpwa_average_many_resident): the parameters are read from one snapshot payload and the result
-    stored into another, nothing written back in place (3*N*s)."""
+    stored into another, nothing written back in place (3*N*s).  `pair` (resident, 2 learners): the
+    two learners average with each other, as the N=1 loop's do -- entry 0 reads A's slot and B's,
+    entry 1 B's and A's -- so the dispatch is a mutual pair (k_lerp_batch's XCD pairing: 4*N*s)."""
     from dpwa_amd import _lib
     esize = 4 if dtype == torch.float32 else 2
     write_through = write_through or resident
+    pair = pair and resident and learners == 2
     nbuf = 3 if write_through else 2
-    per_set = learners * nbuf * numel * esize
+    per_set = (4 if pair else learners * nbuf) * numel * esize
     # > 1.2 GB of other traffic between two uses of a buffer; a set that large by itself is its
     # own rotation (7B bf16: 42 GB per learner, HBM holds the learners' slots too)
     sets = 1 if per_set >= 1.2e9 else max(2, int(np.ceil(1.2e9 / per_set)))
@@ -844,7 +847,13 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
     bufs = []       # per set: [(param, slot, snap)] * learners
     for _ in range(sets):
         entries = []
-        for _ in range(learners):
+        if pair:    # two published slots, each the parameters of one learner and the peer of the other
+            slots = [torch.zeros(hdr + numel, device=device, dtype=dtype) for _ in range(2)]
+            for sl in slots:
+                sl[hdr:].normal_()
+            nxt = [torch.empty(hdr + numel, device=device, dtype=dtype)[hdr:] for _ in range(2)]
+            entries = [(slots[0][hdr:], slots[1], nxt[0]), (slots[1][hdr:], slots[0], nxt[1])]
+        for _ in range(0 if pair else learners):
             param = torch.empty(numel, device=device, dtype=dtype).normal_()
             # a snapshot slot as the learner lays it out: header (zeros) and pad, then the payload
             slot = torch.zeros(hdr + numel, device=device, dtype=dtype)
@@ -904,7 +913,8 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
     torch.cuda.empty_cache()
     return {"avg_launch_us": float(us.mean()), "median_launch_us": float(np.median(us)),
             "min_launch_us": float(us.min()), "max_launch_us": float(us.max()), "launches": launches,
-            "rotating_buffer_sets": sets, "learners_per_launch": learners, "batch_bracket_us": float(batch_us)}
+            "rotating_buffer_sets": sets, "learners_per_launch": learners, "batch_bracket_us": float(batch_us),
+            "mutual_pair": pair}
 
 
 def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None, publish="resident", min_s=0.25):
@@ -1079,12 +1089,13 @@ def size_sweep(device, rows=None):
             forms += [("write-through", 2), ("resident", 2)]
         for form, learners in forms:
             wt = form == "write-through"
+            pair = form == "resident" and learners == 2      # the N=1 loop's mutual pair (4*N*s)
             c = cold_kernel(numel, torch.float32 if dt == "f32" else torch.bfloat16, device, wt, learners=learners,
-                            resident=form == "resident")
-            nbytes = learners * (4 if wt else 3) * numel * esize
+                            resident=form == "resident", pair=pair)
+            nbytes = 4 * numel * esize if pair else learners * (4 if wt else 3) * numel * esize
             gbs = nbytes / (c["avg_launch_us"] * 1e-6) / 1e9
             rows.append({"numel": numel, "dtype": dt, "publish": form,
-                         "learners_per_launch": learners,
+                         "learners_per_launch": learners, "mutual_pair": pair,
                          "bytes_per_launch": nbytes, "avg_launch_us": round(c["avg_launch_us"], 2),
                          "median_launch_us": round(c["median_launch_us"], 2), "achieved": round(gbs, 1),
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "launches": c["launches"],
@@ -1619,21 +1630,26 @@ def main(argv=None):
     unit_bytes = 3 * args.numel * esize
     per_launch = len(learners) if batched else 1
     wt_kernel = wt_main and not resident_main      # resident: the kernel moves the averaging's 3*N*s only
-    kbytes = (4 if wt_kernel else 3) * args.numel * esize * per_launch   # the timed loop's averaging dispatch
+    # the N=1 resident loop's two learners average with each other: one mutual pair per dispatch,
+    # whose two averages read the same two snapshots (k_lerp_batch's XCD pairing): 4*N*s per launch
+    pair_kernel = resident_main and per_launch == 2
+    kbytes = (4 * args.numel * esize if pair_kernel else
+              (4 if wt_kernel else 3) * args.numel * esize * per_launch)   # the timed loop's averaging dispatch
     # the same kernel alone, cold (rotating buffers, per-launch dispatch events): the roofline's basis
     cold = None
     cold_plain = None
     cold_ref = {}           # the reference loop's (write-through) kernels and the single resident one, cold
     if not args.no_cold:
         wd.enter("cold kernel", 300.0)
-        cold = cold_kernel(args.numel, dtype, device, wt_kernel, learners=per_launch, resident=resident_main)
+        cold = cold_kernel(args.numel, dtype, device, wt_kernel, learners=per_launch, resident=resident_main,
+                           pair=pair_kernel)
         if wt_kernel:   # BASELINE's target kernel: the same dispatch without the snapshot write
             cold_plain = cold_kernel(args.numel, dtype, device, False, learners=per_launch)
         for key, wt_, n_, res_ in (("write_through_x%d" % per_launch, True, per_launch, False),
                                    ("write_through_single", True, 1, False), ("resident_single", False, 1, True)):
             if key == "write_through_single" and per_launch == 1:
                 continue
-            same = (n_ == per_launch and res_ == resident_main and wt_ == wt_kernel)
+            same = (n_ == per_launch and res_ == resident_main and wt_ == wt_kernel and not pair_kernel)
             c = cold if same else cold_kernel(args.numel, dtype, device, wt_, learners=n_, resident=res_)
             b = n_ * (4 if wt_ else 3) * args.numel * esize
             cold_ref[key] = {"avg_launch_us": round(c["avg_launch_us"], 2),
@@ -1653,12 +1669,13 @@ def main(argv=None):
         k_us = cold["avg_launch_us"] if cold else lerp_us
         achieved = kbytes / (k_us * 1e-6) / 1e9
         variant = form
-        traffic, traffic_src = pmc_traffic(args.traffic, variant, per_launch, args.numel, args.dtype,
-                                           "cold" if cold else "in-loop")
+        traffic, traffic_src = pmc_traffic(args.traffic, "resident-pair" if pair_kernel else variant, per_launch,
+                                           args.numel, args.dtype, "cold" if cold else "in-loop")
         if resident_main:
             kname = ("dpwa::k_lerp_batch<Ops%s, true, 8, true> (%d resident learners' fused device factor + lerp "
-                     "in one dispatch: each reads its published slot and writes the other)" % (args.dtype.upper(),
-                                                                                               per_launch)
+                     "in one dispatch: each reads its published slot and writes the other; the two average with each "
+                     "other, a mutual pair whose two averages of a span run on one XCD)" % (args.dtype.upper(),
+                                                                                             per_launch)
                      if per_launch > 1 else
                      "dpwa::k_lerp<Ops%s, COEF_FUSED, true, 64, 8, true> (resident: fused device factor + lerp "
                      "from the published slot into the other)" % args.dtype.upper())
@@ -1705,7 +1722,11 @@ def main(argv=None):
                 "parallelism": "gossip x%d" % int(rounds / args.steps),
                 "streams": args.streams,
             },
-            "value_basis": "the timed pass carries no instrumentation (no kernel timing, no events)",
+            "value_basis": "the timed pass carries no instrumentation (no kernel timing, no events); value = 3*N*s "
+                           "per completed averaging (SURVEY 8d's unit) over the wall time" +
+                           ("; the two learners average with each other and share their two snapshot reads "
+                            "(roofline.bytes_per_launch = 4*N*s for both averagings), so value is not an HBM rate and "
+                            "can exceed the HBM peak" if pair_kernel else ""),
             "gossip_rounds_per_s": round(rounds / elapsed, 1),
             "gossip_rounds_per_s_per_learner": round(rounds / elapsed / (rounds / args.steps), 1),
             "averagings": int(averaged),
@@ -1719,7 +1740,13 @@ def main(argv=None):
                 "kernel": kname,
                 "learners_per_launch": per_launch,
                 "bytes_per_launch": kbytes,
-                "bytes_note": (("%d x " % per_launch if per_launch > 1 else "") +
+                "bytes_note": ("4*N*s: the two resident learners average with each other, so the dispatch's two "
+                               "averages read the same two published slots: each is read from HBM once (each span's "
+                               "two averages run in workgroups b and b+8, one XCD, and the second read hits its L2) "
+                               "and the two next slots are written. The metric's unit counts 3*N*s per averaging "
+                               "(SURVEY 8d), 6*N*s for the two, so `value` can exceed the HBM peak"
+                               if pair_kernel else
+                               ("%d x " % per_launch if per_launch > 1 else "") +
                                ("3*N*s: read the parameters (the published slot they are in), read the peer "
                                 "snapshot, write the parameters into the learner's other slot (the next publish "
                                 "then moves nothing)" if resident_main else

@@ -1,0 +1,159 @@
+"""Mutual pairs in the resident batched dispatch (k_lerp_batch, kernels.hip launch_average_batch):
+two co-resident resident learners that average with each other in a round read the same two
+snapshots -- A reads its published slot and B's, B its own and A's -- so the launcher puts each
+pair's two averages of a span in workgroups b and b + 8 (one XCD under round-robin dispatch) and
+the second read of every span hits that XCD's L2.  Only the placement changes: every entry must
+still be exactly the single-learner fused average (factor, clock, lerp into the next slot, ragged
+tail, ZeroDivision no-op) against the CPU oracle, whatever the mix of pairs and single entries
+in the dispatch, and the published slots must stay untouched."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from dpwa_amd import DpwaConnection, _lib
+from dpwa_amd.group import LocalGroup
+from oracle import gossip as ogossip
+from oracle import lerp as olerp
+from oracle import policy as opolicy
+from tests.test_gpu_kernels import average_slot, from_u16, stream, to_u16
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+OFF = _lib.SLOT_PAYLOAD_OFFSET
+
+
+class Learner:
+    """A resident learner as the batch sees it: its published slot (header + parameters), its next
+    slot, its clock pair and coefficient block."""
+
+    def __init__(self, n, dtype, rng, clock, loss):
+        self.n, self.dtype = n, dtype
+        p32 = rng.standard_normal(n).astype(np.float32)
+        self.host = p32 if dtype == "f32" else olerp.f32_to_bf16(p32)
+        t = torch.from_numpy(p32).to(DEV) if dtype == "f32" else from_u16(self.host)
+        self.clock_val, self.loss = clock, loss
+        self.slot = average_slot(t, clock, loss)           # the published snapshot = the parameters
+        self.esize = 4 if dtype == "f32" else 2
+        self.next = torch.full((OFF + n * self.esize,), 0x7f, dtype=torch.uint8, device=DEV)
+        self.clock = torch.tensor([clock, -1.0], dtype=torch.float64, device=DEV)
+        self.coef = torch.zeros(32, dtype=torch.uint8, device=DEV)
+
+    def payload(self, slot):
+        raw = slot[OFF:].cpu().numpy()
+        return raw.view(np.float32) if self.dtype == "f32" else raw.view(np.uint16)
+
+
+def _desc(me, peer, loss):
+    return _lib.AverageDesc(me.slot.data_ptr() + OFF, peer.slot.data_ptr(), me.n, me.clock.data_ptr(), loss,
+                            me.coef.data_ptr(), me.next.data_ptr() + OFF)
+
+
+def _expect(me, peer, method, loss):
+    res = opolicy.factor_and_clock(method, None, 0.0, me.clock_val, peer.clock_val, loss, peer.loss) \
+        if not (method == "loss" and loss + peer.loss == 0.0) else None
+    exp = me.host.copy()
+    if res is not None:
+        (olerp.c_lerp_f32_ if me.dtype == "f32" else olerp.c_lerp_bf16_)(exp, peer.host, res[0])
+    return exp, res
+
+
+def _run(learners, picks, dtype, method="clock", losses=None, env_off=False):
+    """picks: [(me, peer)] in descriptor order; returns per entry (got, expected, res)."""
+    losses = losses or [0.5 + 0.1 * i for i in range(len(picks))]
+    d = (_lib.AverageDesc * len(picks))()
+    for j, ((a, b), loss) in enumerate(zip(picks, losses)):
+        d[j] = _desc(learners[a], learners[b], loss)
+    before = [lr.slot.clone() for lr in learners]
+    cfg = _lib.Interp(opolicy.METHODS[method], 0, 0.0, 0.0)
+    _lib.call("dpwa_average_many_resident", _lib.F32 if dtype == "f32" else _lib.BF16, d, len(picks),
+              ctypes.byref(cfg), stream(), None, None)
+    torch.cuda.synchronize()
+    for lr, b in zip(learners, before):
+        assert torch.equal(lr.slot, b)                   # the published snapshots are only read
+    out = []
+    for (a, b), loss in zip(picks, losses):
+        me = learners[a]
+        exp, res = _expect(me, learners[b], method, loss)
+        out.append((me.payload(me.next), exp, res, me))
+    return out
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("n", [1, 7, 64 * 4, 8 * 64 * 4 - 1, 8 * 64 * 4, 8 * 64 * 4 + 1, 4099, 65536 + 13,
+                               (1 << 20) + 5])
+def test_mutual_pair_vs_oracle(dtype, n):
+    """One mutual pair at sizes around the 8-span group of the XCD pairing (a partial last group,
+    an exact multiple, one element over) and ragged tails: both averages bit-exact with the C
+    oracle, both clocks and coefficient blocks written."""
+    rng = np.random.default_rng(n)
+    ls = [Learner(n, dtype, rng, 1.0, 0.5), Learner(n, dtype, rng, 4.0, 0.75)]
+    for got, exp, res, me in _run(ls, [(0, 1), (1, 0)], dtype):
+        assert olerp.bits_equal(got, exp), n
+        c = _lib.Coef.from_buffer_copy(me.coef.cpu().numpy().tobytes())
+        assert c.status == 0 and c.factor == res[0]
+        assert me.clock[1].item() == res[1]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_pairs_and_single_entries_in_one_dispatch(dtype):
+    """Eight learners, descriptors in a scrambled order: two mutual pairs (found wherever they
+    are in the list), entries that read a peer without being read back, and one whose peer
+    averages with a third learner; equal and unequal sizes mixed (unequal never pair)."""
+    rng = np.random.default_rng(3)
+    sizes = [40_009, 40_009, 40_009, 40_009, 40_009, 123, 40_009, 40_009]
+    ls = [Learner(n, dtype, rng, 1.0 + i, 0.25 + 0.1 * i) for i, n in enumerate(sizes)]
+    picks = [(2, 6), (0, 3), (6, 2), (4, 0), (3, 0), (7, 2), (1, 4)]
+    for got, exp, _, me in _run(ls, picks, dtype):
+        assert olerp.bits_equal(got, exp)
+
+
+def test_pair_with_a_zero_division_entry():
+    """Loss interpolation with loss + peer loss == 0 for one side of a pair (the reference's
+    ZeroDivisionError, interpolation.py:31-33): that entry copies its parameters into its next
+    slot unchanged and keeps its clock; its partner averages normally."""
+    rng = np.random.default_rng(9)
+    ls = [Learner(70_001, "f32", rng, 2.0, 0.0), Learner(70_001, "f32", rng, 3.0, 0.0)]
+    out = _run(ls, [(0, 1), (1, 0)], "f32", method="loss", losses=[0.0, 0.4])
+    (got0, exp0, res0, me0), (got1, exp1, res1, _) = out
+    assert res0 is None and olerp.bits_equal(got0, me0.host)
+    c0 = _lib.Coef.from_buffer_copy(me0.coef.cpu().numpy().tobytes())
+    assert c0.status == _lib.STATUS_ZERO_DIVISION and me0.clock[1].item() == 2.0     # the clock unchanged
+    assert res1 is not None and olerp.bits_equal(got1, exp1)
+
+
+def test_resident_gossip_of_two_learners_matches_oracle(tmp_path):
+    """The N=1 bench's round: two resident learners, each the other's only peer, batched -- every
+    round a mutual pair -- 20 rounds with a step after each update_wait, against
+    oracle/gossip.py (train_after_wait) bit for bit."""
+    names = ["p0", "p1"]
+    cfg = tmp_path / "pair.yaml"
+    lines = ["- nodes:"] + ["  - {name: %s, host: localhost, port: %d}" % (nm, 47100 + i) for i, nm in enumerate(names)]
+    lines += ["- fetch_probability: 1", "- timeout_ms: 2500", "- interpolation: clock", "- divergence_threshold: 0",
+              "- constant: { value: 0.5 }", "- clock: 0", "- loss: 0"]
+    cfg.write_text("\n".join(lines) + "\n")
+    rng = np.random.default_rng(21)
+    n, T = 3 * 8 * 64 * 4 + 77, 20
+    init = rng.standard_normal((2, n)).astype(np.float32)
+    deltas = (0.01 * rng.standard_normal((T, 2, n))).astype(np.float32)
+    send = [[1.0 + g + r for g in range(2)] for r in range(T)]
+    wait = [[0.5 + g + r for g in range(2)] for r in range(T)]
+    exp = ogossip.simulate(names, init, deltas, send, wait, "clock", None, 0.0, 1.0, [5, 6], train_after_wait=True)
+    group = LocalGroup()
+    conns = [DpwaConnection(names[g], str(cfg), seed=5 + g, group=group) for g in range(2)]
+    for g in range(2):
+        conns[g].make_resident(torch.from_numpy(init[g]).to(DEV))
+    for r in range(T):
+        for g in range(2):
+            conns[g].update_send(conns[g].parameters, send[r][g])
+        res = DpwaConnection.update_wait_average_many(conns, [c.parameters for c in conns], wait[r])
+        for g in range(2):
+            assert res[g][0] is not None and res[g][0].peer == names[1 - g]
+            assert olerp.bits_equal(conns[g].parameters.cpu().numpy(), exp["params"][r, g]), (r, g)
+            assert conns[g].clock == exp["clocks"][r, g]
+        for g in range(2):
+            conns[g].parameters.add_(torch.from_numpy(deltas[r, g]).to(DEV))
+    for c in conns:
+        c.close()

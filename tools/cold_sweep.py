@@ -27,7 +27,8 @@ def main():
     ap.add_argument("--sizes", default="%d:f32" % bench.RESNET18_NUMEL,
                     help="comma-separated numel:dtype list (dtype f32 or bf16)")
     ap.add_argument("--all", action="store_true", help="every north_star size (bench.SWEEP)")
-    ap.add_argument("--publish", choices=["full", "write-through", "resident", "both", "all"], default="both")
+    ap.add_argument("--publish", choices=["full", "write-through", "resident", "resident-pair", "both", "all"],
+                    default="both", help="resident-pair (with --learners 2): the N=1 loop's mutual pair, 4*N*s")
     ap.add_argument("--launches", type=int, default=64)
     ap.add_argument("--learners", type=int, default=1,
                     help="averages per dispatch: 1 = dpwa_average (k_lerp), > 1 = dpwa_average_many (k_lerp_batch, "
@@ -36,6 +37,7 @@ def main():
     sizes = [(n, d) for n, d in bench.SWEEP] if args.all else \
         [(int(x.split(":")[0]), x.split(":")[1]) for x in args.sizes.split(",")]
     forms = {"full": ["full"], "write-through": ["write-through"], "resident": ["resident"],
+             "resident-pair": ["resident-pair"],
              "both": ["full", "write-through"], "all": ["full", "write-through", "resident"]}[args.publish]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -44,9 +46,10 @@ def main():
         esize = 4 if dt == "f32" else 2
         for form in forms:
             wt = form == "write-through"
+            pair = form == "resident-pair"
             c = bench.cold_kernel(numel, dtype, dev, wt, args.launches, learners=args.learners,
-                                  resident=form == "resident")
-            nbytes = args.learners * (4 if wt else 3) * numel * esize
+                                  resident=form.startswith("resident"), pair=pair)
+            nbytes = 4 * numel * esize if pair else args.learners * (4 if wt else 3) * numel * esize
             gbs = nbytes / (c["avg_launch_us"] * 1e-6) / 1e9
             print(json.dumps(dict(numel=numel, dtype=dt, publish=form,
                                   bytes_per_launch=nbytes, achieved=round(gbs, 1),

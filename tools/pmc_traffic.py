@@ -47,8 +47,9 @@ def main():
     ap.add_argument("--numel", type=int, default=11_173_962)
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--publish", choices=["full", "write-through", "resident"], default="full",
-                    help="write-through: the kernel also writes the next snapshot (4*N*s algorithmic bytes)")
+    ap.add_argument("--publish", choices=["full", "write-through", "resident", "resident-pair"], default="full",
+                    help="write-through: the kernel also writes the next snapshot (4*N*s algorithmic bytes); "
+                         "resident-pair: two resident learners averaging with each other (4*N*s for both)")
     ap.add_argument("--learners", type=int, default=1, help="averages per dispatch (k_lerp_batch)")
     ap.add_argument("--basis", choices=["cold", "in-loop"], default="cold",
                     help="what the profiled command ran: tools/cold_sweep.py (cold) or bench.py's loop")
@@ -63,7 +64,8 @@ def main():
     read_bytes = 2 * f_kib * 1024      # gfx950 FETCH_SIZE = 1/2 of 16-B/lane streaming reads
     write_bytes = w_kib * 1024
     esize = 4 if args.dtype == "f32" else 2
-    algo = args.learners * (4 if args.publish == "write-through" else 3) * args.numel * esize
+    algo = (4 * args.numel * esize if args.publish == "resident-pair" else
+            args.learners * (4 if args.publish == "write-through" else 3) * args.numel * esize)
     out = {
         "kernel": sorted(set(names.values()))[0],
         "numel": args.numel,
