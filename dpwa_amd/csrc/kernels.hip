@@ -402,21 +402,18 @@ __global__ __launch_bounds__(kStreamBlock) void k_lerp_batch(AvgBatch batch)
 {
     int i = 0;
     uint32_t blk;
-    if (blockIdx.x < batch.pair_end) {
-        // a mutual pair (entries 2k, 2k+1 average with each other: each reads the other's
-        // parameters): the two averages of span s run in workgroups b and b + 8, which round-robin
-        // dispatch puts on the same XCD at about the same time, so each snapshot span is fetched
-        // from HBM once and the second read hits that XCD's L2 (2 reads + 2 writes of N*s for the
-        // two averages instead of 4 + 2)
-        int k = 0;
-#pragma unroll
-        for (int q = 1; q < kMaxAvgBatch / 2; ++q)
-            if (q < batch.pairs && blockIdx.x >= batch.pair_begin[q]) k = q;
-        const uint32_t b = blockIdx.x - batch.pair_begin[k];
-        i = 2 * k + (int)((b >> 3) & 1u);
-        blk = (b >> 4) * 8u + (b & 7u);
-        if (blk >= batch.spans[i]) return;
-    } else if (batch.interleave) {
+    if (batch.interleave == 2) {
+        // XCD-grouped: workgroup b = (s / 8) * 8E + e * 8 + s % 8 takes span s of entry e, so every
+        // entry's span s runs on XCD s % 8 (round-robin dispatch) within a few dispatch slots of the
+        // others': entries that read the same buffer -- two resident learners that average with each
+        // other both read both published slots -- fetch each span from HBM once, the later reads hit
+        // that XCD's L2
+        const uint32_t w = 8u * (uint32_t)batch.count;
+        const uint32_t r = blockIdx.x % w;
+        i = (int)(r >> 3);
+        blk = (blockIdx.x / w) * 8u + (r & 7u);
+        if (blk >= batch.spans) return;
+    } else if (batch.interleave == 1) {
         // entries of equal size, their spans dealt round-robin: a span is read one round after
         // the span at the same position was written by the previous round's dispatch, whichever
         // entry wrote it, so every re-read is equally recent (Infinity Cache residency)
@@ -652,17 +649,27 @@ static int batch_order()
     return forced;
 }
 
-// Mutual pairs of a resident batch on one XCD (k_lerp_batch); DPWA_BATCH_PAIRS=0 turns it off
-// (A/B runs).  tools/pair_tune.hip: two 11.17M fp32 resident learners averaging with each other,
-// 36.8 -> 25-27 us per dispatch in the gossip loop, 41.3 -> 28.5 us cold (the fused one-workgroup
-// form of both averages: 25.6 / 28.5).
-static bool batch_pairs()
+// XCD-grouped span order for resident batches whose entries share a read (k_lerp_batch);
+// DPWA_BATCH_SHARE=0 turns it off (A/B runs).  tools/pair_tune.hip: two 11.17M fp32 resident
+// learners averaging with each other, 36.8 -> 25-27 us per dispatch in the gossip loop, 41.3 ->
+// 28.5 us cold (a fused one-workgroup form of both averages: 25.6 / 28.5).
+static bool batch_share()
 {
     static const bool on = [] {
-        const char *e = getenv("DPWA_BATCH_PAIRS");
+        const char *e = getenv("DPWA_BATCH_SHARE");
         return !(e && strcmp(e, "0") == 0);
     }();
     return on;
+}
+
+// Some buffer is read by two entries (as parameters or as the peer snapshot).
+static bool shares_a_read(const AvgBatch &x)
+{
+    for (int i = 0; i < x.count; ++i)
+        for (int j = 0; j < x.count; ++j)
+            if (i != j && (x.e[i].peer == x.e[j].param || (j > i && x.e[i].peer == x.e[j].peer)))
+                return true;
+    return false;
 }
 
 hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hipStream_t s,
@@ -681,41 +688,11 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
         const int64_t gi = (e.n / per) / kStreamBlock + 1;   // as launch_blocks: last span may be empty
         if (gi > 0x7fffffffLL) return hipErrorInvalidValue;
     }
-    // mutual pairs first (resident entries only: nothing writes what they read), then the rest;
-    // the entries are independent, so their order in the dispatch is free
-    x.pairs = 0;
-    if (oop && batch_pairs()) {
-        int order[kMaxAvgBatch], m = 0;
-        bool used[kMaxAvgBatch] = {};
-        for (int i = 0; i < x.count; ++i) {
-            if (used[i] || b.e[i].n == 0) continue;
-            for (int j = i + 1; j < x.count; ++j)
-                if (!used[j] && b.e[j].n == b.e[i].n && b.e[i].peer == b.e[j].param && b.e[j].peer == b.e[i].param) {
-                    order[m++] = i;
-                    order[m++] = j;
-                    used[i] = used[j] = true;
-                    x.pairs++;
-                    break;
-                }
-        }
-        for (int i = 0; i < x.count; ++i)
-            if (!used[i]) order[m++] = i;
-        for (int i = 0; i < x.count; ++i) x.e[i] = b.e[order[i]];
-    }
-    for (int i = 0; i < x.count; ++i) x.spans[i] = (uint32_t)((x.e[i].n / per) / kStreamBlock + 1);
-    for (int k = 0; k < x.pairs; ++k) {   // 16 workgroups per 8 spans of the pair
-        x.pair_begin[k] = g;
-        x.begin[2 * k] = x.begin[2 * k + 1] = 0;
-        const int64_t gp = (int64_t)(x.spans[2 * k] + 7) / 8 * 16;
-        if ((int64_t)g + gp > 0x7fffffffLL) return hipErrorInvalidValue;
-        g += (uint32_t)gp;
-    }
-    x.pair_end = g;
-    for (int i = 2 * x.pairs; i < x.count; ++i) {
+    for (int i = 0; i < x.count; ++i) {
         x.begin[i] = g;
-        if ((int64_t)g + x.spans[i] > 0x7fffffffLL) return hipErrorInvalidValue;
-        g += x.spans[i];
+        g += (uint32_t)((x.e[i].n / per) / kStreamBlock + 1);
     }
+    if (g > 0x7fffffffu) return hipErrorInvalidValue;
     for (int i = x.count; i < kMaxAvgBatch; ++i) x.begin[i] = 0xffffffffu;
     // span order: see batch_order()
     bool same = true;
@@ -725,8 +702,17 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
         written += (size_t)x.e[i].n * (size_t)(per == OpsF32::PER ? 4 : 2) * (dual && !oop ? 2 : 1);
     }
     const int order = batch_order();
-    x.interleave = x.pairs == 0 && same && x.count > 1 && (order == 1 || (order < 0 && written <= kInfinityCacheBytes))
-                       ? 1 : 0;
+    x.interleave = same && x.count > 1 && (order == 1 || (order < 0 && written <= kInfinityCacheBytes)) ? 1 : 0;
+    // resident entries of equal size that read a common buffer (a learner's published slot is its
+    // own parameters and another's peer): XCD-grouped, whatever the size (nothing writes what they
+    // read, so any order is safe)
+    x.spans = (uint32_t)((x.e[0].n / per) / kStreamBlock + 1);
+    if (oop && same && x.count > 1 && order < 0 && batch_share() && shares_a_read(x)) {
+        const uint64_t gg = (uint64_t)(x.spans + 7) / 8 * 8 * (uint64_t)x.count;
+        if (gg > 0x7fffffffu) return hipErrorInvalidValue;
+        x.interleave = 2;
+        g = (uint32_t)gg;
+    }
 #define DPWA_BATCH_LAUNCH_P(OPS, DL, P, OOP)                                                                \
     do {                                                                                                    \
         if (timing)                                                                                         \

@@ -66,13 +66,11 @@ struct AvgEntry {
 };
 struct AvgBatch {
     int32_t count;
-    int32_t interleave;             // spans dealt round-robin over equal-size entries (launcher)
-    // mutual pairs (launcher, resident entries only): entries 2k and 2k+1 read each other's
-    // parameters; their two averages of a span run on one XCD (k_lerp_batch)
-    int32_t pairs;
-    uint32_t pair_end;              // workgroups [0, pair_end) belong to the pairs
-    uint32_t pair_begin[kMaxAvgBatch / 2];
-    uint32_t spans[kMaxAvgBatch];   // spans of each entry (the last one may be empty)
+    // span order over equal-size entries (launcher): 0 one entry after the other, 1 dealt
+    // round-robin, 2 XCD-grouped (every entry's span s on XCD s % 8, one after the other: entries
+    // that read the same buffer -- resident learners that picked each other -- share it in L2)
+    int32_t interleave;
+    uint32_t spans;                 // spans per entry (XCD-grouped: equal sizes; the last may be empty)
     uint32_t begin[kMaxAvgBatch];   // first workgroup of each entry (filled by the launcher)
     AvgEntry e[kMaxAvgBatch];
 };

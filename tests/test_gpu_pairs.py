@@ -1,11 +1,12 @@
-"""Mutual pairs in the resident batched dispatch (k_lerp_batch, kernels.hip launch_average_batch):
-two co-resident resident learners that average with each other in a round read the same two
-snapshots -- A reads its published slot and B's, B its own and A's -- so the launcher puts each
-pair's two averages of a span in workgroups b and b + 8 (one XCD under round-robin dispatch) and
-the second read of every span hits that XCD's L2.  Only the placement changes: every entry must
-still be exactly the single-learner fused average (factor, clock, lerp into the next slot, ragged
-tail, ZeroDivision no-op) against the CPU oracle, whatever the mix of pairs and single entries
-in the dispatch, and the published slots must stay untouched."""
+"""Shared reads in the resident batched dispatch (k_lerp_batch's XCD-grouped span order,
+kernels.hip launch_average_batch): co-resident resident learners read each other's published
+slots -- two that average with each other both read both slots, and a slot is read by its owner
+and by every learner that picked it -- so for equal-size entries that share a read the launcher
+runs every entry's span s on XCD s % 8, one after the other (for two entries: workgroups b and
+b + 8), and the later reads of a span hit that XCD's L2.  Only the placement changes: every entry
+must still be exactly the single-learner fused average (factor, clock, lerp into the next slot,
+ragged tail, ZeroDivision no-op) against the CPU oracle, whatever the mix of sharing and
+non-sharing entries in the dispatch, and the published slots must stay untouched."""
 import ctypes
 
 import numpy as np
@@ -98,14 +99,18 @@ def test_mutual_pair_vs_oracle(dtype, n):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_pairs_and_single_entries_in_one_dispatch(dtype):
-    """Eight learners, descriptors in a scrambled order: two mutual pairs (found wherever they
-    are in the list), entries that read a peer without being read back, and one whose peer
-    averages with a third learner; equal and unequal sizes mixed (unequal never pair)."""
+@pytest.mark.parametrize("mixed", [False, True])
+def test_shared_reads_in_one_dispatch(dtype, mixed):
+    """Seven learners' averages in one dispatch, descriptors in a scrambled order: two mutual
+    pairs, a slot read by three learners, entries whose peer reads someone else; all sizes equal
+    (XCD-grouped: 8 entries' spans on one XCD) or one entry smaller (the other span orders)."""
     rng = np.random.default_rng(3)
-    sizes = [40_009, 40_009, 40_009, 40_009, 40_009, 123, 40_009, 40_009]
-    ls = [Learner(n, dtype, rng, 1.0 + i, 0.25 + 0.1 * i) for i, n in enumerate(sizes)]
-    picks = [(2, 6), (0, 3), (6, 2), (4, 0), (3, 0), (7, 2), (1, 4)]
+    n = 8 * 64 * 4 * 3 + 4099
+    sizes = [n] * 8
+    if mixed:
+        sizes[5] = 123
+    ls = [Learner(m, dtype, rng, 1.0 + i, 0.25 + 0.1 * i) for i, m in enumerate(sizes)]
+    picks = [(2, 6), (0, 3), (6, 2), (4, 0), (3, 0), (7, 2), (1, 4)] + ([(5, 1)] if mixed else [(5, 0)])
     for got, exp, _, me in _run(ls, picks, dtype):
         assert olerp.bits_equal(got, exp)
 
