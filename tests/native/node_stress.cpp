@@ -52,6 +52,7 @@ int main(int argc, char **argv)
     const uint32_t seed0 = argc > 3 ? (uint32_t)atoi(argv[3]) : 100;
     const double fp = argc > 4 ? atof(argv[4]) : 1.0;
     const int fault_pct = argc > 5 ? atoi(argv[5]) : 0;     // % of (round, learner, peer) with a fault
+    const int prefetch = argc > 6 ? atoi(argv[6]) : 0;       // start every granted fetch once all have published
     g_rng = seed0 * 7919ULL + (uint64_t)G;
     if (G < 2 || G > 16 || rounds < 1) return 1;
     const dpwa_interp cfg{DPWA_INTERP_CONSTANT, 0, 0.5, 0.0};
@@ -99,6 +100,8 @@ int main(int argc, char **argv)
         }
         for (int g = 0; g < G; ++g)
             CHECK(dpwa_node_update_send(nodes[g], nullptr, 1.0, nullptr, 0, nullptr, &fetching[g]));
+        if (prefetch)   // LocalGroup(prefetch=True): the pulls start before the training step
+            for (int g = 0; g < G; ++g) CHECK(dpwa_node_start_fetch(nodes[g], 0, nullptr));
         for (int g = 0; g < G; ++g) {
             int before[5], after[5], peer = -2, f = 0, fp_ = 0, att = 0;
             uint64_t fv = 0;
