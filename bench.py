@@ -88,6 +88,9 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup-s", type=float, default=0.25,
+                    help="after the W warmup steps, more untimed rounds until about this many seconds of rounds "
+                         "have run (the same count on every rank), so the timed steps see steady-state clocks")
     ap.add_argument("--numel", type=int, default=RESNET18_NUMEL)
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32")
     ap.add_argument("--interpolation", choices=["constant", "clock", "loss"], default="constant")
@@ -1224,11 +1227,13 @@ def main(argv=None):
             return 1.0
         return 2.0 * float(np.exp(-loss_t[0] / 200.0)) + 0.05 * float(loss_rngs[i].random())
 
-    def run(steps, warmup, write_through, sample_every=0):
+    def run(steps, warmup, write_through, sample_every=0, warmup_s=0.0):
         """`steps` timed lock-step rounds.  sample_every == 0: nothing but the rounds (the
         pass `value` comes from).  sample_every = k > 0: the averaging dispatch of every k-th
         step is timed by its own dispatch events (and/or bracketed by an event pair on its
-        stream) -- the in-loop kernel figure, from a separate pass."""
+        stream) -- the in-loop kernel figure, from a separate pass.  warmup_s: after the
+        `warmup` rounds, more untimed rounds up to about that many seconds in all (a count agreed
+        by every rank from the warmup rounds' time)."""
         lerp_events = []
         sampled = []        # batched: per timed dispatch (learner whose pair timed it, averages in it)
         n_slots = (steps // sample_every + 1) * len(learners) if sample_every else 0
@@ -1296,8 +1301,20 @@ def main(argv=None):
                 done += payload is not None
             return done
 
+        t_w = time.perf_counter()
         for k in range(warmup):
             step(k, False)
+        if warmup_s > 0:
+            torch.cuda.synchronize()
+            per = (time.perf_counter() - t_w) / max(1, warmup)
+            extra = int(min(200_000, max(0, np.ceil(warmup_s / max(per, 1e-6)) - warmup)))
+            if world > 1:
+                got = [None] * world
+                dist.all_gather_object(got, extra, group=ctl)
+                extra = max(got)
+            for k in range(extra):
+                step(k, False)
+            warm_extra[0] = extra
         if sample_every:
             for conn, _ in learners:    # kernel-dispatch timing of the sampled averaging launches
                 if conn._learner is not None:
@@ -1344,6 +1361,8 @@ def main(argv=None):
             dist.all_gather_object(got, stats.tolist(), group=ctl)
             return (max(g[0] for g in got), sum(g[1] for g in got), sum(g[2] for g in got), lerp_ms)
         return elapsed, float(averaged), float(len(learners) * steps), lerp_ms
+
+    warm_extra = [0]      # untimed rounds the time-based warmup added to the main timed run
 
     def params_of(conn, flat):
         """Where a learner's parameters are now: its resident slot, else its flat buffer."""
@@ -1512,7 +1531,7 @@ def main(argv=None):
     wt_main = pull.endswith("+wt") if sel_async else wt_lockstep
     form = "resident" if resident_main else "write-through" if wt_main else "full"
     wd.enter("timed run: %s, %s publish" % (pull, form), 600.0 + 0.05 * (args.steps + args.warmup))
-    elapsed, averaged, rounds, _ = run(args.steps, args.warmup, wt_main)
+    elapsed, averaged, rounds, _ = run(args.steps, args.warmup, wt_main, warmup_s=args.warmup_s)
     progress("timed run: %.4f ms/step" % (1e3 * elapsed / args.steps))
     # the averaging kernel inside the loop: a separate sampled pass of the same rounds
     wd.enter("in-loop kernel timing", 600.0)
@@ -1722,6 +1741,9 @@ def main(argv=None):
                 "parallelism": "gossip x%d" % int(rounds / args.steps),
                 "streams": args.streams,
             },
+            "warmup_rounds": {"steps": args.warmup, "time_based_extra": warm_extra[0], "warmup_s": args.warmup_s,
+                              "note": "untimed rounds before the timed steps: W, then more up to about warmup_s "
+                                      "seconds in all, so the timed steps run at steady-state clocks"},
             "value_basis": "the timed pass carries no instrumentation (no kernel timing, no events); value = 3*N*s "
                            "per completed averaging (SURVEY 8d's unit) over the wall time" +
                            ("; the two learners average with each other and share their two snapshot reads "

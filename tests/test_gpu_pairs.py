@@ -57,7 +57,8 @@ def _expect(me, peer, method, loss):
         if not (method == "loss" and loss + peer.loss == 0.0) else None
     exp = me.host.copy()
     if res is not None:
-        (olerp.c_lerp_f32_ if me.dtype == "f32" else olerp.c_lerp_bf16_)(exp, peer.host, res[0])
+        (olerp.c_lerp_f32_ if me.dtype == "f32" else olerp.c_lerp_bf16_)(exp, np.ascontiguousarray(peer.host[:me.n]),
+                                                                         res[0])
     return exp, res
 
 
