@@ -1762,6 +1762,12 @@ def main(argv=None):
                 "kernel": kname,
                 "learners_per_launch": per_launch,
                 "bytes_per_launch": kbytes,
+                # SURVEY 8d's per-unit figure (3*N*s per averaging) times the averagings one launch
+                # completes; equals bytes_per_launch except for the mutual pair, whose shared reads move
+                # fewer HBM bytes than its two averagings count
+                "algorithmic_bytes_per_launch": 3 * args.numel * esize * per_launch if resident_main else kbytes,
+                "algorithmic_rate_gbs": round((3 * args.numel * esize * per_launch if resident_main else kbytes)
+                                              / (k_us * 1e-6) / 1e9, 1),
                 "bytes_note": ("4*N*s: the two resident learners average with each other, so the dispatch's two "
                                "averages read the same two published slots: each is read from HBM once (each span's "
                                "two averages run in workgroups b and b+8, one XCD, and the second read hits its L2) "

@@ -120,13 +120,14 @@ def test_overrun_after_the_measurement_prints_the_finished_line():
 def test_committed_pmc_traffic_is_found_for_the_line_kernels():
     """The bench line's `roofline.traffic` and `reference_loop.kernel_cold[*].traffic_x` come from
     committed PMC summaries (profiles/traffic_<round>_*.json, newest round first); each of the
-    four cold kernels of configs[1] has one, within 0.1 % of its algorithmic bytes."""
+    cold kernels of configs[1] has one, within 0.1 % of its algorithmic bytes -- the mutual pair
+    (two resident learners reading each other's slot, XCD-grouped) at its distinct 4*N*s."""
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
     import bench
     n = bench.RESNET18_NUMEL
     for publish, learners, per in (("resident", 2, 3), ("resident", 1, 3), ("write-through", 2, 4),
-                                   ("write-through", 1, 4)):
+                                   ("write-through", 1, 4), ("resident-pair", 2, 2)):
         tb, src = bench.pmc_traffic(None, publish, learners, n, "f32", "cold")
         assert tb and src.startswith("profiles/traffic_"), (publish, learners)
         assert abs(tb / (learners * per * n * 4) - 1) < 1e-3, (publish, learners, tb)
