@@ -1682,11 +1682,16 @@ def main(argv=None):
         value = averaged * unit_bytes / elapsed / 1e9
         lerp_us = float(np.nanmean(lerp_ms) * 1e3)
         # each timed dispatch moved (averages in it) x 4*N*s (3*N*s): the aggregate rate
-        k1 = kbytes / per_launch
+        # algorithmic bytes: SURVEY 8d's per-unit figure (3*N*s per averaging; 4*N*s for the write-through
+        # kernel, which also writes the next snapshot) times the averagings a launch completes.  The mutual
+        # pair moves fewer HBM bytes than that (kbytes = 4*N*s for its two averagings): the `hbm` block.
+        alg_bytes = 3 * args.numel * esize * per_launch if pair_kernel else kbytes
+        k1 = alg_bytes / per_launch
         live_gbs = float(np.nansum(lerp_navg * k1) / np.nansum(lerp_ms * 1e-3) / 1e9) if np.isfinite(lerp_us) \
             else float("nan")
         k_us = cold["avg_launch_us"] if cold else lerp_us
-        achieved = kbytes / (k_us * 1e-6) / 1e9
+        achieved = alg_bytes / (k_us * 1e-6) / 1e9
+        hbm_achieved = kbytes / (k_us * 1e-6) / 1e9
         variant = form
         traffic, traffic_src = pmc_traffic(args.traffic, "resident-pair" if pair_kernel else variant, per_launch,
                                            args.numel, args.dtype, "cold" if cold else "in-loop")
@@ -1747,8 +1752,8 @@ def main(argv=None):
             "value_basis": "the timed pass carries no instrumentation (no kernel timing, no events); value = 3*N*s "
                            "per completed averaging (SURVEY 8d's unit) over the wall time" +
                            ("; the two learners average with each other and share their two snapshot reads "
-                            "(roofline.bytes_per_launch = 4*N*s for both averagings), so value is not an HBM rate and "
-                            "can exceed the HBM peak" if pair_kernel else ""),
+                            "(roofline.hbm.bytes_per_launch = 4*N*s for both averagings), so value is not an HBM rate "
+                            "and can exceed the HBM peak" if pair_kernel else ""),
             "gossip_rounds_per_s": round(rounds / elapsed, 1),
             "gossip_rounds_per_s_per_learner": round(rounds / elapsed / (rounds / args.steps), 1),
             "averagings": int(averaged),
@@ -1761,18 +1766,18 @@ def main(argv=None):
                 "traffic": traffic,
                 "kernel": kname,
                 "learners_per_launch": per_launch,
-                "bytes_per_launch": kbytes,
-                # SURVEY 8d's per-unit figure (3*N*s per averaging) times the averagings one launch
-                # completes; equals bytes_per_launch except for the mutual pair, whose shared reads move
-                # fewer HBM bytes than its two averagings count
-                "algorithmic_bytes_per_launch": 3 * args.numel * esize * per_launch if resident_main else kbytes,
-                "algorithmic_rate_gbs": round((3 * args.numel * esize * per_launch if resident_main else kbytes)
-                                              / (k_us * 1e-6) / 1e9, 1),
-                "bytes_note": ("4*N*s: the two resident learners average with each other, so the dispatch's two "
-                               "averages read the same two published slots: each is read from HBM once (each span's "
-                               "two averages run in workgroups b and b+8, one XCD, and the second read hits its L2) "
-                               "and the two next slots are written. The metric's unit counts 3*N*s per averaging "
-                               "(SURVEY 8d), 6*N*s for the two, so `value` can exceed the HBM peak"
+                "bytes_per_launch": alg_bytes,
+                "hbm": {"bytes_per_launch": kbytes, "achieved": round(hbm_achieved, 1),
+                        "frac": round(hbm_achieved / HBM_PEAK_GBS, 4),
+                        "traffic_x": round(traffic / kbytes, 4) if traffic else None,
+                        "note": "the bytes the launch must move through HBM: equal to bytes_per_launch except for "
+                                "the mutual pair, whose two averagings share their two snapshot reads (4*N*s)"},
+                "bytes_note": ("6*N*s: two averagings of 3*N*s (SURVEY 8d's unit: read the parameters, read the peer "
+                               "snapshot, write the next slot) in one dispatch. The two resident learners average "
+                               "with each other, so both averagings read the same two published slots; each span's "
+                               "two averagings run in workgroups b and b+8, one XCD, and the second read of a span "
+                               "hits its L2. The launch therefore moves only 4*N*s through HBM (`hbm`, confirmed by "
+                               "`traffic`), and `achieved` / `frac` on the algorithmic 6*N*s can exceed the HBM peak"
                                if pair_kernel else
                                ("%d x " % per_launch if per_launch > 1 else "") +
                                ("3*N*s: read the parameters (the published slot they are in), read the peer "
@@ -1810,9 +1815,10 @@ def main(argv=None):
                              "there it is link-bound and its bytes are not all HBM bytes"),
                 },
                 "traffic_source": traffic_src,
-                "vs_measured_ceiling": {"gbs": HBM_MEASURED_GBS, "frac": round(achieved / HBM_MEASURED_GBS, 4),
+                "vs_measured_ceiling": {"gbs": HBM_MEASURED_GBS, "frac": round(hbm_achieved / HBM_MEASURED_GBS, 4),
                                         "source": "MI355X_MICROARCH.md: 6.29 TB/s measured for a float4 copy "
-                                                  "(79 % of the 8 TB/s spec); peak above stays the spec"},
+                                                  "(79 % of the 8 TB/s spec); peak above stays the spec; "
+                                                  "HBM bytes (the hbm block)"},
             },
         })
         if cold_plain is not None:
