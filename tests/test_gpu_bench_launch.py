@@ -93,3 +93,23 @@ def test_resident_parity_failure_falls_back_to_write_through():
     assert out["parity"]["local+res"] is False and out["parity"]["local"] is True
     assert "publish_fallback" in out and out["config"]["publish"] == "write-through"
     assert out["value"] > 0 and out["parity_of_timed_transport"] == {"transport": "local", "ok": True}
+
+
+def test_one_gpu_line_prices_the_mutual_pair_on_algorithmic_and_hbm_bytes():
+    """N=1 resident: the two learners average with each other in one dispatch, so the roofline
+    counts §8(d)'s 3*N*s per averaging for both (6*N*s, `bytes_per_launch`, `achieved`, `frac`)
+    and, in `hbm`, the 4*N*s the shared reads leave to move; both rates come from one launch time."""
+    n = 1_000_003
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--numel", str(n), "--steps", "5",
+                        "--warmup", "2", "--no-cpu-baseline", "--no-sweep", "--compute-us", "0", "--no-secondary"],
+                       cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=280)
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads(lines[0])
+    r = out["roofline"]
+    assert out["config"]["publish"] == "resident" and r["learners_per_launch"] == 2 and r["cold"]["mutual_pair"]
+    assert r["bytes_per_launch"] == 6 * n * 4 and r["hbm"]["bytes_per_launch"] == 4 * n * 4
+    assert abs(r["achieved"] / r["hbm"]["achieved"] - 1.5) < 1e-3
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3 and r["hbm"]["traffic_x"] is None
