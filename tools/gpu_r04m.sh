@@ -6,7 +6,7 @@ set -o pipefail
 TAG=${1:-r04m}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for N in 2 8; do
+for N in ${NS:-2 8}; do
   t0=$(date +%s)
   timeout -k 10 600 python -u bench.py --gpus $N --dist-backend gloo --dist-sweep-max-numel 100000000 --steps 20 \
       --warmup 5 --no-cpu-baseline > gpurun_out/rh_${TAG}_n$N.json 2> gpurun_out/rh_${TAG}_n$N.err
