@@ -834,7 +834,7 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
     (dpwa_average_many_resident): the parameters are read from one snapshot payload and the result
     stored into another, nothing written back in place (3*N*s).  `pair` (resident, 2 learners): the
     two learners average with each other, as the N=1 loop's do -- entry 0 reads A's slot and B's,
-    entry 1 B's and A's -- so the dispatch is a mutual pair (k_lerp_batch's XCD pairing: 4*N*s)."""
+    entry 1 B's and A's -- so the dispatch is a mutual pair (k_lerp_pair: 4*N*s)."""
     from dpwa_amd import _lib
     esize = 4 if dtype == torch.float32 else 2
     write_through = write_through or resident
@@ -1650,7 +1650,7 @@ def main(argv=None):
     per_launch = len(learners) if batched else 1
     wt_kernel = wt_main and not resident_main      # resident: the kernel moves the averaging's 3*N*s only
     # the N=1 resident loop's two learners average with each other: one mutual pair per dispatch,
-    # whose two averages read the same two snapshots (k_lerp_batch's XCD pairing): 4*N*s per launch
+    # whose two averages read the same two snapshots (k_lerp_pair: both read once per span): 4*N*s per launch
     pair_kernel = resident_main and per_launch == 2
     kbytes = (4 * args.numel * esize if pair_kernel else
               (4 if wt_kernel else 3) * args.numel * esize * per_launch)   # the timed loop's averaging dispatch
@@ -1696,10 +1696,13 @@ def main(argv=None):
         traffic, traffic_src = pmc_traffic(args.traffic, "resident-pair" if pair_kernel else variant, per_launch,
                                            args.numel, args.dtype, "cold" if cold else "in-loop")
         if resident_main:
-            kname = ("dpwa::k_lerp_batch<Ops%s, true, 8, true> (%d resident learners' fused device factor + lerp "
-                     "in one dispatch: each reads its published slot and writes the other; the two average with each "
-                     "other, a mutual pair whose two averages of a span run on one XCD)" % (args.dtype.upper(),
-                                                                                             per_launch)
+            kname = ("dpwa::k_lerp_pair<Ops%s, 8> (the two resident learners average with each other, a mutual "
+                     "pair: one workgroup per span reads both published slots once and stores both averages, fused "
+                     "device factor + lerp, into the two next slots)" % args.dtype.upper()
+                     if pair_kernel else
+                     "dpwa::k_lerp_batch<Ops%s, true, 8, true> (%d resident learners' fused device factor + lerp "
+                     "in one dispatch: each reads its published slot and writes the other)" % (args.dtype.upper(),
+                                                                                              per_launch)
                      if per_launch > 1 else
                      "dpwa::k_lerp<Ops%s, COEF_FUSED, true, 64, 8, true> (resident: fused device factor + lerp "
                      "from the published slot into the other)" % args.dtype.upper())
@@ -1774,10 +1777,10 @@ def main(argv=None):
                                 "the mutual pair, whose two averagings share their two snapshot reads (4*N*s)"},
                 "bytes_note": ("6*N*s: two averagings of 3*N*s (SURVEY 8d's unit: read the parameters, read the peer "
                                "snapshot, write the next slot) in one dispatch. The two resident learners average "
-                               "with each other, so both averagings read the same two published slots; each span's "
-                               "two averagings run in workgroups b and b+8, one XCD, and the second read of a span "
-                               "hits its L2. The launch therefore moves only 4*N*s through HBM (`hbm`, confirmed by "
-                               "`traffic`), and `achieved` / `frac` on the algorithmic 6*N*s can exceed the HBM peak"
+                               "with each other, so both averagings read the same two published slots; one "
+                               "workgroup per span loads each once and computes both. The launch therefore moves "
+                               "only 4*N*s through HBM (`hbm`, confirmed by `traffic`), and `achieved` / `frac` on "
+                               "the algorithmic 6*N*s can exceed the HBM peak"
                                if pair_kernel else
                                ("%d x " % per_launch if per_launch > 1 else "") +
                                ("3*N*s: read the parameters (the published slot they are in), read the peer "

@@ -434,6 +434,54 @@ __global__ __launch_bounds__(kStreamBlock) void k_lerp_batch(AvgBatch batch)
                                                                            ContigSrc{(const char *)e.peer}, e.n, args);
 }
 
+// A mutual pair of resident averages in one pass: entry 0's parameters are entry 1's peer
+// snapshot and the other way round (the N=1 loop's two learners, each the other's only peer),
+// so one workgroup per span reads the two published slots once each and stores both averages
+// into their next slots -- 2 loads and 2 stores per lane where the batched span code spends 4
+// loads (2 served by L2) and 2 stores over two workgroups, and one fp64 factor evaluation per
+// entry per workgroup as there.  Per entry exactly k_lerp_batch's span code: the factor and its
+// commit by workgroup 0, the ZeroDivision no-op (the parameters stored unchanged), the ragged
+// tail in workgroup 0.
+template <class Ops, int POLICY>
+__global__ __launch_bounds__(kStreamBlock) void k_lerp_pair(AvgBatch batch)
+{
+    using V = typename Ops::V;
+    using S = typename Ops::S;
+    using P = LerpPolicy<POLICY>;
+    constexpr int SPAN = kStreamBlock * 16;
+    const AvgEntry &e0 = batch.e[0];
+    const AvgEntry &e1 = batch.e[1];
+    const int64_t n = e0.n;
+    const int64_t nv = n / Ops::PER;
+    const uint32_t blk = blockIdx.x;
+    const int64_t off = (int64_t)blk * SPAN;
+    const int lane_off = threadIdx.x * 16;
+    // issue both loads first: x = entry 0's parameters (entry 1's peer), y = the reverse
+    const V x = span_load<V, P::param_load>(span_rsrc<SPAN>(e0.param, off, nv * 16), lane_off);
+    const V y = span_load<V, P::param_load>(span_rsrc<SPAN>(e1.param, off, nv * 16), lane_off);
+    const dpwa_coef c0 = factor_math(e0.fa.cfg, *e0.fa.clock_in, e0.fa.hdr->clock, e0.fa.hdr->loss,
+                                     read_loss(e0.fa.loss_d, e0.fa.loss_f32, e0.fa.loss_h));
+    const dpwa_coef c1 = factor_math(e1.fa.cfg, *e1.fa.clock_in, e1.fa.hdr->clock, e1.fa.hdr->loss,
+                                     read_loss(e1.fa.loss_d, e1.fa.loss_f32, e1.fa.loss_h));
+    if (blk == 0 && threadIdx.x == 0) {
+        factor_commit(e0.fa, c0);
+        factor_commit(e1.fa, c1);
+    }
+    const bool ok0 = c0.status == DPWA_STATUS_OK;
+    const bool ok1 = c1.status == DPWA_STATUS_OK;
+    span_store<V, P::snap_store>(span_rsrc<SPAN>(e0.snap, off, nv * 16), lane_off,
+                                 ok0 ? Ops::lerp(c0.a, c0.b, y, x) : x);
+    span_store<V, P::snap_store>(span_rsrc<SPAN>(e1.snap, off, nv * 16), lane_off,
+                                 ok1 ? Ops::lerp(c1.a, c1.b, x, y) : y);
+    if (blk == 0 && threadIdx.x < n - nv * Ops::PER) {
+        const int64_t j = nv * Ops::PER + threadIdx.x;
+        const S a = reinterpret_cast<const S *>(e0.param)[j];
+        const S b = reinterpret_cast<const S *>(e1.param)[j];
+        reinterpret_cast<S *>(e0.snap)[j] = ok0 ? Ops::lerp_s(c0.a, c0.b, b, a) : a;
+        reinterpret_cast<S *>(e1.snap)[j] = ok1 ? Ops::lerp_s(c1.a, c1.b, a, b) : b;
+    }
+}
+
 // Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
 template <class Ops, int MODE, bool DUAL>
 __global__ __launch_bounds__(kBlock) void k_lerp_unaligned(typename Ops::S *__restrict__ param,
@@ -662,6 +710,17 @@ static bool batch_share()
     return on;
 }
 
+// A mutual resident pair runs as k_lerp_pair (one workgroup per span for both averages);
+// DPWA_PAIR_FUSED=0 keeps it on the XCD-grouped batch (A/B runs).
+static bool pair_fused()
+{
+    static const bool on = [] {
+        const char *e = getenv("DPWA_PAIR_FUSED");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
 // Some buffer is read by two entries (as parameters or as the peer snapshot).
 static bool shares_a_read(const AvgBatch &x)
 {
@@ -707,6 +766,28 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
     // own parameters and another's peer): XCD-grouped, whatever the size (nothing writes what they
     // read, so any order is safe)
     x.spans = (uint32_t)((x.e[0].n / per) / kStreamBlock + 1);
+    if (oop && same && x.count == 2 && order < 0 && batch_share() && pair_fused() && x.e[0].peer == x.e[1].param &&
+        x.e[1].peer == x.e[0].param) {
+        // a mutual pair: both averages in one workgroup per span
+#define DPWA_PAIR_LAUNCH(OPS, P)                                                                             \
+    do {                                                                                                    \
+        if (timing)                                                                                         \
+            hipExtLaunchKernelGGL((k_lerp_pair<OPS, P>), dim3(x.spans), dim3(kStreamBlock), 0, s,            \
+                                  timing->start, timing->stop, 0, x);                                       \
+        else                                                                                                \
+            hipLaunchKernelGGL((k_lerp_pair<OPS, P>), dim3(x.spans), dim3(kStreamBlock), 0, s, x);         \
+    } while (0)
+        const bool p0 = lerp_policy() == 0;
+        if (dtype == DPWA_F32) {
+            if (p0) DPWA_PAIR_LAUNCH(OpsF32, 0);
+            else DPWA_PAIR_LAUNCH(OpsF32, kProductPolicy);
+        } else {
+            if (p0) DPWA_PAIR_LAUNCH(OpsBF16, 0);
+            else DPWA_PAIR_LAUNCH(OpsBF16, kProductPolicy);
+        }
+#undef DPWA_PAIR_LAUNCH
+        return hipGetLastError();
+    }
     if (oop && same && x.count > 1 && order < 0 && batch_share() && shares_a_read(x)) {
         const uint64_t gg = (uint64_t)(x.spans + 7) / 8 * 8 * (uint64_t)x.count;
         if (gg > 0x7fffffffu) return hipErrorInvalidValue;

@@ -1,12 +1,13 @@
-"""Shared reads in the resident batched dispatch (k_lerp_batch's XCD-grouped span order,
-kernels.hip launch_average_batch): co-resident resident learners read each other's published
-slots -- two that average with each other both read both slots, and a slot is read by its owner
-and by every learner that picked it -- so for equal-size entries that share a read the launcher
-runs every entry's span s on XCD s % 8, one after the other (for two entries: workgroups b and
-b + 8), and the later reads of a span hit that XCD's L2.  Only the placement changes: every entry
-must still be exactly the single-learner fused average (factor, clock, lerp into the next slot,
-ragged tail, ZeroDivision no-op) against the CPU oracle, whatever the mix of sharing and
-non-sharing entries in the dispatch, and the published slots must stay untouched."""
+"""Shared reads in the resident batched dispatch (kernels.hip launch_average_batch): co-resident
+resident learners read each other's published slots -- two that average with each other both read
+both slots, and a slot is read by its owner and by every learner that picked it.  A mutual pair
+(two entries, each the other's peer: the N=1 loop) runs as k_lerp_pair, one workgroup per span
+loading both slots once and storing both averages; other equal-size entries that share a read run
+k_lerp_batch's XCD-grouped span order (every entry's span s on XCD s % 8, one after the other, so
+the later reads of a span hit that XCD's L2).  Either way every entry must still be exactly the
+single-learner fused average (factor, clock, lerp into the next slot, ragged tail, ZeroDivision
+no-op) against the CPU oracle, whatever the mix of sharing and non-sharing entries in the
+dispatch, and the published slots must stay untouched."""
 import ctypes
 
 import numpy as np
@@ -112,6 +113,20 @@ def test_shared_reads_in_one_dispatch(dtype, mixed):
         sizes[5] = 123
     ls = [Learner(m, dtype, rng, 1.0 + i, 0.25 + 0.1 * i) for i, m in enumerate(sizes)]
     picks = [(2, 6), (0, 3), (6, 2), (4, 0), (3, 0), (7, 2), (1, 4)] + ([(5, 1)] if mixed else [(5, 0)])
+    for got, exp, _, me in _run(ls, picks, dtype):
+        assert olerp.bits_equal(got, exp)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("picks", [[(0, 1), (2, 1)], [(0, 1), (1, 2)], [(1, 0), (0, 1)]],
+                         ids=["same-peer", "chain", "mutual-reversed"])
+def test_two_entries_sharing_a_read(dtype, picks):
+    """Two entries that share a read without being a mutual pair (both pick the same peer; one's
+    peer is the other's parameters) take the XCD-grouped batch; the mutual pair given in the other
+    order takes k_lerp_pair: each bit-exact with the C oracle."""
+    rng = np.random.default_rng(17)
+    n = 8 * 64 * 4 * 5 + 4097
+    ls = [Learner(n, dtype, rng, 1.5 + i, 0.3 + 0.2 * i) for i in range(3)]
     for got, exp, _, me in _run(ls, picks, dtype):
         assert olerp.bits_equal(got, exp)
 

@@ -24,6 +24,7 @@ for fl in resident-pair:2 resident:1 write-through:2 write-through:1; do
   oop=$([ $form = write-through ] && echo false || echo true)
   k="k_lerp<dpwa::OpsF32, 2, true, 64, 8, $oop>"; suf=""
   [ $L -gt 1 ] && { k="k_lerp_batch<dpwa::OpsF32, true, 8, $oop>"; suf="_x$L"; }
+  [ $form = resident-pair ] && k="k_lerp_pair<dpwa::OpsF32, 8>"
   python3 tools/pmc_traffic.py gpurun_out/pmc_${TAG}_${form}_FETCH_SIZE_x$L gpurun_out/pmc_${TAG}_${form}_WRITE_SIZE_x$L \
       --kernel "$k" --publish $form --learners $L --basis cold --out gpurun_out/traffic_${TAG}_$form$suf.json || exit 1
 done
