@@ -106,6 +106,35 @@ def test_average_many_zero_division_entry_is_a_noop(dtype):
         assert olerp.bits_equal(got, ents[i]["exp"]), i
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("write_through", [False, True])
+@pytest.mark.parametrize("n", [0, 1, 5, 4099, 8 * 64 * 4, 65536 + 13, (1 << 20) + 5])
+@pytest.mark.parametrize("zero_div_at", [None, 0, 1])
+def test_two_equal_entries_vs_oracle(dtype, write_through, n, zero_div_at):
+    """Two equal-size in-place entries -- the N=1 reference loop's write-through pair, its spans
+    dealt round-robin: each bit-exact with the C oracle at ragged sizes, clocks and coefficient
+    blocks written, a ZeroDivision entry (loss interpolation, loss + peer loss == 0) left unchanged
+    with its snapshot still written, whichever of the two it is."""
+    method = "loss" if zero_div_at is not None else "clock"
+    ents = _entries([n, n], dtype, 90 + n % 97, write_through, method=method, zero_div_at=zero_div_at)
+    before = [e["p"].clone() for e in ents]
+    cfg = _lib.Interp(_lib.INTERP_LOSS if method == "loss" else _lib.INTERP_CLOCK, 0, 0.0, 0.0)
+    _lib.call("dpwa_average_many", _lib.F32 if dtype == "f32" else _lib.BF16, _descs(ents), 2,
+              ctypes.byref(cfg), stream(), None, None)
+    torch.cuda.synchronize()
+    for i, e in enumerate(ents):
+        c = _lib.Coef.from_buffer_copy(e["coef"].cpu().numpy().tobytes())
+        if i == zero_div_at:
+            assert c.status == _lib.STATUS_ZERO_DIVISION and torch.equal(e["p"], before[i])
+            assert e["clock"][1].item() == e["my_clock"]
+        else:
+            got = e["p"].cpu().numpy() if dtype == "f32" else to_u16(e["p"])
+            assert olerp.bits_equal(got, e["exp"]), (i, n)
+            assert c.status == 0 and c.factor == e["res"][0] and e["clock"][1].item() == e["res"][1], i
+        if write_through and n:
+            assert torch.equal(e["snap"].view(torch.uint8), e["p"].view(torch.uint8)), i
+
+
 def test_average_many_argument_errors():
     ents = _entries([64, 64], "f32", 3, True)
     d = _descs(ents)
