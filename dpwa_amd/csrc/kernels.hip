@@ -777,12 +777,19 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
         else                                                                                                \
             hipLaunchKernelGGL((k_lerp_pair<OPS, P>), dim3(x.spans), dim3(kStreamBlock), 0, s, x);         \
     } while (0)
-        const bool p0 = lerp_policy() == 0;
+        // cache-policy variants for tuning (DPWA_LERP_POLICY); both loads take the parameter load's
+        // policy (each slot is one entry's parameters and the other's peer)
         if (dtype == DPWA_F32) {
-            if (p0) DPWA_PAIR_LAUNCH(OpsF32, 0);
-            else DPWA_PAIR_LAUNCH(OpsF32, kProductPolicy);
+            switch (lerp_policy()) {
+            case 0: DPWA_PAIR_LAUNCH(OpsF32, 0); break;
+            case 1: DPWA_PAIR_LAUNCH(OpsF32, 1); break;
+            case 2: DPWA_PAIR_LAUNCH(OpsF32, 2); break;
+            case 16: DPWA_PAIR_LAUNCH(OpsF32, 16); break;
+            case 32: DPWA_PAIR_LAUNCH(OpsF32, 32); break;
+            default: DPWA_PAIR_LAUNCH(OpsF32, kProductPolicy); break;
+            }
         } else {
-            if (p0) DPWA_PAIR_LAUNCH(OpsBF16, 0);
+            if (lerp_policy() == 0) DPWA_PAIR_LAUNCH(OpsBF16, 0);
             else DPWA_PAIR_LAUNCH(OpsBF16, kProductPolicy);
         }
 #undef DPWA_PAIR_LAUNCH
