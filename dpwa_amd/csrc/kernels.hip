@@ -434,52 +434,80 @@ __global__ __launch_bounds__(kStreamBlock) void k_lerp_batch(AvgBatch batch)
                                                                            ContigSrc{(const char *)e.peer}, e.n, args);
 }
 
-// A mutual pair of resident averages in one pass: entry 0's parameters are entry 1's peer
-// snapshot and the other way round (the N=1 loop's two learners, each the other's only peer),
-// so one workgroup per span reads the two published slots once each and stores both averages
-// into their next slots -- 2 loads and 2 stores per lane where the batched span code spends 4
-// loads (2 served by L2) and 2 stores over two workgroups, and one fp64 factor evaluation per
-// entry per workgroup as there.  Per entry exactly k_lerp_batch's span code: the factor and its
-// commit by workgroup 0, the ZeroDivision no-op (the parameters stored unchanged), the ragged
-// tail in workgroup 0.
-template <class Ops, int POLICY>
-__global__ __launch_bounds__(kStreamBlock) void k_lerp_pair(AvgBatch batch)
+// A closed group of G resident averages in one pass: every entry's peer snapshot is another
+// entry's parameters (co-resident learners that picked each other; the N=1 loop's two learners,
+// each the other's only peer, are the mutual pair G = 2), so one workgroup per span loads the G
+// published slots once each and stores the G averages into their next slots -- G loads and G
+// stores per lane where the batched span code spends 2G loads (the repeated ones served by L2 at
+// best) over G workgroups, and one fp64 factor evaluation per entry per workgroup as there.  Per
+// entry exactly k_lerp_batch's span code: the factor and its commit by workgroup 0, the
+// ZeroDivision no-op (the parameters stored unchanged), the ragged tail in workgroup 0.
+template <class Ops, int POLICY, int G>
+__device__ __forceinline__ void group_span(const AvgBatch &batch)
 {
     using V = typename Ops::V;
     using S = typename Ops::S;
     using P = LerpPolicy<POLICY>;
     constexpr int SPAN = kStreamBlock * 16;
-    const AvgEntry &e0 = batch.e[0];
-    const AvgEntry &e1 = batch.e[1];
-    const int64_t n = e0.n;
+    const int64_t n = batch.e[0].n;
     const int64_t nv = n / Ops::PER;
     const uint32_t blk = blockIdx.x;
     const int64_t off = (int64_t)blk * SPAN;
     const int lane_off = threadIdx.x * 16;
-    // issue both loads first: x = entry 0's parameters (entry 1's peer), y = the reverse
-    const V x = span_load<V, P::param_load>(span_rsrc<SPAN>(e0.param, off, nv * 16), lane_off);
-    const V y = span_load<V, P::param_load>(span_rsrc<SPAN>(e1.param, off, nv * 16), lane_off);
-    const dpwa_coef c0 = factor_math(e0.fa.cfg, *e0.fa.clock_in, e0.fa.hdr->clock, e0.fa.hdr->loss,
-                                     read_loss(e0.fa.loss_d, e0.fa.loss_f32, e0.fa.loss_h));
-    const dpwa_coef c1 = factor_math(e1.fa.cfg, *e1.fa.clock_in, e1.fa.hdr->clock, e1.fa.hdr->loss,
-                                     read_loss(e1.fa.loss_d, e1.fa.loss_f32, e1.fa.loss_h));
-    if (blk == 0 && threadIdx.x == 0) {
-        factor_commit(e0.fa, c0);
-        factor_commit(e1.fa, c1);
+    V v[G];   // entry i's parameters: its own average's `p`, and the `q` of every entry that picked it
+#pragma unroll
+    for (int i = 0; i < G; ++i)   // all loads first
+        v[i] = span_load<V, P::param_load>(span_rsrc<SPAN>(batch.e[i].param, off, nv * 16), lane_off);
+    dpwa_coef c[G];
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+        const FusedArgs &fa = batch.e[i].fa;
+        c[i] = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, read_loss(fa.loss_d, fa.loss_f32, fa.loss_h));
     }
-    const bool ok0 = c0.status == DPWA_STATUS_OK;
-    const bool ok1 = c1.status == DPWA_STATUS_OK;
-    span_store<V, P::snap_store>(span_rsrc<SPAN>(e0.snap, off, nv * 16), lane_off,
-                                 ok0 ? Ops::lerp(c0.a, c0.b, y, x) : x);
-    span_store<V, P::snap_store>(span_rsrc<SPAN>(e1.snap, off, nv * 16), lane_off,
-                                 ok1 ? Ops::lerp(c1.a, c1.b, x, y) : y);
+    if (blk == 0 && threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < G; ++i) factor_commit(batch.e[i].fa, c[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+        const int k = batch.peer_of[i];   // uniform: a select over registers, no indexed access
+        V q = v[0];
+#pragma unroll
+        for (int j = 1; j < G; ++j)
+            if (k == j) q = v[j];
+        span_store<V, P::snap_store>(span_rsrc<SPAN>(batch.e[i].snap, off, nv * 16), lane_off,
+                                     c[i].status == DPWA_STATUS_OK ? Ops::lerp(c[i].a, c[i].b, q, v[i]) : v[i]);
+    }
     if (blk == 0 && threadIdx.x < n - nv * Ops::PER) {
         const int64_t j = nv * Ops::PER + threadIdx.x;
-        const S a = reinterpret_cast<const S *>(e0.param)[j];
-        const S b = reinterpret_cast<const S *>(e1.param)[j];
-        reinterpret_cast<S *>(e0.snap)[j] = ok0 ? Ops::lerp_s(c0.a, c0.b, b, a) : a;
-        reinterpret_cast<S *>(e1.snap)[j] = ok1 ? Ops::lerp_s(c1.a, c1.b, a, b) : b;
+        S t[G];
+#pragma unroll
+        for (int i = 0; i < G; ++i) t[i] = reinterpret_cast<const S *>(batch.e[i].param)[j];
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const int k = batch.peer_of[i];
+            S q = t[0];
+#pragma unroll
+            for (int m = 1; m < G; ++m)
+                if (k == m) q = t[m];
+            reinterpret_cast<S *>(batch.e[i].snap)[j] =
+                c[i].status == DPWA_STATUS_OK ? Ops::lerp_s(c[i].a, c[i].b, q, t[i]) : t[i];
+        }
     }
+}
+
+// The mutual pair (G = 2), the N=1 bench's kernel.
+template <class Ops, int POLICY>
+__global__ __launch_bounds__(kStreamBlock) void k_lerp_pair(AvgBatch batch)
+{
+    group_span<Ops, POLICY, 2>(batch);
+}
+
+// Closed groups of 3..8 co-resident learners.
+template <class Ops, int POLICY, int G>
+__global__ __launch_bounds__(kStreamBlock) void k_lerp_group(AvgBatch batch)
+{
+    group_span<Ops, POLICY, G>(batch);
 }
 
 // Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
@@ -710,8 +738,8 @@ static bool batch_share()
     return on;
 }
 
-// A mutual resident pair runs as k_lerp_pair (one workgroup per span for both averages);
-// DPWA_PAIR_FUSED=0 keeps it on the XCD-grouped batch (A/B runs).
+// A closed resident group runs as k_lerp_pair / k_lerp_group (one workgroup per span for all its
+// averages); DPWA_PAIR_FUSED=0 keeps it on the XCD-grouped batch (A/B runs).
 static bool pair_fused()
 {
     static const bool on = [] {
@@ -766,8 +794,49 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
     // own parameters and another's peer): XCD-grouped, whatever the size (nothing writes what they
     // read, so any order is safe)
     x.spans = (uint32_t)((x.e[0].n / per) / kStreamBlock + 1);
-    if (oop && same && x.count == 2 && order < 0 && batch_share() && pair_fused() && x.e[0].peer == x.e[1].param &&
-        x.e[1].peer == x.e[0].param) {
+    // a closed group: every entry's peer is another entry's parameters (distinct parameters)
+    bool closed = oop && same && x.count > 1 && order < 0 && batch_share() && pair_fused();
+    for (int i = 0; closed && i < x.count; ++i) {
+        x.peer_of[i] = -1;
+        for (int j = 0; j < x.count; ++j) {
+            if (j != i && x.e[j].param == x.e[i].param) closed = false;
+            if (j != i && x.e[j].param == x.e[i].peer) x.peer_of[i] = (int8_t)j;
+        }
+        closed = closed && x.peer_of[i] >= 0;
+    }
+    if (closed && x.count > 2) {
+#define DPWA_GROUP_LAUNCH(OPS, P, G)                                                                         \
+    do {                                                                                                    \
+        if (timing)                                                                                         \
+            hipExtLaunchKernelGGL((k_lerp_group<OPS, P, G>), dim3(x.spans), dim3(kStreamBlock), 0, s,        \
+                                  timing->start, timing->stop, 0, x);                                       \
+        else                                                                                                \
+            hipLaunchKernelGGL((k_lerp_group<OPS, P, G>), dim3(x.spans), dim3(kStreamBlock), 0, s, x);     \
+    } while (0)
+#define DPWA_GROUP_G(OPS, P)                                                                                 \
+    do {                                                                                                    \
+        switch (x.count) {                                                                                  \
+        case 3: DPWA_GROUP_LAUNCH(OPS, P, 3); break;                                                        \
+        case 4: DPWA_GROUP_LAUNCH(OPS, P, 4); break;                                                        \
+        case 5: DPWA_GROUP_LAUNCH(OPS, P, 5); break;                                                        \
+        case 6: DPWA_GROUP_LAUNCH(OPS, P, 6); break;                                                        \
+        case 7: DPWA_GROUP_LAUNCH(OPS, P, 7); break;                                                        \
+        default: DPWA_GROUP_LAUNCH(OPS, P, 8); break;                                                       \
+        }                                                                                                   \
+    } while (0)
+        const bool p0 = lerp_policy() == 0;
+        if (dtype == DPWA_F32) {
+            if (p0) DPWA_GROUP_G(OpsF32, 0);
+            else DPWA_GROUP_G(OpsF32, kProductPolicy);
+        } else {
+            if (p0) DPWA_GROUP_G(OpsBF16, 0);
+            else DPWA_GROUP_G(OpsBF16, kProductPolicy);
+        }
+#undef DPWA_GROUP_G
+#undef DPWA_GROUP_LAUNCH
+        return hipGetLastError();
+    }
+    if (closed) {
         // a mutual pair: both averages in one workgroup per span
 #define DPWA_PAIR_LAUNCH(OPS, P)                                                                             \
     do {                                                                                                    \

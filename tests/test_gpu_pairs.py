@@ -1,9 +1,10 @@
 """Shared reads in the resident batched dispatch (kernels.hip launch_average_batch): co-resident
 resident learners read each other's published slots -- two that average with each other both read
 both slots, and a slot is read by its owner and by every learner that picked it.  A mutual pair
-(two entries, each the other's peer: the N=1 loop) runs as k_lerp_pair, one workgroup per span
-loading both slots once and storing both averages; other equal-size entries that share a read run
-k_lerp_batch's XCD-grouped span order (every entry's span s on XCD s % 8, one after the other, so
+(two entries, each the other's peer: the N=1 loop) runs as k_lerp_pair, and any closed group
+(every entry's peer is another entry of the dispatch) as k_lerp_group, one workgroup per span
+loading every slot once and storing all the averages; other equal-size entries that share a read
+run k_lerp_batch's XCD-grouped span order (every entry's span s on XCD s % 8, one after the other, so
 the later reads of a span hit that XCD's L2).  Either way every entry must still be exactly the
 single-learner fused average (factor, clock, lerp into the next slot, ragged tail, ZeroDivision
 no-op) against the CPU oracle, whatever the mix of sharing and non-sharing entries in the
@@ -105,7 +106,7 @@ def test_mutual_pair_vs_oracle(dtype, n):
 def test_shared_reads_in_one_dispatch(dtype, mixed):
     """Seven learners' averages in one dispatch, descriptors in a scrambled order: two mutual
     pairs, a slot read by three learners, entries whose peer reads someone else; all sizes equal
-    (XCD-grouped: 8 entries' spans on one XCD) or one entry smaller (the other span orders)."""
+    (a closed group of eight: k_lerp_group) or one entry smaller (the batch's span orders)."""
     rng = np.random.default_rng(3)
     n = 8 * 64 * 4 * 3 + 4099
     sizes = [n] * 8
@@ -115,6 +116,48 @@ def test_shared_reads_in_one_dispatch(dtype, mixed):
     picks = [(2, 6), (0, 3), (6, 2), (4, 0), (3, 0), (7, 2), (1, 4)] + ([(5, 1)] if mixed else [(5, 0)])
     for got, exp, _, me in _run(ls, picks, dtype):
         assert olerp.bits_equal(got, exp)
+
+
+CLOSED = {
+    "3-cycle": [(0, 1), (1, 2), (2, 0)],
+    "3-star": [(0, 1), (1, 0), (2, 0)],
+    "4-two-pairs": [(3, 2), (0, 1), (2, 3), (1, 0)],
+    "4-shared": [(0, 1), (1, 0), (2, 1), (3, 1)],
+    "5": [(0, 4), (1, 0), (2, 0), (3, 2), (4, 3)],
+    "6": [(5, 0), (0, 5), (1, 2), (2, 1), (3, 4), (4, 3)],
+    "7": [(i, (i + 3) % 7) for i in range(7)],
+}
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("name", sorted(CLOSED))
+@pytest.mark.parametrize("n", [5, 8 * 64 * 4 * 3 + 4099])
+def test_closed_groups_vs_oracle(dtype, name, n):
+    """Co-resident resident learners that all picked learners of the same dispatch (a closed group:
+    cycles, stars, two mutual pairs, one slot read by three) run as k_lerp_group, one workgroup per
+    span loading every slot once: each entry bit-exact with the C oracle, ragged tails included."""
+    picks = CLOSED[name]
+    rng = np.random.default_rng(len(name) + n)
+    ls = [Learner(n, dtype, rng, 1.0 + 0.5 * i, 0.2 + 0.1 * i) for i in range(len(picks))]
+    for got, exp, _, me in _run(ls, picks, dtype):
+        assert olerp.bits_equal(got, exp)
+
+
+def test_closed_group_with_zero_division_entries():
+    """Loss interpolation in a closed group of four where two entries have loss + peer loss == 0:
+    those copy their parameters into their next slots and keep their clocks; the others average."""
+    rng = np.random.default_rng(23)
+    n = 70_003
+    ls = [Learner(n, "f32", rng, 2.0 + i, 0.0 if i in (0, 1) else 0.3 * i) for i in range(4)]
+    picks = [(0, 1), (1, 0), (2, 3), (3, 2)]
+    out = _run(ls, picks, "f32", method="loss", losses=[0.0, 0.0, 0.4, 0.7])
+    for k, (got, exp, res, me) in enumerate(out):
+        c = _lib.Coef.from_buffer_copy(me.coef.cpu().numpy().tobytes())
+        if k < 2:
+            assert res is None and olerp.bits_equal(got, me.host) and c.status == _lib.STATUS_ZERO_DIVISION
+            assert me.clock[1].item() == me.clock_val
+        else:
+            assert res is not None and olerp.bits_equal(got, exp) and c.status == 0
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
