@@ -434,61 +434,68 @@ __global__ __launch_bounds__(kStreamBlock) void k_lerp_batch(AvgBatch batch)
                                                                            ContigSrc{(const char *)e.peer}, e.n, args);
 }
 
-// A closed group of G resident averages in one pass: every entry's peer snapshot is another
-// entry's parameters (co-resident learners that picked each other; the N=1 loop's two learners,
-// each the other's only peer, are the mutual pair G = 2), so one workgroup per span loads the G
-// published slots once each and stores the G averages into their next slots -- G loads and G
-// stores per lane where the batched span code spends 2G loads (the repeated ones served by L2 at
-// best) over G workgroups, and one fp64 factor evaluation per entry per workgroup as there.  Per
-// entry exactly k_lerp_batch's span code: the factor and its commit by workgroup 0, the
-// ZeroDivision no-op (the parameters stored unchanged), the ragged tail in workgroup 0.
-template <class Ops, int POLICY, int G>
+// A group of resident averages in one pass: co-resident learners whose reads overlap (a slot is
+// one learner's parameters and another's peer snapshot, or two learners picked the same peer;
+// the N=1 loop's two learners, each the other's only peer, are the mutual pair).  The dispatch's
+// U distinct source buffers -- the entries' parameters, then peer snapshots that are no entry's
+// parameters -- are loaded once per span by one workgroup, which stores every entry's average
+// into its next slot: U loads and `count` stores per lane where the batched span code spends
+// 2*count loads (the repeated ones served by L2 at best) over `count` workgroups, and one fp64
+// factor evaluation per entry per workgroup as there.  Per entry exactly k_lerp_batch's span
+// code: the factor and its commit by workgroup 0, the ZeroDivision no-op (the parameters stored
+// unchanged), the ragged tail in workgroup 0.  Entries i < batch.count are src[i]'s averages.
+template <class Ops, int POLICY, int U>
 __device__ __forceinline__ void group_span(const AvgBatch &batch)
 {
     using V = typename Ops::V;
     using S = typename Ops::S;
     using P = LerpPolicy<POLICY>;
     constexpr int SPAN = kStreamBlock * 16;
+    const int G = batch.count;       // outputs (<= U), uniform
     const int64_t n = batch.e[0].n;
     const int64_t nv = n / Ops::PER;
     const uint32_t blk = blockIdx.x;
     const int64_t off = (int64_t)blk * SPAN;
     const int lane_off = threadIdx.x * 16;
-    V v[G];   // entry i's parameters: its own average's `p`, and the `q` of every entry that picked it
+    V v[U];
 #pragma unroll
-    for (int i = 0; i < G; ++i)   // all loads first
-        v[i] = span_load<V, P::param_load>(span_rsrc<SPAN>(batch.e[i].param, off, nv * 16), lane_off);
-    dpwa_coef c[G];
+    for (int j = 0; j < U; ++j)   // all loads first
+        v[j] = span_load<V, P::param_load>(span_rsrc<SPAN>(batch.src[j], off, nv * 16), lane_off);
+    dpwa_coef c[U];
 #pragma unroll
-    for (int i = 0; i < G; ++i) {
+    for (int i = 0; i < U; ++i) {
+        if (i >= G) break;
         const FusedArgs &fa = batch.e[i].fa;
         c[i] = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, read_loss(fa.loss_d, fa.loss_f32, fa.loss_h));
     }
     if (blk == 0 && threadIdx.x == 0) {
 #pragma unroll
-        for (int i = 0; i < G; ++i) factor_commit(batch.e[i].fa, c[i]);
+        for (int i = 0; i < U; ++i)
+            if (i < G) factor_commit(batch.e[i].fa, c[i]);
     }
 #pragma unroll
-    for (int i = 0; i < G; ++i) {
+    for (int i = 0; i < U; ++i) {
+        if (i >= G) break;
         const int k = batch.peer_of[i];   // uniform: a select over registers, no indexed access
         V q = v[0];
 #pragma unroll
-        for (int j = 1; j < G; ++j)
+        for (int j = 1; j < U; ++j)
             if (k == j) q = v[j];
         span_store<V, P::snap_store>(span_rsrc<SPAN>(batch.e[i].snap, off, nv * 16), lane_off,
                                      c[i].status == DPWA_STATUS_OK ? Ops::lerp(c[i].a, c[i].b, q, v[i]) : v[i]);
     }
     if (blk == 0 && threadIdx.x < n - nv * Ops::PER) {
         const int64_t j = nv * Ops::PER + threadIdx.x;
-        S t[G];
+        S t[U];
 #pragma unroll
-        for (int i = 0; i < G; ++i) t[i] = reinterpret_cast<const S *>(batch.e[i].param)[j];
+        for (int m = 0; m < U; ++m) t[m] = reinterpret_cast<const S *>(batch.src[m])[j];
 #pragma unroll
-        for (int i = 0; i < G; ++i) {
+        for (int i = 0; i < U; ++i) {
+            if (i >= G) break;
             const int k = batch.peer_of[i];
             S q = t[0];
 #pragma unroll
-            for (int m = 1; m < G; ++m)
+            for (int m = 1; m < U; ++m)
                 if (k == m) q = t[m];
             reinterpret_cast<S *>(batch.e[i].snap)[j] =
                 c[i].status == DPWA_STATUS_OK ? Ops::lerp_s(c[i].a, c[i].b, q, t[i]) : t[i];
@@ -496,18 +503,18 @@ __device__ __forceinline__ void group_span(const AvgBatch &batch)
     }
 }
 
-// The mutual pair (G = 2), the N=1 bench's kernel.
+// The mutual pair (two entries, two sources), the N=1 bench's kernel.
 template <class Ops, int POLICY>
 __global__ __launch_bounds__(kStreamBlock) void k_lerp_pair(AvgBatch batch)
 {
     group_span<Ops, POLICY, 2>(batch);
 }
 
-// Closed groups of 3..8 co-resident learners.
-template <class Ops, int POLICY, int G>
+// Groups of 3..8 source buffers.
+template <class Ops, int POLICY, int U>
 __global__ __launch_bounds__(kStreamBlock) void k_lerp_group(AvgBatch batch)
 {
-    group_span<Ops, POLICY, G>(batch);
+    group_span<Ops, POLICY, U>(batch);
 }
 
 // Element-wise path for pointers that are not 16-byte aligned (arbitrary views).
@@ -794,17 +801,33 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
     // own parameters and another's peer): XCD-grouped, whatever the size (nothing writes what they
     // read, so any order is safe)
     x.spans = (uint32_t)((x.e[0].n / per) / kStreamBlock + 1);
-    // a closed group: every entry's peer is another entry's parameters (distinct parameters)
-    bool closed = oop && same && x.count > 1 && order < 0 && batch_share() && pair_fused();
-    for (int i = 0; closed && i < x.count; ++i) {
-        x.peer_of[i] = -1;
-        for (int j = 0; j < x.count; ++j) {
-            if (j != i && x.e[j].param == x.e[i].param) closed = false;
-            if (j != i && x.e[j].param == x.e[i].peer) x.peer_of[i] = (int8_t)j;
-        }
-        closed = closed && x.peer_of[i] >= 0;
+    // a group: entries of equal size, distinct parameters, whose reads overlap; its sources are
+    // the parameters, then the peers that are no entry's parameters (at most kMaxAvgBatch)
+    bool grouped = oop && same && x.count > 1 && order < 0 && batch_share() && pair_fused();
+    int nsrc = x.count;
+    for (int i = 0; grouped && i < x.count; ++i) {
+        x.src[i] = x.e[i].param;
+        for (int j = 0; j < i; ++j)
+            if (x.e[j].param == x.e[i].param) grouped = false;
     }
-    if (closed && x.count > 2) {
+    for (int i = 0; grouped && i < x.count; ++i) {
+        int k = -1;
+        for (int j = 0; j < nsrc && k < 0; ++j)
+            if (x.src[j] == x.e[i].peer) k = j;
+        if (k < 0) {
+            if (nsrc == kMaxAvgBatch) grouped = false;
+            else {
+                k = nsrc;
+                x.src[nsrc++] = x.e[i].peer;
+            }
+        }
+        x.peer_of[i] = (int8_t)k;
+        grouped = grouped && k != i;
+    }
+    grouped = grouped && nsrc < 2 * x.count;   // some read is shared
+    for (int j = nsrc; j < kMaxAvgBatch; ++j) x.src[j] = nullptr;
+    const bool closed = grouped && nsrc == 2 && x.count == 2;   // the mutual pair
+    if (grouped && !closed) {
 #define DPWA_GROUP_LAUNCH(OPS, P, G)                                                                         \
     do {                                                                                                    \
         if (timing)                                                                                         \
@@ -815,7 +838,7 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
     } while (0)
 #define DPWA_GROUP_G(OPS, P)                                                                                 \
     do {                                                                                                    \
-        switch (x.count) {                                                                                  \
+        switch (nsrc) {                                                                                     \
         case 3: DPWA_GROUP_LAUNCH(OPS, P, 3); break;                                                        \
         case 4: DPWA_GROUP_LAUNCH(OPS, P, 4); break;                                                        \
         case 5: DPWA_GROUP_LAUNCH(OPS, P, 5); break;                                                        \

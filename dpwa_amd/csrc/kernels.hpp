@@ -72,9 +72,12 @@ struct AvgBatch {
     int32_t interleave;
     uint32_t spans;                 // spans per entry (XCD-grouped: equal sizes; the last may be empty)
     uint32_t begin[kMaxAvgBatch];   // first workgroup of each entry (filled by the launcher)
-    // a closed group (resident entries whose peers are all entries of the batch: k_lerp_pair /
-    // k_lerp_group): entry i's peer is entry peer_of[i]'s parameters (filled by the launcher)
+    // a group (k_lerp_pair / k_lerp_group: resident entries of equal size whose reads overlap):
+    // the distinct buffers its entries read, src[0..count) the entries' parameters and then the
+    // peer snapshots of no entry's parameters; entry i's peer is src[peer_of[i]] (filled by the
+    // launcher)
     int8_t peer_of[kMaxAvgBatch];
+    const void *src[kMaxAvgBatch];
     AvgEntry e[kMaxAvgBatch];
 };
 hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hipStream_t s,

@@ -137,11 +137,10 @@ int dpwa_average_many(int32_t dtype, const dpwa_average_desc *descs, int count, 
                       dpwa_stream_t stream, void *start_event, void *stop_event);
 /* The same in the resident form (dpwa_learner_set_resident below): each `param` is read only and the
  * result goes to its snap_payload (required for n > 0) -- 3*n*s bytes per descriptor.  One
- * descriptor runs the single-learner kernel, several the batched one.  Equal-size descriptors that
- * form a closed group (every peer payload is another descriptor's `param`: co-resident learners
- * that picked each other, e.g. a mutual pair) run one fused pass that reads each payload once --
- * 2*n*s per descriptor; equal-size descriptors that otherwise share a read are dispatched so the
- * repeated reads hit L2. */
+ * descriptor runs the single-learner kernel, several the batched one.  Equal-size descriptors whose
+ * reads overlap (a `param` is another descriptor's peer payload, or two share a peer: co-resident
+ * learners that picked each other, e.g. a mutual pair) run one fused pass that reads each distinct
+ * buffer once, up to 8 of them; beyond that the repeated reads are dispatched to hit L2. */
 int dpwa_average_many_resident(int32_t dtype, const dpwa_average_desc *descs, int count, const dpwa_interp *cfg,
                                dpwa_stream_t stream, void *start_event, void *stop_event);
 

@@ -1,10 +1,11 @@
 """Shared reads in the resident batched dispatch (kernels.hip launch_average_batch): co-resident
 resident learners read each other's published slots -- two that average with each other both read
 both slots, and a slot is read by its owner and by every learner that picked it.  A mutual pair
-(two entries, each the other's peer: the N=1 loop) runs as k_lerp_pair, and any closed group
-(every entry's peer is another entry of the dispatch) as k_lerp_group, one workgroup per span
-loading every slot once and storing all the averages; other equal-size entries that share a read
-run k_lerp_batch's XCD-grouped span order (every entry's span s on XCD s % 8, one after the other, so
+(two entries, each the other's peer: the N=1 loop) runs as k_lerp_pair, and any other group of
+equal-size entries whose reads overlap as k_lerp_group (up to eight distinct buffers: the entries'
+parameters and the peers outside the dispatch), one workgroup per span loading every buffer once
+and storing all the averages; sharing batches beyond eight buffers run k_lerp_batch's
+XCD-grouped span order (every entry's span s on XCD s % 8, one after the other, so
 the later reads of a span hit that XCD's L2).  Either way every entry must still be exactly the
 single-learner fused average (factor, clock, lerp into the next slot, ragged tail, ZeroDivision
 no-op) against the CPU oracle, whatever the mix of sharing and non-sharing entries in the
@@ -160,13 +161,48 @@ def test_closed_group_with_zero_division_entries():
             assert res is not None and olerp.bits_equal(got, exp) and c.status == 0
 
 
+OPEN = {
+    "3-outside-peer": [(0, 3), (1, 3), (2, 0)],
+    "4-pairs-and-outside": [(0, 1), (1, 0), (2, 4), (3, 4)],
+    "5-outside-peers": [(0, 5), (1, 6), (2, 5), (3, 0), (4, 6)],
+}
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("name", sorted(OPEN))
+def test_open_groups_vs_oracle(dtype, name):
+    """Entries whose reads overlap while some peer is outside the dispatch (a learner that did not
+    fetch this round) still run as one group: the outside slots are extra sources with no output.
+    Each entry is bit-exact with the C oracle, and the outside learners' slots stay untouched."""
+    picks = OPEN[name]
+    L = 1 + max(max(a, b) for a, b in picks)
+    rng = np.random.default_rng(31 + len(name))
+    n = 8 * 64 * 4 * 2 + 4097
+    ls = [Learner(n, dtype, rng, 1.0 + 0.25 * i, 0.2 + 0.1 * i) for i in range(L)]
+    for got, exp, _, me in _run(ls, picks, dtype):
+        assert olerp.bits_equal(got, exp)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_more_than_eight_sources_keep_the_xcd_grouped_batch(dtype):
+    """Six entries with five distinct outside peers (eleven buffers read, one peer read twice):
+    beyond the group kernel's eight sources, so the batch runs the XCD-grouped span order -- each
+    entry bit-exact with the C oracle."""
+    rng = np.random.default_rng(41)
+    n = 8 * 64 * 4 * 2 + 77
+    ls = [Learner(n, dtype, rng, 1.0 + 0.25 * i, 0.2 + 0.1 * i) for i in range(11)]
+    picks = [(0, 6), (1, 7), (2, 8), (3, 9), (4, 10), (5, 6)]
+    for got, exp, _, me in _run(ls, picks, dtype):
+        assert olerp.bits_equal(got, exp)
+
+
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("picks", [[(0, 1), (2, 1)], [(0, 1), (1, 2)], [(1, 0), (0, 1)]],
                          ids=["same-peer", "chain", "mutual-reversed"])
 def test_two_entries_sharing_a_read(dtype, picks):
     """Two entries that share a read without being a mutual pair (both pick the same peer; one's
-    peer is the other's parameters) take the XCD-grouped batch; the mutual pair given in the other
-    order takes k_lerp_pair: each bit-exact with the C oracle."""
+    peer is the other's parameters) run as a group of three sources (k_lerp_group); the mutual
+    pair given in the other order takes k_lerp_pair: each bit-exact with the C oracle."""
     rng = np.random.default_rng(17)
     n = 8 * 64 * 4 * 5 + 4097
     ls = [Learner(n, dtype, rng, 1.5 + i, 0.3 + 0.2 * i) for i in range(3)]

@@ -11,7 +11,7 @@ timeout -k 10 800 python3 -u -m pytest -x -v --timeout 300 --timeout-method thre
     "tests/test_gpu_configs.py::test_full_size_configs_resident" "tests/test_gpu_configs.py::test_configs0_resnet18_resident_training" \
     > gpurun_out/pytest_$TAG.log 2>&1 || { grep -E "FAILED|Error" gpurun_out/pytest_$TAG.log | head; tail -30 gpurun_out/pytest_$TAG.log; exit 1; }
 tail -1 gpurun_out/pytest_$TAG.log
-for pass in 1 2; do
+for pass in ${PASSES:-1 2}; do
   for f in 1 0; do
     DPWA_PAIR_FUSED=$f timeout -k 10 300 python3 -u tools/group_round.py > gpurun_out/group_${TAG}_f${f}_$pass.log 2>&1 \
       || { tail -20 gpurun_out/group_${TAG}_f${f}_$pass.log; exit 1; }
