@@ -461,28 +461,27 @@ __device__ __forceinline__ void group_span(const AvgBatch &batch)
 #pragma unroll
     for (int j = 0; j < U; ++j)   // all loads first
         v[j] = span_load<V, P::param_load>(span_rsrc<SPAN>(batch.src[j], off, nv * 16), lane_off);
-    dpwa_coef c[U];
+    // per entry: its factor (and workgroup 0's commit), then its average -- one entry's factor
+    // live at a time
+    float fa_[U], fb_[U];
+    bool ok_[U];
 #pragma unroll
     for (int i = 0; i < U; ++i) {
         if (i >= G) break;
         const FusedArgs &fa = batch.e[i].fa;
-        c[i] = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, read_loss(fa.loss_d, fa.loss_f32, fa.loss_h));
-    }
-    if (blk == 0 && threadIdx.x == 0) {
-#pragma unroll
-        for (int i = 0; i < U; ++i)
-            if (i < G) factor_commit(batch.e[i].fa, c[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < U; ++i) {
-        if (i >= G) break;
+        const dpwa_coef c =
+            factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, read_loss(fa.loss_d, fa.loss_f32, fa.loss_h));
+        if (blk == 0 && threadIdx.x == 0) factor_commit(fa, c);
+        fa_[i] = c.a;
+        fb_[i] = c.b;
+        ok_[i] = c.status == DPWA_STATUS_OK;
         const int k = batch.peer_of[i];   // uniform: a select over registers, no indexed access
         V q = v[0];
 #pragma unroll
         for (int j = 1; j < U; ++j)
             if (k == j) q = v[j];
         span_store<V, P::snap_store>(span_rsrc<SPAN>(batch.e[i].snap, off, nv * 16), lane_off,
-                                     c[i].status == DPWA_STATUS_OK ? Ops::lerp(c[i].a, c[i].b, q, v[i]) : v[i]);
+                                     ok_[i] ? Ops::lerp(c.a, c.b, q, v[i]) : v[i]);
     }
     if (blk == 0 && threadIdx.x < n - nv * Ops::PER) {
         const int64_t j = nv * Ops::PER + threadIdx.x;
@@ -497,8 +496,7 @@ __device__ __forceinline__ void group_span(const AvgBatch &batch)
 #pragma unroll
             for (int m = 1; m < U; ++m)
                 if (k == m) q = t[m];
-            reinterpret_cast<S *>(batch.e[i].snap)[j] =
-                c[i].status == DPWA_STATUS_OK ? Ops::lerp_s(c[i].a, c[i].b, q, t[i]) : t[i];
+            reinterpret_cast<S *>(batch.e[i].snap)[j] = ok_[i] ? Ops::lerp_s(fa_[i], fb_[i], q, t[i]) : t[i];
         }
     }
 }
