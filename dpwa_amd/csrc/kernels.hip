@@ -37,6 +37,9 @@
 #ifndef DPWA_FACTOR_LDS
 #define DPWA_FACTOR_LDS 0     // 1: one-wave workgroups hand the factor over through LDS too (A/B builds)
 #endif
+#ifndef DPWA_GROUP_FACTORS_FIRST
+#define DPWA_GROUP_FACTORS_FIRST 0   // 1: group_span evaluates every entry's factor before any store (A/B builds)
+#endif
 
 namespace dpwa {
 
@@ -465,16 +468,34 @@ __device__ __forceinline__ void group_span(const AvgBatch &batch)
     // live at a time
     float fa_[U], fb_[U];
     bool ok_[U];
+    if (DPWA_GROUP_FACTORS_FIRST) {
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            if (i >= G) break;
+            const FusedArgs &fa = batch.e[i].fa;
+            const dpwa_coef c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss,
+                                            read_loss(fa.loss_d, fa.loss_f32, fa.loss_h));
+            if (blk == 0 && threadIdx.x == 0) factor_commit(fa, c);
+            fa_[i] = c.a;
+            fb_[i] = c.b;
+            ok_[i] = c.status == DPWA_STATUS_OK;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < U; ++i) {
         if (i >= G) break;
-        const FusedArgs &fa = batch.e[i].fa;
-        const dpwa_coef c =
-            factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, read_loss(fa.loss_d, fa.loss_f32, fa.loss_h));
-        if (blk == 0 && threadIdx.x == 0) factor_commit(fa, c);
-        fa_[i] = c.a;
-        fb_[i] = c.b;
-        ok_[i] = c.status == DPWA_STATUS_OK;
+        dpwa_coef c;
+        if (DPWA_GROUP_FACTORS_FIRST) {
+            c.a = fa_[i];
+            c.b = fb_[i];
+        } else {
+            const FusedArgs &fa = batch.e[i].fa;
+            c = factor_math(fa.cfg, *fa.clock_in, fa.hdr->clock, fa.hdr->loss, read_loss(fa.loss_d, fa.loss_f32, fa.loss_h));
+            if (blk == 0 && threadIdx.x == 0) factor_commit(fa, c);
+            fa_[i] = c.a;
+            fb_[i] = c.b;
+            ok_[i] = c.status == DPWA_STATUS_OK;
+        }
         const int k = batch.peer_of[i];   // uniform: a select over registers, no indexed access
         V q = v[0];
 #pragma unroll
