@@ -1,16 +1,19 @@
 #!/usr/bin/env python3
 """bench.py -- gossip-round throughput of the MI355X pairwise-averaging hot path.
 
-A *step* is one lock-step gossip round of every learner in the job through the drop-in
-API: ``update_send`` (device clock += 1, snapshot publish, Bernoulli gate, peer choice,
-pull) then ``update_wait`` + ``average`` (device factor/clock, fused in-place lerp).
+A *step* is one gossip round of every learner in the job through the drop-in API:
+``update_send`` (device clock += 1, snapshot publish, Bernoulli gate, peer choice, pull) then
+``update_wait_average`` (device factor/clock, fused lerp that also writes the next snapshot).
 
-Workload (BASELINE.json configs[1]): a synthetic 11,173,962-element fp32 parameter
-vector (ResNet-18 size) per learner, N(0,1) data, constant interpolation 0.5,
-fetch_probability 1.
-  * ``--gpus 1``: two learners co-resident on cuda:0 (the minimal non-degenerate gossip:
-    each averages with the other's snapshot, read in place from HBM); both averages of a
-    round run as one batched dispatch (``DpwaConnection.update_wait_average_many``).
+Workload (BASELINE.json configs[1]): a synthetic 11,173,962-element fp32 parameter vector
+(ResNet-18 size) per learner, N(0,1) data, constant interpolation 0.5, fetch_probability 1,
+the adapter's default write-through form, one learner per GPU at every N.
+  * ``--gpus 1``: one learner whose peer is its own snapshot -- configs[1]'s self-peer: its YAML
+    has a second node entry at the learner's own host:port, which the reference's TxThread dials
+    like any peer (conn.py:246-251), so it averages with what it published at update_send, read
+    in place from HBM.  Beside it: ``value_cold`` (the same loop over learner sets rotated beyond
+    the Infinity Cache) and ``co_resident_pair`` (two resident learners averaging with each other
+    in one dispatch, round 4's line).
   * ``--gpus N``: one learner per GPU, one process per GPU.  Under an external launcher
     (``torch.distributed.run``, WORLD_SIZE set) every process is a rank; without one, this
     script starts ``torch.distributed.run`` itself as a child process (before anything touches
@@ -21,18 +24,20 @@ fetch_probability 1.
     pick the transport of the timed run by the median rate.  Per-GPU work is fixed ->
     "scaling": "weak".  Every rank logs its phases to stderr (``[bench rN +s]``).
 
-``value`` = algorithmic averaged bytes (3 * numel * sizeof(dtype) per completed
-averaging) summed over all learners / the max-over-ranks wall time of the
-K timed steps, from a pass with no instrumentation.  ``roofline`` prices the averaging
-kernel alone, cold, per launch (dispatch begin/end events); ``roofline.in_loop`` times the same
-kernel inside the gossip loop in a separate sampled pass.  ``parity`` (before the timed
-rounds; at N>1 before the trials, so only verified transports are timed) checks every transport bit for bit against the
-oracle, each transport isolated (an error becomes ``false``, not a teardown), with a watchdog
-that prints a partial line and exits non-zero if a phase overruns.  ``cpu_baseline`` times the
-reference's own CPU round restated (oracle/ref_round.py: two learner processes on localhost
-TCP, pickle framing, numpy fp32 lerp -- the path this one replaces) on the box's host cores
-before the GPU is touched, and beside it the averaging arithmetic on the host (C oracle, numpy
-single thread, torch-CPU on every thread) at every north_star size.
+``value`` = algorithmic averaged bytes (3 * numel * sizeof(dtype) per completed averaging,
+SURVEY.md §8d) summed over all learners / the max-over-ranks wall time of the K timed steps,
+from a pass with no instrumentation.  ``roofline`` prices the averaging kernel alone, cold, per
+launch (dispatch begin/end events) on the bytes it moves (4*N*s write-through, PMC-confirmed in
+``traffic``); ``roofline.in_loop`` times the same kernel inside the loop in a separate sampled
+pass.  ``scaling_basis`` carries the raw and weak (fixed training step) rounds/s with the same
+keys at every N.  ``parity`` (before the timed rounds; at N>1 before the trials, so only
+verified transports are timed) checks every transport bit for bit against the oracle, each
+transport isolated (an error becomes ``false``, not a teardown), with a watchdog that prints a
+partial line and exits non-zero if a phase overruns.  ``cpu_baseline`` times the reference's own
+CPU round restated (oracle/ref_round.py: two learner processes on localhost TCP, pickle framing,
+numpy fp32 lerp -- the path this one replaces) on the box's host cores before the GPU is
+touched, and beside it the averaging arithmetic on the host (C oracle, numpy single thread,
+torch-CPU on every thread) at every north_star size.
 """
 import argparse
 import ctypes
@@ -105,13 +110,17 @@ def parse(argv=None):
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel measurement")
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the sweeps over the north_star sizes (cold kernel, and whole rounds at N=1)")
-    ap.add_argument("--publish", choices=["resident", "write-through", "full"], default="resident",
-                    help="how a round publishes and averages in the timed loop: resident (the parameters live in "
-                         "the learner's two snapshot slots: the publish moves nothing, the average reads the "
-                         "published slot and writes the other, 3*N*s), write-through (the averaging kernel also "
-                         "writes the next snapshot, 4*N*s, the publish moves the header only) or full (a 2*N*s "
-                         "snapshot copy every round, then the 3*N*s average)")
-    ap.add_argument("--no-secondary", action="store_true", help="skip the run of the other publish form(s)")
+    ap.add_argument("--publish", choices=["resident", "write-through", "full"], default="write-through",
+                    help="how a round publishes and averages in the timed loop: write-through (the adapter's "
+                         "default and the form the reference's loop order update_send -> step -> update_wait "
+                         "needs: the averaging kernel also writes the next snapshot, 4*N*s, the publish moves "
+                         "the header only), full (a 2*N*s snapshot copy every round, then the 3*N*s average) or, "
+                         "at N>1, resident (the parameters live in the learner's two snapshot slots, 3*N*s; "
+                         "needs update_send -> update_wait -> step)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the run of the other publish form and, at N=1, the co-resident pair")
+    ap.add_argument("--no-value-cold", action="store_true",
+                    help="skip value_cold (the timed loop over rotating learner sets, no Infinity-Cache reuse)")
     ap.add_argument("--no-write-through", action="store_true", help="same as --publish full --no-secondary")
     ap.add_argument("--no-batch", action="store_true",
                     help="N=1: one averaging dispatch per learner instead of one batched dispatch per round")
@@ -321,9 +330,15 @@ class _NoCtxType:
 _NoCtx = _NoCtxType()
 
 
-def write_config(path, names, interp, fetch_probability=1.0, divergence_threshold=0.0):
-    """The reference's YAML node config (dpwa/conn.py:246-262, dpwa/dpwa.py:60-90)."""
-    lines = ["- nodes:"] + ["  - {name: %s, host: 127.0.0.1, port: %d}" % (n, 45000 + i)
+def write_config(path, names, interp, fetch_probability=1.0, divergence_threshold=0.0, self_peer=False,
+                 base_port=45000):
+    """The reference's YAML node config (dpwa/conn.py:246-262, dpwa/dpwa.py:60-90).  self_peer
+    (configs[1], one learner): a second node entry "<name>-self" at the learner's own host:port --
+    the reference's TxThread dials that address and reaches its own RxThread (conn.py:246-251 ->
+    98-110), so the learner's peer is its own published snapshot."""
+    if self_peer:
+        names = [names[0], names[0] + "-self"]
+    lines = ["- nodes:"] + ["  - {name: %s, host: 127.0.0.1, port: %d}" % (n, base_port + (0 if self_peer else i))
                             for i, n in enumerate(names)]
     lines += ["- fetch_probability: %r" % fetch_probability, "- timeout_ms: 2500",
               "- interpolation: %s" % interp, "- divergence_threshold: %r" % divergence_threshold,
@@ -481,7 +496,7 @@ def parity_transports(world, gossip="auto"):
     path that configs[3]/[4] use above 1.5 GiB, through the lock-step fused relay (slots and
     relay buffers fd-imported) and the free-running board."""
     if world == 1:
-        return ["local", "local+res"]
+        return ["self", "local", "local+res"]
     t = []
     if gossip != "async":
         t += ["lockstep/copy", "lockstep/kernel:256", "lockstep/relay:32", "lockstep/relay-avg:32",
@@ -574,6 +589,45 @@ def _parity_lockstep_resident(conns, flats, mine, device, n, T, batch):
             conn.parameters.add_(torch.from_numpy(parity_delta(g, r, n)).to(device))
     torch.cuda.synchronize()
     return rec
+
+
+def parity_self(cfg, device, n=PARITY_N, T=PARITY_T, conns=None):
+    """The N=1 timed form: one learner whose peer is its own snapshot (a self-peer config), T rounds
+    in the reference order -- update_send (reusing the snapshot the last average wrote through),
+    the seeded training delta, update_wait_average with the write-through average -- clock
+    interpolation, fetch_probability PARITY_FP.  Returns the per-round (sha1 of the parameters,
+    clock, peer)."""
+    import hashlib
+    from dpwa_amd import DpwaConnection
+    from dpwa_amd.group import LocalGroup
+    conns = [] if conns is None else conns
+    conn = DpwaConnection("w1", cfg, seed=900, group=LocalGroup())
+    conns.append(conn)
+    flat = torch.from_numpy(parity_init(0, n)).to(device)
+    rec, reuse = [], False
+    for r in range(T):
+        conn.update_send(flat, parity_loss(0, r, False), reuse_snapshot=reuse)
+        flat.add_(torch.from_numpy(parity_delta(0, r, n)).to(device))
+        payload, _ = conn.update_wait_average(flat, parity_loss(0, r, True), write_through=True)
+        reuse = payload is not None
+        rec.append((hashlib.sha1(flat.cpu().numpy().tobytes()).hexdigest(), conn.clock,
+                    payload.peer if payload is not None else ""))
+    torch.cuda.synchronize()
+    return rec
+
+
+def parity_self_expected(n=PARITY_N, T=PARITY_T):
+    """oracle/gossip.py's trajectory of parity_self: nodes [w1, w1-self], w1-self served by w1
+    (pinned to the reference's own self-peer runs, tests/golden/gossip_self.*)."""
+    import hashlib
+    from oracle import gossip as ogossip
+    init = parity_init(0, n)[None]
+    deltas = np.stack([parity_delta(0, r, n)[None] for r in range(T)])
+    exp = ogossip.simulate(["w1"], init, deltas, [[parity_loss(0, r, False)] for r in range(T)],
+                           [[parity_loss(0, r, True)] for r in range(T)], "clock", None, 0.0, PARITY_FP, [900],
+                           nodes=["w1", "w1-self"], serves={"w1-self": 0})
+    return [(hashlib.sha1(exp["params"][r, 0].tobytes()).hexdigest(), float(exp["clocks"][r, 0]),
+             (exp["picks"][r][0][-1] if exp["picks"][r][0] else "")) for r in range(T)]
 
 
 def parity_lockstep_expected(names, n=PARITY_N, T=PARITY_T, resident=False):
@@ -715,6 +769,8 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
     names = ["w%d" % (g + 1) for g in range(max(world, 2))]
     cfg = os.path.join(cfg_dir, "parity.yaml")
     write_config(cfg, names, "clock", PARITY_FP, 0.0)
+    cfg_self = os.path.join(cfg_dir, "parity_self.yaml")
+    write_config(cfg_self, ["w1"], "clock", PARITY_FP, 0.0, self_peer=True, base_port=45900)
     if world > 1 and ctl is None:
         ctl = dist.new_group(backend="gloo")
     result = {}
@@ -735,7 +791,9 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
             with _Env(DPWA_VMM="1") if vmm else _Env():
                 if injected(t, rank, "start"):
                     raise RuntimeError("injected failure (DPWA_BENCH_INJECT, start)")
-                if kind == "local":                   # one GPU: both learners in this process, batched
+                if kind == "self":                    # the N=1 timed form: one learner, its own snapshot
+                    rec = parity_self(cfg_self, device, conns=conns)
+                elif kind == "local":                 # one GPU: both learners in this process, batched
                     from dpwa_amd.group import LocalGroup
                     _, rec = parity_lockstep(names, [(names[0], 0), (names[1], 1)], cfg, LocalGroup(), None, device,
                                              conns=conns, batch=True, resident=res)
@@ -759,7 +817,9 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
                 except Exception as e:   # noqa: BLE001
                     progress("parity %s: close failed: %s" % (t, e))
         want = expected[res] if expected is not None else None
-        if kind == "local":
+        if kind == "self":
+            ok = err is None and rec == parity_self_expected()
+        elif kind == "local":
             ok = err is None and rec == want
         elif kind == "lockstep":
             got = [None] * world
@@ -920,47 +980,30 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
             "mutual_pair": pair}
 
 
-def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None, publish="resident", min_s=0.25):
-    """Whole gossip rounds (two co-resident learners, `publish` form -- resident or write-through --,
-    constant 0.5, fetch_probability 1, both averages in one dispatch) at every north_star size in
-    its config's dtype: the averaged GB/s and rounds/s the north star asks for at 11M/100M/1B/7B
-    on one GPU.  Each size runs at least `steps` rounds and at least `min_s` seconds (sized from
-    one probe round), so the 11.17M row is a longer window than the driver's 20-step timed run."""
+def round_sweep(device, cfg_dir, steps=20, warmup=3, rows=None, publish="write-through", min_s=0.25):
+    """Whole gossip rounds of the N=1 line's form at every north_star size in its config's dtype:
+    one learner whose peer is its own snapshot (configs[1]'s self-peer), constant 0.5,
+    fetch_probability 1, `publish` write-through (the snapshot the average writes through is the
+    next publish) or full (every publish copies the 2*N*s snapshot) -- the averaged GB/s and
+    rounds/s the north star asks for at 11M/100M/1B/7B on one GPU, on the basis of the N>1 sweep
+    (one learner per GPU).  Each size runs at least `steps` rounds and at least `min_s` seconds
+    (sized from one probe round)."""
     from dpwa_amd import DpwaConnection
     from dpwa_amd.group import LocalGroup
     rows = [] if rows is None else rows
     cfg = os.path.join(cfg_dir, "sweep.yaml")
-    write_config(cfg, ["w1", "w2"], "constant")
+    write_config(cfg, ["w1"], "constant", self_peer=True, base_port=45800)
+    wt = publish == "write-through"
     for numel, dt in SWEEP:
         dtype = torch.float32 if dt == "f32" else torch.bfloat16
         esize = 4 if dt == "f32" else 2
-        flats = []
-        for g in range(2):
-            t = torch.empty(numel, dtype=dtype, device=device)
-            t.normal_(generator=torch.Generator(device=device).manual_seed(g))
-            flats.append(t)
-        group = LocalGroup()
-        conns = [DpwaConnection(nm, cfg, seed=1000 + g, group=group) for g, nm in enumerate(("w1", "w2"))]
-        resident = publish == "resident"
-        if resident:
-            for c, f in zip(conns, flats):
-                c.make_resident(f)
-            del flats
-            flats = [c.parameters for c in conns]
+        flat = torch.empty(numel, dtype=dtype, device=device)
+        flat.normal_(generator=torch.Generator(device=device).manual_seed(0))
+        conn = DpwaConnection("w1", cfg, seed=1000, group=LocalGroup())
 
         def step():
-            for c, f in zip(conns, flats):
-                c.update_send(f, 1.0, reuse_snapshot=True)
-            if batch:
-                res = DpwaConnection.update_wait_average_many(conns, flats, [1.0, 1.0], write_through=True)
-                n = sum(p is not None for p, _ in res)
-            else:
-                n = 0
-                for c, f in zip(conns, flats):
-                    n += c.update_wait_average(f, 1.0, write_through=True)[0] is not None
-            if resident:
-                flats[:] = [c.parameters for c in conns]
-            return n
+            conn.update_send(flat, 1.0, reuse_snapshot=wt)
+            return conn.update_wait_average(flat, 1.0, write_through=wt)[0] is not None
 
         for _ in range(warmup):
             step()
@@ -974,11 +1017,10 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3, batch=True, rows=None, publ
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         rows.append({"numel": numel, "dtype": dt, "value": round(averaged * 3 * numel * esize / el / 1e9, 1),
-                     "ms_per_step": round(1e3 * el / n_steps, 4), "gossip_rounds_per_s": round(2 * n_steps / el, 1),
-                     "steps": n_steps, "seconds": round(el, 3), "batched": batch, "publish": publish})
-        for c in conns:
-            c.close()
-        del flats, conns
+                     "ms_per_step": round(1e3 * el / n_steps, 4), "gossip_rounds_per_s": round(n_steps / el, 1),
+                     "steps": n_steps, "seconds": round(el, 3), "learners": 1, "peer": "self", "publish": publish})
+        conn.close()
+        del flat, conn
         torch.cuda.empty_cache()
     return rows
 
@@ -1078,6 +1120,107 @@ def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, wat
     return rows
 
 
+def cold_rounds(device, cfg_dir, numel, dtype, steps, warmup=2, publish="write-through", min_bytes=1.2e9):
+    """SURVEY §8(d) cache honesty for the whole round: the timed loop of the N=1 line over K
+    self-peer learners taken in turn (round i runs learner i mod K), K chosen so more than
+    `min_bytes` of other learners' buffers are touched between two rounds of one learner -- the
+    256 MiB Infinity Cache holds nothing a round re-reads.  Same calls as the timed loop
+    (update_send with the write-through snapshot, update_wait_average); value = 3*N*s per
+    completed averaging over the wall time."""
+    from dpwa_amd import DpwaConnection
+    from dpwa_amd.group import LocalGroup
+    esize = 4 if dtype == torch.float32 else 2
+    per = 3 * numel * esize         # what one round touches: parameters, published slot, next slot
+    K = 1 if per >= min_bytes else max(2, int(np.ceil(min_bytes / per)) + 1)
+    wt = publish == "write-through"
+    conns, flats = [], []
+    for k in range(K):
+        cfg = os.path.join(cfg_dir, "cold_%d.yaml" % k)
+        write_config(cfg, ["c%d" % k], "constant", self_peer=True, base_port=45600 + k)
+        conns.append(DpwaConnection("c%d" % k, cfg, seed=2000 + k, group=LocalGroup()))
+        f = torch.empty(numel, dtype=dtype, device=device)
+        f.normal_(generator=torch.Generator(device=device).manual_seed(k))
+        flats.append(f)
+
+    def step(i):
+        c, f = conns[i % K], flats[i % K]
+        c.update_send(f, 1.0, reuse_snapshot=wt)
+        return c.update_wait_average(f, 1.0, write_through=wt)[0] is not None
+
+    for i in range(warmup * K):
+        step(i)
+    n = max(steps, 4 * K)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    averaged = sum(step(i) for i in range(n))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    for c in conns:
+        c.close()
+    del conns, flats
+    torch.cuda.empty_cache()
+    return {"value": round(averaged * 3 * numel * esize / el / 1e9, 2), "ms_per_step": round(1e3 * el / n, 4),
+            "gossip_rounds_per_s": round(n / el, 1), "steps": n, "learner_sets": K,
+            "bytes_between_reuses": (K - 1) * per, "publish": publish,
+            "basis": "the timed loop's rounds over %d self-peer learners in turn: %.2f GB of other learners' "
+                     "buffers between two rounds of one learner (Infinity Cache 256 MiB), so every round reads "
+                     "HBM" % (K, (K - 1) * per / 1e9)}
+
+
+def co_resident_pair(device, cfg_dir, numel, dtype, steps, warmup=5, cold=True):
+    """Round 4's N=1 line, kept as an extra: two resident learners co-resident on one GPU that
+    average with each other (each the other's only peer), both averages in one dispatch
+    (k_lerp_pair: one workgroup per span loads both published slots once and stores both
+    averages).  Two averagings (2 x 3*N*s of the metric's unit) move 4*N*s through HBM, so the
+    metric-unit rate exceeds what HBM moves; `hbm` prices the dispatch on the bytes it moves."""
+    from dpwa_amd import DpwaConnection
+    from dpwa_amd.group import LocalGroup
+    esize = 4 if dtype == torch.float32 else 2
+    cfg = os.path.join(cfg_dir, "pair.yaml")
+    write_config(cfg, ["w1", "w2"], "constant", base_port=45500)
+    group = LocalGroup()
+    conns = []
+    for g, nm in enumerate(("w1", "w2")):
+        c = DpwaConnection(nm, cfg, seed=1000 + g, group=group)
+        f = torch.empty(numel, dtype=dtype, device=device)
+        f.normal_(generator=torch.Generator(device=device).manual_seed(g))
+        c.make_resident(f)
+        del f
+        conns.append(c)
+
+    def step():
+        for c in conns:
+            c.update_send(c.parameters, 1.0)
+        res = DpwaConnection.update_wait_average_many(conns, [c.parameters for c in conns], [1.0, 1.0])
+        return sum(p is not None for p, _ in res)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    averaged = sum(step() for _ in range(steps))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    for c in conns:
+        c.close()
+    del conns
+    torch.cuda.empty_cache()
+    out = {"value": round(averaged * 3 * numel * esize / el / 1e9, 2), "ms_per_step": round(1e3 * el / steps, 4),
+           "gossip_rounds_per_s": round(averaged / el, 1), "steps": steps, "learners": 2,
+           "kernel": "dpwa::k_lerp_pair (two resident learners averaging with each other in one dispatch)",
+           "value_note": "3*N*s per averaging, two averagings per round; they share their two snapshot reads, "
+                         "so this is not an HBM rate (it can exceed the HBM peak)"}
+    if cold:
+        c = cold_kernel(numel, dtype, device, False, learners=2, resident=True, pair=True)
+        hb = 4 * numel * esize
+        out["hbm"] = {"bytes_per_launch": hb, "avg_launch_us": round(c["avg_launch_us"], 2),
+                      "achieved": round(hb / (c["avg_launch_us"] * 1e-6) / 1e9, 1),
+                      "frac": round(hb / (c["avg_launch_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                      "basis": "cold (rotating buffers), the 4*N*s the dispatch moves"}
+        out["algorithmic_gbs"] = round(6 * numel * esize / (c["avg_launch_us"] * 1e-6) / 1e9, 1)
+    return out
+
+
 def size_sweep(device, rows=None):
     """The averaging kernel, cold, per launch, at every north_star size (11.17M/100M fp32,
     1B/7B bf16), in every publish form: plain (3*N*s bytes per launch), write-through
@@ -1107,6 +1250,36 @@ def size_sweep(device, rows=None):
     return rows
 
 
+SCALING_DEFINITION = ("one learner per GPU at every N (N=1: its peer is its own snapshot, configs[1]; N>1: one "
+                      "rank per GPU, peers over xGMI), the same publish form at every N.  raw = aggregate "
+                      "gossip rounds/s of the bandwidth loop (update_send -> update_wait, no training step): "
+                      "HBM-bound at N=1, xGMI-bound at N>1, so its N-ratio cannot reach 6x (DESIGN §6).  "
+                      "weak = aggregate rounds/s with a fixed synthetic training step per learner (bf16 GEMMs "
+                      "+ a write of every parameter) between update_send and update_wait, the reference's loop "
+                      "(main.py:130-145, SURVEY §7/§8d C4): per-learner work is fixed, so its N-ratio is the "
+                      "weak-scaling figure")
+
+
+def scaling_basis(world, learners_per_gpu, publish, rounds, elapsed, value, overlap):
+    """The line's `scaling_basis`: the same keys at every N (tests/test_bench_host.py checks it), so
+    the driver's 1/2/4/8-GPU lines compare like with like."""
+    learners = world * learners_per_gpu
+    raw = rounds / elapsed if elapsed else None
+    weak = {"gossip_rounds_per_s": None, "gossip_rounds_per_s_per_learner": None, "ms_per_step": None,
+            "compute_only_ms_per_step": None, "gossip_overhead_frac": None}
+    if overlap is not None:
+        weak.update(gossip_rounds_per_s=overlap["gossip_rounds_per_s"],
+                    gossip_rounds_per_s_per_learner=round(overlap["gossip_rounds_per_s"] / learners, 1),
+                    ms_per_step=overlap["ms_per_step"], compute_only_ms_per_step=overlap["compute_only_ms_per_step"],
+                    gossip_overhead_frac=overlap["gossip_overhead_frac"])
+    return {"definition": SCALING_DEFINITION, "n_gpus": world, "learners_per_gpu": learners_per_gpu,
+            "learners": learners, "publish": publish,
+            "raw": {"gossip_rounds_per_s": round(raw, 1) if raw else None,
+                    "gossip_rounds_per_s_per_learner": round(raw / learners, 1) if raw else None,
+                    "value": value, "loop": "update_send -> update_wait (no training step)"},
+            "weak": dict(weak, loop="update_send -> step (GEMMs, then a write of every parameter) -> update_wait")}
+
+
 # ---------------------------------------------------------------- the run
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
@@ -1131,6 +1304,10 @@ def main(argv=None):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    if world == 1 and args.publish == "resident":
+        raise SystemExit("--publish resident at N=1: the line's learner averages with its own snapshot "
+                         "(configs[1]'s self-peer), which resident parameters would read twice from one slot; "
+                         "the resident co-resident pair is the line's `co_resident_pair` block")
     wd = Watchdog(args, world, rank)
     # the CPU baseline first, before anything touches the GPU (its learners are child processes)
     wd.enter("start: world %d, numel %d %s" % (world, args.numel, args.dtype), 600.0)
@@ -1164,9 +1341,11 @@ def main(argv=None):
     tmp = tempfile.mkdtemp(prefix="dpwa_bench_")
     cfg = os.path.join(tmp, "bench.yaml")
     if world == 1:
-        names = ["w1", "w2"]
-        write_config(cfg, names, args.interpolation, args.fetch_probability, args.divergence_threshold)
-        mine = [(names[0], 0), (names[1], 1)]
+        # configs[1]: one learner whose peer is its own snapshot (a node entry at its own address)
+        names = ["w1"]
+        write_config(cfg, names, args.interpolation, args.fetch_probability, args.divergence_threshold,
+                     self_peer=True)
+        mine = [(names[0], 0)]
     else:
         names = ["w%d" % (r + 1) for r in range(world)]
         write_config(cfg, names, args.interpolation, args.fetch_probability, args.divergence_threshold)
@@ -1477,7 +1656,7 @@ def main(argv=None):
             learners[:] = async_learners
             run(2, 2, False)
             for m in [m for m in modes if not m.startswith("relay")]:
-                for wt in ((False, True) if wt_lockstep else (False,)):
+                for wt in ((True,) if wt_lockstep else (False,)):    # the line's publish form only
                     key = "async/" + m + ("+wt" if wt else res_sfx)
                     if verified(key):
                         cands.append((key, False, m, wt))
@@ -1617,7 +1796,7 @@ def main(argv=None):
             "gossip_overhead_frac": round(t_both / t_compute - 1.0, 4),
             "rounds_per_s_per_learner": round(o_steps / t_both, 1),
             "gossip_rounds_per_s": round(o_steps * len(wt_set) * world / t_both, 1),   # all learners, all ranks
-            "transport": o_mode if world > 1 else "in-place HBM read (co-resident peer)",
+            "transport": o_mode if world > 1 else "in-place HBM read of its own published snapshot (self-peer)",
             "publish": "write-through" if o_wt else "full",
             "loop_order": "update_send -> step (GEMMs, then a write of every parameter) -> update_wait",
             "note": "the reference's loop order (main.py:130-145; SURVEY §8d C4 weak scaling) with a synthetic "
@@ -1635,131 +1814,80 @@ def main(argv=None):
         for conn, _ in wt_set:
             conn.close()
         wt_set = None
+    value_cold = None
+    if world == 1 and not args.no_value_cold:
+        # SURVEY §8(d) cache honesty for the whole round: the same loop over learner sets rotated
+        # beyond the Infinity Cache
+        wd.enter("value_cold", 600.0)
+        value_cold = cold_rounds(device, tmp, args.numel, dtype, args.steps, publish=form)
+    pair = None
+    if world == 1 and not args.no_secondary:
+        wd.enter("co-resident pair", 600.0)
+        pair = co_resident_pair(device, tmp, args.numel, dtype, args.steps, warmup=args.warmup, cold=not args.no_cold)
 
     if parity is not None:
         parity["workload"] = ("%d-element fp32 vector per learner, %d lock-step rounds (clock interpolation, "
                               "fetch_probability %g, seeded training-step deltas, write-through and split rounds "
-                              "mixed; at N=1 both learners' averages batched), %d free-running rounds over the "
+                              "mixed; 'self': the N=1 line's form, one learner whose peer is its own snapshot, "
+                              "write-through in the reference order; 'local': two learners, averages batched), "
+                              "%d free-running rounds over the "
                               "gossip board; every learner's parameters, clocks and peers compared bit for bit with "
                               "oracle/gossip.py (lock-step) and oracle/async_check.py (per version read); '+vmm': "
                               "snapshot slots (and relay buffers) fd-shared hipMemCreate chunks, the configs[3]/[4] "
                               "path" % (PARITY_N, PARITY_T, PARITY_FP, PARITY_ASYNC_T))
-    used = ("local+res" if resident_main else "local") if world == 1 else parity_key(pull)
+    used = "self" if world == 1 else parity_key(pull)
 
     unit_bytes = 3 * args.numel * esize
     per_launch = len(learners) if batched else 1
     wt_kernel = wt_main and not resident_main      # resident: the kernel moves the averaging's 3*N*s only
-    # the N=1 resident loop's two learners average with each other: one mutual pair per dispatch,
-    # whose two averages read the same two snapshots (k_lerp_pair: both read once per span): 4*N*s per launch
-    pair_kernel = resident_main and per_launch == 2
-    kbytes = (4 * args.numel * esize if pair_kernel else
-              (4 if wt_kernel else 3) * args.numel * esize * per_launch)   # the timed loop's averaging dispatch
+    # the bytes the timed loop's averaging dispatch moves through HBM (PMC-confirmed, `traffic`):
+    # write-through 4*N*s (read parameters, read the peer snapshot, write parameters, write the next
+    # snapshot), full / resident 3*N*s
+    kbytes = (4 if wt_kernel else 3) * args.numel * esize * per_launch
     # the same kernel alone, cold (rotating buffers, per-launch dispatch events): the roofline's basis
     cold = None
-    cold_plain = None
-    cold_ref = {}           # the reference loop's (write-through) kernels and the single resident one, cold
+    forms_cold = {}         # every single-learner form at the workload size, cold
     if not args.no_cold:
         wd.enter("cold kernel", 300.0)
-        cold = cold_kernel(args.numel, dtype, device, wt_kernel, learners=per_launch, resident=resident_main,
-                           pair=pair_kernel)
-        if wt_kernel:   # BASELINE's target kernel: the same dispatch without the snapshot write
-            cold_plain = cold_kernel(args.numel, dtype, device, False, learners=per_launch)
-        for key, wt_, n_, res_ in (("write_through_x%d" % per_launch, True, per_launch, False),
-                                   ("write_through_single", True, 1, False), ("resident_single", False, 1, True)):
-            if key == "write_through_single" and per_launch == 1:
-                continue
-            same = (n_ == per_launch and res_ == resident_main and wt_ == wt_kernel and not pair_kernel)
-            c = cold if same else cold_kernel(args.numel, dtype, device, wt_, learners=n_, resident=res_)
-            b = n_ * (4 if wt_ else 3) * args.numel * esize
-            cold_ref[key] = {"avg_launch_us": round(c["avg_launch_us"], 2),
-                             "frac": round(b / (c["avg_launch_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
-            tb, _ = pmc_traffic(None, "write-through" if wt_ else "resident", n_, args.numel, args.dtype, "cold")
+        cold = cold_kernel(args.numel, dtype, device, wt_kernel, learners=per_launch, resident=resident_main)
+        for key, wt_, res_ in (("write_through", True, False), ("full", False, False), ("resident", False, True)):
+            same = per_launch == 1 and res_ == resident_main and wt_ == wt_kernel
+            c = cold if same else cold_kernel(args.numel, dtype, device, wt_, learners=1, resident=res_)
+            b = (4 if wt_ else 3) * args.numel * esize
+            forms_cold[key] = {"bytes_per_launch": b, "avg_launch_us": round(c["avg_launch_us"], 2),
+                               "frac": round(b / (c["avg_launch_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+            tb, _ = pmc_traffic(None, "write-through" if wt_ else "resident" if res_ else "full", 1, args.numel,
+                                args.dtype, "cold")
             if tb:
-                cold_ref[key]["traffic_x"] = round(tb / b, 4)     # PMC HBM bytes / algorithmic bytes
+                forms_cold[key]["traffic_x"] = round(tb / b, 4)     # PMC HBM bytes / moved bytes
     wd.enter("report", 120.0)
     out = None
     if rank == 0:
         value = averaged * unit_bytes / elapsed / 1e9
         lerp_us = float(np.nanmean(lerp_ms) * 1e3)
-        # each timed dispatch moved (averages in it) x 4*N*s (3*N*s): the aggregate rate
-        # algorithmic bytes: SURVEY 8d's per-unit figure (3*N*s per averaging; 4*N*s for the write-through
-        # kernel, which also writes the next snapshot) times the averagings a launch completes.  The mutual
-        # pair moves fewer HBM bytes than that (kbytes = 4*N*s for its two averagings): the `hbm` block.
-        alg_bytes = 3 * args.numel * esize * per_launch if pair_kernel else kbytes
-        k1 = alg_bytes / per_launch
+        k1 = kbytes / per_launch
         live_gbs = float(np.nansum(lerp_navg * k1) / np.nansum(lerp_ms * 1e-3) / 1e9) if np.isfinite(lerp_us) \
             else float("nan")
         k_us = cold["avg_launch_us"] if cold else lerp_us
-        achieved = alg_bytes / (k_us * 1e-6) / 1e9
-        hbm_achieved = kbytes / (k_us * 1e-6) / 1e9
+        achieved = kbytes / (k_us * 1e-6) / 1e9
         variant = form
-        traffic, traffic_src = pmc_traffic(args.traffic, "resident-pair" if pair_kernel else variant, per_launch,
-                                           args.numel, args.dtype, "cold" if cold else "in-loop")
+        traffic, traffic_src = pmc_traffic(args.traffic, variant, per_launch, args.numel, args.dtype,
+                                           "cold" if cold else "in-loop")
+        ops = "Ops%s" % args.dtype.upper()
         if resident_main:
-            kname = ("dpwa::k_lerp_pair<Ops%s, 8> (the two resident learners average with each other, a mutual "
-                     "pair: one workgroup per span reads both published slots once and stores both averages, fused "
-                     "device factor + lerp, into the two next slots)" % args.dtype.upper()
-                     if pair_kernel else
-                     "dpwa::k_lerp_batch<Ops%s, true, 8, true> (%d resident learners' fused device factor + lerp "
-                     "in one dispatch: each reads its published slot and writes the other)" % (args.dtype.upper(),
-                                                                                              per_launch)
-                     if per_launch > 1 else
-                     "dpwa::k_lerp<Ops%s, COEF_FUSED, true, 64, 8, true> (resident: fused device factor + lerp "
-                     "from the published slot into the other)" % args.dtype.upper())
+            kname = ("dpwa::k_lerp<%s, COEF_FUSED, true, 64, 8, true> (resident: fused device factor + lerp from "
+                     "the published slot into the other)" % ops)
         else:
-            kname = ("dpwa::k_lerp_batch<Ops%s, %s> (%d learners' fused device factor + lerp%s in one dispatch)"
-                     % (args.dtype.upper(), "true" if wt_main else "false", per_launch,
-                        " + write-through of the next snapshot" if wt_main else "") if per_launch > 1 else
-                     "dpwa::k_lerp<Ops%s, COEF_FUSED, %s> (fused device factor + lerp%s)"
-                     % (args.dtype.upper(), "true" if wt_main else "false",
-                        " + write-through of the next snapshot" if wt_main else ""))
+            kname = ("dpwa::k_lerp<%s, COEF_FUSED, %s> (fused device factor + lerp%s)"
+                     % (ops, "true" if wt_main else "false", " + write-through of the next snapshot" if wt_main else ""))
+        sb = scaling_basis(world, len(mine), form, rounds, elapsed, round(value, 2), overlap)
         out = base_line(args, world)
         out.update({
             "value": round(value, 2),
             "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "dtype": "f32" if dtype == torch.float32 else "bf16",
-            "config": {
-                "workload": ("%ssynthetic %d-element %s vector per learner%s, %s interpolation, "
-                             "fetch_probability %g, divergence_threshold %g, %s loss, %s gossip rounds, %s publish"
-                             % ("configs[1]: " if args.numel == RESNET18_NUMEL else "", args.numel, args.dtype,
-                                " (ResNet-18 size)" if args.numel == RESNET18_NUMEL else "", args.interpolation,
-                                args.fetch_probability, args.divergence_threshold, args.loss_schedule,
-                                "free-running" if sel_async else "lock-step", variant)),
-                "learners": int(rounds / args.steps),
-                "learners_per_gpu": len(mine),
-                "numel": args.numel,
-                "publish": variant,
-                "publish_note": ("resident: each learner's parameters live in its two snapshot slots; the average "
-                                 "reads the published slot and writes the other (3*N*s), the publish moves nothing. "
-                                 "This value assumes the loop order update_send -> update_wait -> step (nothing "
-                                 "writes the parameters between update_send and update_wait; these synthetic rounds "
-                                 "have no step, and update_wait raises if the window was written). The reference's "
-                                 "own order update_send -> step -> update_wait needs the write-through form: "
-                                 "reference_loop (last key) and secondary_publish; --publish write-through times "
-                                 "it as the main run"
-                                 if resident_main else
-                                 "write-through: the average also writes the next snapshot (4*N*s)" if wt_main else
-                                 "full: every publish copies the 2*N*s snapshot"),
-                "averaging_dispatch": ("one batched dispatch per round for the %d co-resident learners" % per_launch
-                                       if per_launch > 1 else "one dispatch per learner per round"),
-                "transport": "in-place HBM read (co-resident peer)" if world == 1 else
-                             "peer slot mapped into this process (hipIpc handle, or fds of hipMemCreate chunks from "
-                             "1.5 GiB up) pulled over xGMI on a side stream (%s, %s rounds)"
-                             % (sel_mode, "free-running" if sel_async else "lock-step"),
-                "parallelism": "gossip x%d" % int(rounds / args.steps),
-                "streams": args.streams,
-            },
-            "warmup_rounds": {"steps": args.warmup, "time_based_extra": warm_extra[0], "warmup_s": args.warmup_s,
-                              "note": "untimed rounds before the timed steps: W, then more up to about warmup_s "
-                                      "seconds in all, so the timed steps run at steady-state clocks"},
-            "value_basis": "the timed pass carries no instrumentation (no kernel timing, no events); value = 3*N*s "
-                           "per completed averaging (SURVEY 8d's unit) over the wall time" +
-                           ("; the two learners average with each other and share their two snapshot reads "
-                            "(roofline.hbm.bytes_per_launch = 4*N*s for both averagings), so value is not an HBM rate "
-                            "and can exceed the HBM peak" if pair_kernel else ""),
-            "gossip_rounds_per_s": round(rounds / elapsed, 1),
-            "gossip_rounds_per_s_per_learner": round(rounds / elapsed / (rounds / args.steps), 1),
-            "averagings": int(averaged),
+            "value_cold": value_cold,
+            "scaling_basis": sb,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -1768,32 +1896,21 @@ def main(argv=None):
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel": kname,
-                "learners_per_launch": per_launch,
-                "bytes_per_launch": alg_bytes,
-                "hbm": {"bytes_per_launch": kbytes, "achieved": round(hbm_achieved, 1),
-                        "frac": round(hbm_achieved / HBM_PEAK_GBS, 4),
-                        "traffic_x": round(traffic / kbytes, 4) if traffic else None,
-                        "note": "the bytes the launch must move through HBM: equal to bytes_per_launch except for "
-                                "the mutual pair, whose two averagings share their two snapshot reads (4*N*s)"},
-                "bytes_note": ("6*N*s: two averagings of 3*N*s (SURVEY 8d's unit: read the parameters, read the peer "
-                               "snapshot, write the next slot) in one dispatch. The two resident learners average "
-                               "with each other, so both averagings read the same two published slots; one "
-                               "workgroup per span loads each once and computes both. The launch therefore moves "
-                               "only 4*N*s through HBM (`hbm`, confirmed by `traffic`), and `achieved` / `frac` on "
-                               "the algorithmic 6*N*s can exceed the HBM peak"
-                               if pair_kernel else
-                               ("%d x " % per_launch if per_launch > 1 else "") +
-                               ("3*N*s: read the parameters (the published slot they are in), read the peer "
-                                "snapshot, write the parameters into the learner's other slot (the next publish "
-                                "then moves nothing)" if resident_main else
-                                "4*N*s: read parameters, read peer snapshot, write parameters, write the next "
-                                "snapshot (which the publish then does not copy)" if wt_main else
-                                "3*N*s: read parameters, read peer snapshot, write parameters")),
+                "bytes_per_launch": kbytes,
+                "bytes_note": ("4*N*s moved per averaging: read parameters, read the peer snapshot, write "
+                               "parameters, write the next snapshot (the publish then copies nothing)" if wt_kernel else
+                               "3*N*s moved per averaging: read the parameters, read the peer snapshot, write the "
+                               "result"),
+                "metric_bytes_per_averaging": unit_bytes,
                 "avg_launch_us": round(k_us, 2),
-                "basis": ("cold: the kernel alone over rotating buffers (> 1.2 GB between reuses, no "
-                          "Infinity-Cache hits), every launch timed by its own dispatch begin/end events "
-                          "(hipExtLaunchKernelGGL), mean over %d launches" % cold["launches"]) if cold else
+                "basis": ("cold: the kernel alone over rotating buffers (> 1.2 GB between reuses), every launch "
+                          "timed by its dispatch begin/end events, mean of %d" % cold["launches"]) if cold else
                          "in-loop (--no-cold)",
+                "traffic_source": traffic_src,
+                "traffic_x": round(traffic / kbytes, 4) if traffic else None,
+                "in_loop_frac": round(live_gbs / HBM_PEAK_GBS, 4) if np.isfinite(live_gbs) else None,
+                "in_loop_avg_launch_us": round(lerp_us, 2) if np.isfinite(lerp_us) else None,
+                "learners_per_launch": per_launch,
                 "cold": ({k: (round(v, 2) if isinstance(v, float) else v) for k, v in cold.items()}
                          if cold else None),
                 "in_loop": {
@@ -1801,7 +1918,6 @@ def main(argv=None):
                     "frac": round(live_gbs / HBM_PEAK_GBS, 4),
                     "avg_launch_us": round(lerp_us, 2),
                     "launches_timed": int(np.isfinite(lerp_ms).sum()),
-                    "averages_per_launch": round(float(np.nanmean(lerp_navg)), 3),
                     "timing": ("kernel dispatch begin/end events (hipExtLaunchKernelGGL) on the averaging "
                                "kernel's own stream" if args.timing != "bracket" else
                                "HIP event pair recorded around the launch on its stream")
@@ -1810,39 +1926,59 @@ def main(argv=None):
                     "sampled_pass_ms_per_step": round(1e3 * s_el / s_steps, 4),
                     "event_bracket_us": (round(float(np.nanmean(bracket_ms) * 1e3), 2)
                                          if args.timing != "dispatch" else None),
-                    "note": ("inside the gossip round the peer snapshot was written just before the average and "
-                             "is partly Infinity-Cache resident, so this live figure is warmer than the basis"
+                    "note": ("inside the loop the learner re-reads what its last average wrote (134 MB at "
+                             "configs[1], inside the 256 MiB Infinity Cache), so this live figure is warmer "
+                             "than the cold basis; value_cold is the whole loop without that reuse"
                              if world == 1 else
                              "the averaging kernel of the timed rounds: it reads the staged peer snapshot (copy / "
                              "kernel / relay pulls) or, under relay-avg, the peer's stripes over xGMI itself, so "
                              "there it is link-bound and its bytes are not all HBM bytes"),
                 },
-                "traffic_source": traffic_src,
-                "vs_measured_ceiling": {"gbs": HBM_MEASURED_GBS, "frac": round(hbm_achieved / HBM_MEASURED_GBS, 4),
+                "forms_cold": forms_cold or None,
+                "vs_measured_ceiling": {"gbs": HBM_MEASURED_GBS, "frac": round(achieved / HBM_MEASURED_GBS, 4),
                                         "source": "MI355X_MICROARCH.md: 6.29 TB/s measured for a float4 copy "
-                                                  "(79 % of the 8 TB/s spec); peak above stays the spec; "
-                                                  "HBM bytes (the hbm block)"},
+                                                  "(79 % of the 8 TB/s spec); peak above stays the spec"},
             },
+            "config": {
+                "workload": ("%ssynthetic %d-element %s vector, %s, %s interpolation, fetch_probability %g, "
+                             "divergence_threshold %g, %s loss, %s publish"
+                             % ("configs[1]: " if args.numel == RESNET18_NUMEL and world == 1 else "", args.numel,
+                                args.dtype, "one learner, its peer its own snapshot (self-peer)" if world == 1 else
+                                "one learner per GPU, %s rounds" % ("free-running" if sel_async else "lock-step"),
+                                args.interpolation, args.fetch_probability, args.divergence_threshold,
+                                args.loss_schedule, variant)),
+                "learners": int(rounds / args.steps),
+                "learners_per_gpu": len(mine),
+                "numel": args.numel,
+                "publish": variant,
+                "loop_order": ("update_send -> update_wait -> step" if resident_main else
+                               "update_send -> step -> update_wait (README.md:18-29, main.py:130-145); the timed "
+                               "rounds have no step, scaling_basis.weak has one"),
+                "peer": ("its own published snapshot: a second YAML node entry at the learner's own host:port, "
+                         "which the reference's TxThread dials like any peer (conn.py:246-251)" if world == 1 else
+                         "a random other rank's snapshot (TxThread's choice), pulled over xGMI (%s)" % sel_mode),
+                "value_cold": value_cold["value"] if value_cold else None,
+                "frac_moved_bytes_cold": round(achieved / HBM_PEAK_GBS, 4),
+                "scaling_raw_rounds_per_s": sb["raw"]["gossip_rounds_per_s"],
+                "scaling_weak_rounds_per_s": sb["weak"]["gossip_rounds_per_s"],
+                "parallelism": "gossip x%d" % int(rounds / args.steps),
+                "streams": args.streams,
+            },
+            "value_basis": "the timed pass carries no instrumentation (no kernel timing, no events); value = 3*N*s "
+                           "per completed averaging (SURVEY 8d's unit) over the wall time",
+            "gossip_rounds_per_s": round(rounds / elapsed, 1),
+            "gossip_rounds_per_s_per_learner": round(rounds / elapsed / (rounds / args.steps), 1),
+            "averagings": int(averaged),
+            "warmup_rounds": {"steps": args.warmup, "time_based_extra": warm_extra[0], "warmup_s": args.warmup_s,
+                              "note": "untimed rounds before the timed steps: W, then more up to about warmup_s "
+                                      "seconds in all, so the timed steps run at steady-state clocks"},
         })
-        if cold_plain is not None:
-            pb = 3 * args.numel * esize * per_launch
-            out["roofline"]["plain_average"] = {
-                "kernel": kname.replace(", true>", ", false>").replace(" + write-through of the next snapshot", ""),
-                "bytes_per_launch": pb,
-                "avg_launch_us": round(cold_plain["avg_launch_us"], 2),
-                "achieved": round(pb / (cold_plain["avg_launch_us"] * 1e-6) / 1e9, 1),
-                "frac": round(pb / (cold_plain["avg_launch_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                "basis": "cold, as above",
-                "note": "BASELINE's target kernel counted its way (3*N*s per averaging: read parameters, read the "
-                        "peer snapshot, write parameters): the same dispatch without the write-through of the "
-                        "next snapshot, i.e. what the full-publish rounds run; the timed loop's kernel is the "
-                        "write-through one above",
-            }
         if wt_kernel and args.numel == RESNET18_NUMEL and args.dtype == "f32":
             out["roofline"]["vs_mix_ceiling"] = dict(MIX_CEILING_11M, kernel_frac_over_ceiling=round(
                 achieved / HBM_PEAK_GBS / MIX_CEILING_11M["frac"], 4),
-                note="the chip's cold ceiling for one 11.17M-element 2R:2W launch (single learner); a batched "
-                     "dispatch moves more bytes per ramp/drain, so it can exceed it")
+                note="the chip's cold ceiling for one 11.17M-element 2R:2W launch")
+        if pair is not None:
+            out["co_resident_pair"] = pair
         if publish_fallback:
             out["publish_fallback"] = publish_fallback
         if pull_trials:
@@ -1893,14 +2029,10 @@ def main(argv=None):
                 "ms_per_step": round(1e3 * w_el / args.steps, 4),
                 "avg_launch_us": round(w_us, 2),
                 "kernel_gbs": round(w_bytes / (w_us * 1e-6) / 1e9, 1),
-                "note": "the same rounds with another publish form (value from an uninstrumented pass, the kernel "
-                        "from a sampled one; under a resident main run, a second pair of learners). resident: the "
-                        "parameters live in the learner's two slots, the average reads one and writes the other "
-                        "(3*N*s) and the publish moves nothing. write-through: the averaging kernel also writes the next snapshot "
-                        "(4*N*s) and the publish moves nothing; full: every publish copies the 2*N*s snapshot. "
-                        "Write-through is valid when nothing modifies the parameters between update_wait and the "
-                        "next update_send (the reference's loop, examples/pytorch-cifar/main.py:130-145); the "
-                        "adapter checks the parameters' version counters and storage before reusing a snapshot",
+                "note": "the same rounds with the other publish form (value from an uninstrumented pass, the kernel "
+                        "from a sampled one). full: every publish copies the 2*N*s snapshot, then the 3*N*s "
+                        "average; write-through: the averaging kernel also writes the next snapshot (4*N*s) and "
+                        "the publish moves nothing",
             }
         if overlap is not None:
             out["overlap"] = overlap
@@ -1917,29 +2049,12 @@ def main(argv=None):
         if world == 1:
             out["roofline"]["size_sweep"] = size_rows
         out["round_sweep"] = round_rows
-    if out is not None:
-        # last key, so it stays in the tail of the output a driver keeps: the drop-in form's numbers
-        # (the reference's own loop order) beside the headline's
-        ref = {"order": "update_send -> step -> update_wait (README.md:18-29, main.py:130-145)",
-               "publish": "write-through"}
-        sp = out.get("secondary_publish")
-        if sp is not None and sp["publish"] == "write-through":
-            ref.update(value=sp["value"], ms_per_step=sp["ms_per_step"])
-        elif not resident_main and wt_main:
-            ref.update(value=out["value"], ms_per_step=out["ms_per_step"])
-        else:
-            ref.update(value=None, ms_per_step=None)
-        ref["kernel_cold"] = cold_ref or None
-        if resident_main:
-            ref["headline"] = "resident (update_send -> update_wait -> step): %.1f GB/s" % out["value"]
-        out["reference_loop"] = ref
     wd.hold(out, 1 if parity_failed else 0)
     if world == 1 and not args.no_sweep:
         wd.enter("size sweep", 900.0)
         size_sweep(device, rows=size_rows)
         wd.enter("round sweep", 900.0)
-        round_sweep(device, tmp, batch=batched, rows=round_rows,
-                    publish="resident" if resident_main else "write-through")
+        round_sweep(device, tmp, rows=round_rows, publish=form)
     elif world > 1 and not args.no_sweep:
         # the timed learners' buffers go first: the sweep's 7B learner needs ~80 GB per GPU
         for conn, _ in lockstep_learners + async_learners:

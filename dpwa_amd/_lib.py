@@ -99,6 +99,8 @@ SIGNATURES = {
     "dpwa_node_set_resident": [_vp, _vp, _vp],
     "dpwa_learner_fetch_state": [_vp, _i64, _pint],
     "dpwa_learner_rescue_free": [_vp, _pint],
+    "dpwa_learner_rescue_lanes": [_vp, _pint, _pint],
+    "dpwa_learner_set_rescue_cap": [_vp, ctypes.c_int],
     "dpwa_learner_fetch_stream": [_vp, ctypes.POINTER(_vp)],
     "dpwa_learner_copy_factor": [_vp, _vp, _vp],
     "dpwa_learner_copy_fetched": [_vp, _vp, _vp],

@@ -302,8 +302,15 @@ static void close_endpoint(Endpoint &ep)
 
 // A rescue lane: where a fetch re-selected after a timed-out pull goes (conn.py:304-309) -- a
 // buffer and a stream of the greatest priority (a hardware queue no stalled normal-priority stream
-// shares), so no stalled pull ahead of it can hold it up.
-constexpr int kRescueLanes = 3;
+// shares), so no stalled pull ahead of it can hold it up.  Lanes are made at first use, up to
+// kMaxRescueLanes and only while the device keeps kRescueReserve free beyond the new buffer; an
+// allocation that fails caps the count where it is (rescue_cap) instead of failing the round.
+constexpr int kMaxRescueLanes = 8;
+// fetch_state: a backlog on the caller's stream longer than this no longer defers the timeout (a
+// stream that never reaches update_send is stuck, not slow); a probe waits at most kProbeWaitUs
+constexpr int64_t kMaxBacklogMs = 60000;
+constexpr int64_t kProbeWaitUs = 5000;
+constexpr size_t kRescueReserve = (size_t)1 << 30;
 struct RescueLane {
     char *buf = nullptr;
     hipStream_t stream = nullptr;
@@ -358,9 +365,15 @@ struct dpwa_learner {
     bool stage_read[2] = {false, false};
     // rescue lanes (RescueLane), allocated at first use: a lane whose pull has not landed stays
     // taken and the next re-selected pull takes another, as TxThread keeps re-selecting
-    RescueLane rescue[kRescueLanes];
+    RescueLane rescue[kMaxRescueLanes];
     int rescue_lanes = 0;
+    int rescue_cap = kMaxRescueLanes;   // lowered when a lane's allocation fails
     int64_t fetch_issue_ns = 0;         // host time the fetch in flight was issued (its timeout clock)
+    // the fetch in flight waits for ev_issue (the caller's stream at update_send): its deadline runs
+    // from when that point is reached, not from the host's enqueue (fetch_state)
+    bool issue_evented = false;
+    hipStream_t probe_stream = nullptr; // greatest priority, only ever holds ev_probe (fetch_state)
+    hipEvent_t ev_probe = nullptr;
     hipStream_t fetch_stream = nullptr; // stream the fetch in flight moves its bytes on
     int stage_next = 0;
     int src_stage = -1;                 // buffer l->src points into: staging 0 / 1, rescue lane 2 + j; -1: none
@@ -546,7 +559,7 @@ int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype
         for (auto &ev : l->ev_published)
             if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) break;
         if (e != hipSuccess) break;
-        if ((e = hipEventCreateWithFlags(&l->ev_issue, hipEventDisableTiming)) != hipSuccess) break;
+        if ((e = hipEventCreate(&l->ev_issue)) != hipSuccess) break;     // timed: the fetch deadline
         if ((e = hipEventCreateWithFlags(&l->ev_fetched, hipEventDisableTiming)) != hipSuccess) break;
         if ((e = hipEventCreateWithFlags(&l->ev_consumed, hipEventDisableTiming)) != hipSuccess) break;
         for (auto &ev : l->ev_stage_done)
@@ -590,6 +603,8 @@ int dpwa_learner_destroy(dpwa_learner *l)
     for (auto ev : l->ev_published)
         if (ev) (void)hipEventDestroy(ev);
     if (l->ev_issue) (void)hipEventDestroy(l->ev_issue);
+    if (l->ev_probe) (void)hipEventDestroy(l->ev_probe);
+    if (l->probe_stream) (void)hipStreamDestroy(l->probe_stream);
     if (l->ev_fetched) (void)hipEventDestroy(l->ev_fetched);
     if (l->ev_consumed) (void)hipEventDestroy(l->ev_consumed);
     for (auto ev : l->ev_stage_done)
@@ -723,9 +738,10 @@ int dpwa_learner_version(const dpwa_learner *l, uint64_t *version)
     return DPWA_OK;
 }
 
+// peer == l is the self-peer (the learner's own published slot, read like any local peer's)
 int dpwa_learner_attach_local(dpwa_learner *l, int peer_id, dpwa_learner *peer)
 {
-    if (!l || !peer || peer == l) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_local: bad peer");
+    if (!l || !peer) return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_local: bad peer");
     if (peer->n != l->n || peer->dtype != l->dtype)
         return set_error(DPWA_ERR_ARG, "dpwa_learner_attach_local: peer holds %lld elements of dtype %d, this learner %lld of %d",
                          (long long)peer->n, peer->dtype, (long long)l->n, l->dtype);
@@ -846,10 +862,9 @@ int dpwa_learner_attach_fds(dpwa_learner *l, int peer_id, const void *handle, in
     return DPWA_OK;
 }
 
-// A free rescue lane (its last pull landed, or none issued), allocating one when every lane is
-// taken and fewer than kRescueLanes exist; *lane = -1 when all kRescueLanes are still pulling.
-// A new lane is built in a local and counted only once every resource exists.
-static int rescue_lane(dpwa_learner *l, int *lane)
+// A free rescue lane: one whose last pull landed (or none issued); *lane = -1 when every lane made
+// so far is still pulling.
+static int free_lane(dpwa_learner *l, int *lane)
 {
     *lane = -1;
     for (int j = 0; j < l->rescue_lanes; ++j) {
@@ -861,7 +876,23 @@ static int rescue_lane(dpwa_learner *l, int *lane)
         }
         if (e != hipErrorNotReady) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(e));
     }
-    if (l->rescue_lanes == kRescueLanes) return DPWA_OK;
+    return DPWA_OK;
+}
+
+// A free rescue lane, making a new one when every lane is taken and fewer than rescue_cap exist;
+// *lane = -1 when none is free and none can be made.  A new lane is built in a local and counted
+// only once every resource exists.  Running short of memory (or an allocation failing) is not an
+// error of the round: the lane count is capped where it is and the caller waits for a lane to land.
+static int rescue_lane(dpwa_learner *l, int *lane)
+{
+    int rc = free_lane(l, lane);
+    if (rc || *lane >= 0 || l->rescue_lanes >= l->rescue_cap) return rc;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < l->slot_stride + kRescueReserve) {
+        (void)hipGetLastError();
+        l->rescue_cap = l->rescue_lanes;
+        return DPWA_OK;
+    }
     RescueLane r;
     int least = 0, greatest = 0;
     hipError_t e;
@@ -874,8 +905,9 @@ static int rescue_lane(dpwa_learner *l, int *lane)
     } while (0);
     if (e != hipSuccess) {
         destroy_lane(r);
-        return set_error(DPWA_ERR_HIP, "rescue lane %d: %s (%zu bytes)", l->rescue_lanes, hipGetErrorString(e),
-                         l->slot_stride);
+        (void)hipGetLastError();          // clear the sticky error: the round goes on without a new lane
+        l->rescue_cap = l->rescue_lanes;
+        return DPWA_OK;
     }
     l->rescue[l->rescue_lanes] = r;
     *lane = l->rescue_lanes++;
@@ -910,6 +942,7 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
     }
     l->fetch_issue_ns = now_ns();
     l->fetch_stream = l->side;
+    l->issue_evented = false;
     if (flags & DPWA_FETCH_RESCUE) {
         // re-selected after a timed-out pull: a free lane (its own stream and buffer), ordered
         // after the publish of the snapshot (above, local peers) and after the last reader of the
@@ -918,11 +951,13 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
         const int rc = rescue_lane(l, &j);
         if (rc) return rc;
         if (j < 0)
-            return set_error(DPWA_ERR_STATE, "dpwa_learner_fetch: all %d rescue lanes are still pulling", kRescueLanes);
+            return set_error(DPWA_ERR_STATE, "dpwa_learner_fetch: all %d rescue lanes are still pulling",
+                             l->rescue_lanes);
         RescueLane &r = l->rescue[j];
         if (!(flags & DPWA_FETCH_PUBLISHED)) {
             HIP_TRY(hipEventRecord(l->ev_issue, s));
             HIP_TRY(hipStreamWaitEvent(r.stream, l->ev_issue, 0));
+            l->issue_evented = true;
         }
         if (r.read) HIP_TRY(hipStreamWaitEvent(r.stream, r.ev_done, 0));
         const size_t nbytes = kPayloadOff + round_up(l->payload_bytes, 16);
@@ -969,6 +1004,7 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
         if (l->stage_read[0]) HIP_TRY(hipStreamWaitEvent(l->side, l->ev_stage_done[0], 0));
         HIP_TRY(hipEventRecord(l->ev_issue, s));
         HIP_TRY(hipStreamWaitEvent(l->side, l->ev_issue, 0));
+        l->issue_evented = true;
         // WAR on our own staging buffer: the previous average must have consumed it.
         if (l->consumed_once && l->consume_stream != s) {
             HIP_TRY(hipEventRecord(l->ev_consumed, l->consume_stream));
@@ -1814,6 +1850,30 @@ int dpwa_learner_copy_fetched(dpwa_learner *l, void *dst_dev, dpwa_stream_t stre
     return DPWA_OK;
 }
 
+// Milliseconds since the (completed, timing) event `since`, on the device's clock: an event
+// recorded now on the probe stream -- a stream of the greatest priority that holds nothing else --
+// and the two timestamps' difference.  DPWA_ERR_STATE when the probe does not complete within
+// kProbeWaitUs (the probe's hardware queue is held up: no measurement).
+static int probe_since(dpwa_learner *l, hipEvent_t since, float *ms)
+{
+    if (!l->probe_stream) {
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&l->probe_stream, hipStreamNonBlocking, greatest));
+        HIP_TRY(hipEventCreate(&l->ev_probe));
+    }
+    HIP_TRY(hipEventRecord(l->ev_probe, l->probe_stream));
+    const int64_t t0 = now_ns();
+    for (;;) {
+        const hipError_t q = hipEventQuery(l->ev_probe);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(q));
+        if (now_ns() - t0 > kProbeWaitUs * 1000) return set_error(DPWA_ERR_STATE, "probe held up");
+    }
+    HIP_TRY(hipEventElapsedTime(ms, since, l->ev_probe));
+    return DPWA_OK;
+}
+
 int dpwa_learner_fetch_state(dpwa_learner *l, int64_t timeout_ms, int *state)
 {
     if (!l || !state) return set_error(DPWA_ERR_ARG, "dpwa_learner_fetch_state: NULL argument");
@@ -1823,23 +1883,51 @@ int dpwa_learner_fetch_state(dpwa_learner *l, int64_t timeout_ms, int *state)
     const hipError_t e = hipEventQuery(l->ev_fetched);
     if (e == hipSuccess) return DPWA_OK;
     if (e != hipErrorNotReady) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(e));
-    const bool late = timeout_ms >= 0 && now_ns() - l->fetch_issue_ns >= timeout_ms * 1000000LL;
-    *state = late ? DPWA_FETCH_TIMED_OUT : DPWA_FETCH_IN_FLIGHT;
+    *state = DPWA_FETCH_IN_FLIGHT;
+    if (timeout_ms < 0) return DPWA_OK;
+    // The host's enqueue is an upper bound on how long the request has been out: within the
+    // timeout by it, the pull is in time.  Past it, a pull ordered after the caller's stream
+    // (ev_issue: a local peer's snapshot) is timed from when that stream reached update_send --
+    // the reference's socket timeout bounds only the wait for the reply (conn.py:249), and work the
+    // caller queued before update_send is not the peer's delay.
+    const int64_t waited_ns = now_ns() - l->fetch_issue_ns;
+    if (waited_ns < timeout_ms * 1000000LL) return DPWA_OK;
+    if (l->issue_evented && waited_ns < (timeout_ms + kMaxBacklogMs) * 1000000LL) {
+        const hipError_t q = hipEventQuery(l->ev_issue);
+        if (q == hipErrorNotReady) return DPWA_OK;        // the request has not gone out yet
+        if (q != hipSuccess) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(q));
+        float ms = 0.f;
+        if (probe_since(l, l->ev_issue, &ms) == DPWA_OK && ms >= 0.f) {
+            *state = ms >= (float)timeout_ms ? DPWA_FETCH_TIMED_OUT : DPWA_FETCH_IN_FLIGHT;
+            return DPWA_OK;
+        }
+    }
+    *state = DPWA_FETCH_TIMED_OUT;
     return DPWA_OK;
 }
 
 int dpwa_learner_rescue_free(dpwa_learner *l, int *free_out)
 {
     if (!l || !free_out) return set_error(DPWA_ERR_ARG, "dpwa_learner_rescue_free: NULL argument");
-    *free_out = 1;
-    if (l->rescue_lanes < kRescueLanes) return DPWA_OK;     // a lane can still be made
     DeviceGuard dg(l->device);
-    for (int j = 0; j < l->rescue_lanes; ++j) {
-        const hipError_t e = hipEventQuery(l->rescue[j].ev_landed);
-        if (e == hipSuccess) return DPWA_OK;
-        if (e != hipErrorNotReady) return set_error(DPWA_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(e));
-    }
-    *free_out = 0;
+    int lane = -1;
+    const int rc = rescue_lane(l, &lane);     // makes a lane now if one is needed and can be made
+    *free_out = lane >= 0 ? 1 : 0;
+    return rc;
+}
+
+int dpwa_learner_rescue_lanes(dpwa_learner *l, int *lanes, int *cap)
+{
+    if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_rescue_lanes: NULL learner");
+    if (lanes) *lanes = l->rescue_lanes;
+    if (cap) *cap = l->rescue_cap;
+    return DPWA_OK;
+}
+
+int dpwa_learner_set_rescue_cap(dpwa_learner *l, int cap)
+{
+    if (!l || cap < 0) return set_error(DPWA_ERR_ARG, "dpwa_learner_set_rescue_cap: bad arguments");
+    l->rescue_cap = std::min(std::max(cap, l->rescue_lanes), kMaxRescueLanes);
     return DPWA_OK;
 }
 

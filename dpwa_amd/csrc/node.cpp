@@ -8,7 +8,9 @@
 //   update_wait          dpwa/dpwa.py:125-156  (factor only; the lerp follows separately)
 //   update_wait_average  dpwa/dpwa.py:125-156 + dpwa/adapters/pytorch.py:60-68 in one kernel
 // Built only on the public C ABI of the learner and the scheduler.
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <thread>
@@ -50,6 +52,9 @@ struct dpwa_node {
     // update_wait polls it (reply_pending), as data or as a timeout
     int timeout_ms = -1;
     bool reply_pending = false;
+    // how long a re-selected request waits for a free rescue lane (every lane still pulling) before
+    // it is given up: DPWA_RESCUE_WAIT_MS, default 60 s
+    int64_t rescue_wait_ms = 60000;
 };
 
 using namespace dpwa;
@@ -89,6 +94,7 @@ int dpwa_node_create(dpwa_node **out, int n_peers, const uint32_t *seed_key, int
         return rc;
     }
     n->cfg = *cfg;
+    if (const char *w = getenv("DPWA_RESCUE_WAIT_MS")) n->rescue_wait_ms = std::max(0LL, atoll(w));
     n->peers.assign((size_t)n_peers, PeerRef());
     n->status.assign((size_t)(n_peers > 0 ? n_peers : 1), DPWA_PEER_DOWN);
     n->attached.assign((size_t)n_peers, 0);
@@ -121,10 +127,13 @@ int dpwa_node_handles(dpwa_node *n, dpwa_learner **learner, dpwa_sched **sched)
     return DPWA_OK;
 }
 
+// A LOCAL peer may be the node itself: a YAML node entry at this node's own host:port is its own
+// RxThread, which the reference's TxThread dials like any other (conn.py:246-251, 98-110), so the
+// node averages with the snapshot it published (configs[1]'s self-peer).
 int dpwa_node_set_peer(dpwa_node *n, int peer, int kind, dpwa_node *local)
 {
     if (!n || peer < 0 || (size_t)peer >= n->peers.size() || kind < PEER_UNSET || kind > PEER_REMOTE ||
-        (kind == PEER_LOCAL && (!local || local == n)))
+        (kind == PEER_LOCAL && !local))
         return set_error(DPWA_ERR_ARG, "dpwa_node_set_peer: bad arguments");
     PeerRef &p = n->peers[peer];
     p.kind = kind;
@@ -274,13 +283,17 @@ static int fetch_loop(dpwa_node *n, int flags, dpwa_stream_t stream, bool rescue
             int state = DPWA_FETCH_LANDED;
             if (rescue && judged) {
                 // a rescue lane must be free: its last pull landed, or another lane can be made
-                // (with every lane's pull stalled our own transport is stuck: wait up to the
-                // timeout, then this request times out and the round ends)
+                // (up to 8, memory permitting).  With every lane's pull still in flight it is this
+                // learner's own transport that is held up, not the peer: the request waits for a
+                // lane to land before it goes out, unjudged -- the reference's timeout bounds only
+                // the reply (conn.py:249) -- and TxThread's loop goes on (conn.py:286-313).  Only a
+                // transport stuck for rescue_wait_ms gives the request up as a timeout and ends
+                // the round without data.
                 int free_ = 1;
                 const int64_t t0 = now_ms();
                 while ((rc = dpwa_learner_rescue_free(n->learner, &free_)) == DPWA_OK && !free_ &&
-                       now_ms() - t0 < n->timeout_ms)
-                    std::this_thread::sleep_for(std::chrono::microseconds(20));
+                       now_ms() - t0 < n->rescue_wait_ms)
+                    std::this_thread::sleep_for(std::chrono::microseconds(50));
                 if (rc) break;
                 if (!free_) {
                     if (via_board) dpwa_board_release(n->board, n->board_rank[peer], nullptr, 1);

@@ -32,6 +32,13 @@ import torch
 from . import _lib
 
 
+def _address(node):
+    """(host, port) of a YAML node entry as the reference dials it (conn.py:250); localhost
+    and 127.0.0.1 are one address."""
+    host = str(getattr(node, "host", ""))
+    return ("127.0.0.1" if host == "localhost" else host, int(getattr(node, "port", -1)))
+
+
 class LocalGroup:
     """prefetch: once every learner of the group has published the round, start all granted
     fetches at once on the learners' side streams, so the pulls overlap the training step that
@@ -59,19 +66,36 @@ class LocalGroup:
         ref = self.members.get(name)
         return ref() if ref is not None else None
 
+    def _server(self, p):
+        """The member whose RxThread a TxThread dialling peer entry `p` reaches: the reference
+        connects by (host, port) (conn.py:246-251), so an entry at a member's own address is that
+        member whatever its name -- including the dialling node itself (configs[1]'s self-peer:
+        a node entry at the learner's own host:port serves its own published snapshot)."""
+        other = self.member(p.name)
+        if other is not None:
+            return other
+        for name in list(self.members):
+            m = self.member(name)
+            if m is not None and _address(m.me) == _address(p):
+                return m
+        return None
+
     def join(self, conn):
         old = self.member(conn.name)
         if old is not None and old is not conn:
             raise OSError(98, "node %r is already bound in this process" % conn.name)   # EADDRINUSE
         self.members[conn.name] = weakref.ref(conn)
         for k, p in enumerate(conn.peers):          # wire both directions
-            other = self.member(p.name)
-            if other is None:
+            other = self._server(p)
+            if other is not None:
+                conn._set_peer(k, _lib.NODE_PEER_LOCAL, other)
+        for name in list(self.members):
+            other = self.member(name)
+            if other is None or other is conn:
                 continue
-            conn._set_peer(k, _lib.NODE_PEER_LOCAL, other)
-            j = other._peer_index.get(conn.name)
-            if j is not None:
-                other._set_peer(j, _lib.NODE_PEER_LOCAL, conn)
+            for j, q in enumerate(other.peers):
+                if q.name == conn.name or _address(q) == _address(conn.me):
+                    other._set_peer(j, _lib.NODE_PEER_LOCAL, conn)
 
     def leave(self, conn):
         if self.member(conn.name) is not conn:
@@ -79,9 +103,11 @@ class LocalGroup:
         del self.members[conn.name]
         for name in list(self.members):
             other = self.member(name)
-            j = other._peer_index.get(conn.name) if other is not None else None
-            if j is not None:
-                other._set_peer(j, _lib.NODE_PEER_UNSET, None)
+            if other is None:
+                continue
+            for j, q in enumerate(other.peers):
+                if q.name == conn.name or _address(q) == _address(conn.me):
+                    other._set_peer(j, _lib.NODE_PEER_UNSET, None)
 
     def on_bind(self, conn):
         pass

@@ -169,7 +169,8 @@ int dpwa_learner_publish(dpwa_learner *l, const void *flat, double loss, const d
 int dpwa_learner_version(const dpwa_learner *l, uint64_t *version);
 
 /* Peers.  `peer_id` is the caller's index of that peer (e.g. its node index).
- * attach_local: the peer learner lives in this process (any device).
+ * attach_local: the peer learner lives in this process (any device); peer == l is the
+ * self-peer (a YAML node at the learner's own host:port: its own published snapshot).
  * ipc_handle / attach_ipc: the peer lives in another process; ipc_handle describes the
  * snapshot allocation (handle_len = DPWA_IPC_HANDLE_BYTES) and, for an ordinary allocation,
  * carries its hipIpcGetMemHandle.  Allocations of 1.5 GiB and more (or any size with
@@ -201,27 +202,35 @@ int dpwa_learner_attach_fds(dpwa_learner *l, int peer_id, const void *handle, in
 /* DPWA_FETCH_RESCUE: the fetch re-selected after a timed-out pull (conn.py:304-309 reconnects and
  * picks again): it copies into a rescue lane -- a buffer and a stream of the greatest priority of
  * its own -- so the stalled pull ahead of it on the side stream cannot hold it up.  A lane whose
- * pull has not landed stays taken and the next re-selected pull takes another (up to 3 lanes,
- * allocated at first use, one snapshot each); DPWA_ERR_STATE when all are still pulling. */
+ * pull has not landed stays taken and the next re-selected pull takes another (lanes made at first
+ * use, up to 8, see rescue_free); DPWA_ERR_STATE when no lane is free. */
 #define DPWA_FETCH_RESCUE 4
 int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int flags,
                        dpwa_stream_t stream);
 /* The fetch timeout of the device path (the reference's socket timeout, conn.py:249 with
  * timeout_ms from the YAML, and its handling at conn.py:304-309).  fetch_state polls the copying
  * fetch in flight without blocking: DPWA_FETCH_LANDED (landed, or nothing to wait for),
- * DPWA_FETCH_IN_FLIGHT, or DPWA_FETCH_TIMED_OUT (still in flight timeout_ms after it was issued).
- * The clock starts when the host issues the pull, so for a pull ordered after the caller's
- * stream (a local peer's snapshot, not through the board) a device backlog queued on that stream
- * before update_send counts toward timeout_ms -- the reference's socket timeout measures only the
- * reply; judged pulls are LocalGroup copying pulls and board pulls (which wait for nothing of
- * the caller's).  rescue_free: *free_out = 1 when a rescue lane is free (its pull landed) or can
- * still be allocated.  fetch_stream: the stream the fetch in flight moves its bytes on (side
- * stream or a rescue lane's). */
+ * DPWA_FETCH_IN_FLIGHT, or DPWA_FETCH_TIMED_OUT (still in flight timeout_ms after the request went
+ * out).  The reference's socket timeout bounds only the wait for the reply (conn.py:249), so a pull
+ * ordered after the caller's stream (a local peer's snapshot) is timed from when that stream
+ * reached update_send -- a device backlog the caller queued before update_send is not the peer's
+ * delay: while the stream has not reached it the pull is in flight, after it the time since is read
+ * on the device's clock (an event on a probe stream of its own, timestamps compared); a backlog of
+ * over 60 s, or a probe that cannot run, falls back to the host's issue time.  Board pulls wait
+ * for nothing of the caller's and are timed from the issue.  Judged pulls are LocalGroup copying
+ * pulls and board pulls.  rescue_free: *free_out = 1 when a rescue lane is free (its pull landed) or one
+ * could be made now (it is made here: up to 8 lanes, each one snapshot, while 1 GiB stays free on
+ * the device; a failed allocation caps the count where it is, *free_out = 0, no error).
+ * rescue_lanes: lanes made so far and the current cap; set_rescue_cap lowers (or raises, up to 8)
+ * the cap -- not below the lanes already made.  fetch_stream: the stream the fetch in flight moves
+ * its bytes on (side stream or a rescue lane's). */
 #define DPWA_FETCH_LANDED 0
 #define DPWA_FETCH_IN_FLIGHT 1
 #define DPWA_FETCH_TIMED_OUT 2
 int dpwa_learner_fetch_state(dpwa_learner *l, int64_t timeout_ms, int *state);
 int dpwa_learner_rescue_free(dpwa_learner *l, int *free_out);
+int dpwa_learner_rescue_lanes(dpwa_learner *l, int *lanes, int *cap);
+int dpwa_learner_set_rescue_cap(dpwa_learner *l, int cap);
 int dpwa_learner_fetch_stream(dpwa_learner *l, dpwa_stream_t *stream);
 
 /* update_wait's averaging (dpwa.py:133-155 + pytorch.py:64-68) as ONE kernel: make `stream`
@@ -467,7 +476,9 @@ int dpwa_node_destroy(dpwa_node *n);
 int dpwa_node_bind(dpwa_node *n, int device, int64_t numel, int32_t dtype);
 /* Borrowed handles of the node's learner (NULL before bind) and scheduler. */
 int dpwa_node_handles(dpwa_node *n, dpwa_learner **learner, dpwa_sched **sched);
-/* How peer `peer` (scheduler index) is reached: DPWA_NODE_PEER_*; `local` for LOCAL. */
+/* How peer `peer` (scheduler index) is reached: DPWA_NODE_PEER_*; `local` for LOCAL (may be n
+ * itself: a node entry at this node's own host:port, whose RxThread the reference dials like any
+ * peer's -- the self-peer of configs[1]). */
 int dpwa_node_set_peer(dpwa_node *n, int peer, int kind, dpwa_node *local);
 /* Fault injection: force a DPWA_PEER_* status for a peer, -1 clears. */
 int dpwa_node_set_fault(dpwa_node *n, int peer, int status);
@@ -479,16 +490,18 @@ typedef struct dpwa_board dpwa_board;
 int dpwa_node_set_board(dpwa_node *n, dpwa_board *board, const int32_t *peer_ranks, int publish_timeout_ms);
 /* The YAML's timeout_ms (DpwaConfiguration.get_timeoutms, dpwa.py:90 -> conn.py:249) on the
  * device path (< 0 disables).  A copying pull from a local peer or through the gossip board is
- * judged when update_wait polls it (never a host wait in the normal path): landed, or issued
- * less than timeout_ms ago -> the reply with data (score +10, conn.py:301-302; a pull still in
- * flight is then waited for on the device); still in flight after timeout_ms -> a socket timeout
- * (score -100, reconnect, conn.py:304-309) and the loop picks again, the re-selected pull going
- * to a rescue lane (DPWA_FETCH_RESCUE) and being polled on the host up to timeout_ms like the
- * reference's blocking receive; a rescue pull that times out too is followed by the next pick on
- * another lane, until data, no peer, or every lane stalled (then the request times out and the
- * round ends without data -- the reference would keep picking; the learner's own transport is
- * what is stuck).  Lock-step (DistGroup) pulls wait for the round's barrier,
- * i.e. for the slowest learner, not for the peer, and are not judged. */
+ * judged when update_wait polls it (never a host wait in the normal path): landed, or out less
+ * than timeout_ms (dpwa_learner_fetch_state) -> the reply with data (score +10, conn.py:301-302;
+ * a pull still in flight is then waited for on the device); still in flight after timeout_ms -> a
+ * socket timeout (score -100, reconnect, conn.py:304-309) and the loop picks again, the
+ * re-selected pull going to a rescue lane (DPWA_FETCH_RESCUE) and being polled on the host up to
+ * timeout_ms like the reference's blocking receive; a rescue pull that times out too is followed
+ * by the next pick on another lane, until data, no peer or every peer removed, as TxThread
+ * (conn.py:286-313).  With every lane (up to 8) still pulling, the next request waits for one to
+ * land before it goes out; only a learner whose own transport stays stuck for
+ * $DPWA_RESCUE_WAIT_MS (default 60000) gives that request up as a timeout and ends the round
+ * without data.  Lock-step (DistGroup) pulls wait for the round's barrier, i.e. for the slowest
+ * learner, not for the peer, and are not judged. */
 int dpwa_node_set_timeout(dpwa_node *n, int timeout_ms);
 
 /* update_send (dpwa.py:104-123): publish, then the Bernoulli gate; with DPWA_FLAG_EAGER a

@@ -22,15 +22,25 @@ def add_bf16(param_u16, delta_u16):
 
 
 def simulate(names, init, deltas, send_loss, wait_loss, method, value, threshold, fetch_probability,
-             seeds, lerp=lerp_f32, add=None, train_after_wait=False):
+             seeds, lerp=lerp_f32, add=None, train_after_wait=False, nodes=None, serves=None):
     """init (G, n) and deltas (T, G, n): fp32 arrays, or raw bf16 bits (uint16) with
     lerp=lerp_bf16, add=add_bf16.  train_after_wait: round r's training delta is applied after
     its update_wait instead of between update_send and update_wait (the order a loop with
     resident parameters must keep: update_send, update_wait, training step); out_params then
-    holds the parameters after the average, before that delta."""
+    holds the parameters after the average, before that delta.
+
+    nodes (default `names`): the YAML's node list; each learner's peers are the nodes other than
+    itself, by name (dpwa.py:65-72).  serves (default: each learner by its own name): node name ->
+    index of the learner whose RxThread answers at that node's address -- TxThread dials
+    (host, port) (conn.py:246-251), so a node entry at a learner's own address is that learner;
+    {"w1-self": 0} with nodes ["w1", "w1-self"] is configs[1]'s self-peer."""
     G, n = init.shape
     T = deltas.shape[0]
-    learners = [OracleLearner(names[g], [x for x in names if x != names[g]], fetch_probability,
+    nodes = list(names) if nodes is None else list(nodes)
+    idx = {nm: i for i, nm in enumerate(names)}
+    if serves is not None:
+        idx.update(serves)
+    learners = [OracleLearner(names[g], [x for x in nodes if x != names[g]], fetch_probability,
                               method, value, threshold, seeds[g]) for g in range(G)]
     params = init.copy()
     out_params = np.zeros((T, G, n), init.dtype)
@@ -54,7 +64,6 @@ def simulate(names, init, deltas, send_loss, wait_loss, method, value, threshold
             L = learners[g]
             state, payload, attempts = None, None, []
             if L.fetching:
-                idx = {nm: i for i, nm in enumerate(names)}
                 state, payload, attempts = L.fetch(
                     lambda peer: "ok",
                     lambda peer: ("payload", states[idx[peer]], snaps[idx[peer]]))

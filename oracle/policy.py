@@ -93,8 +93,9 @@ class OracleLearner:
     def fetch(self, connect_fn, request_fn, max_attempts=None, stop=None):
         """Returns (state, payload, attempts); state/payload None when no data.  stop (not the
         reference's): called after each request's outcome is applied; True ends the loop there
-        without data -- this implementation's one divergence, a round whose every rescue lane is
-        stalled."""
+        without data -- the one case where the device path stops where TxThread would go on: the
+        learner's own transport stuck (every rescue lane still pulling for DPWA_RESCUE_WAIT_MS,
+        DESIGN §4)."""
         attempts = []
         while True:
             if max_attempts is not None and len(attempts) >= max_attempts:

@@ -26,6 +26,7 @@ Outputs (all small; see tests/golden/README.md):
   peer_add.json         the same with removed peers put back by add_peer (dpwa.py:95-96, conn.py:208-213)
   gossip.npz/.json      lock-step G-learner gossip through the real adapter + connection + TxThread
   gossip_step_after_wait.npz/.json   the same with the step after update_wait (the resident order)
+  gossip_self.npz/.json one learner whose peer is its own RxThread (a node entry at its own address)
   wire.json             <HLL + pickle frames (dpwa/messaging.py:24-94)
   config.json           YAML parsing (dpwa/dpwa.py:29-93)
 
@@ -673,6 +674,99 @@ def gen_gossip_step_after_wait(tmp):
     gen_gossip(tmp, step_after_wait=True)
 
 
+# configs[1]'s self-peer: one learner whose YAML lists a second node entry at its own host:port,
+# so its TxThread dials its own RxThread (conn.py:246-251 -> 98-110) and averages with the
+# snapshot it published.  (interpolation, constant value, divergence threshold, fetch_probability)
+GOSSIP_SELF_CASES = [("constant", 0.5, 0.0, 1.0), ("clock", None, 0.5, 0.7), ("loss", None, 0.5, 1.0),
+                     ("constant", 0.25, 0.0, 0.7)]
+
+
+def gen_gossip_self(tmp):
+    """One learner, README order (update_send, step, update_wait), nodes [w1 @ P, w1-self @ P]:
+    every fetch reaches w1's own RxThread.  The fake socket layer routes a connection by address,
+    as TCP does (FakeRx.registry), so the reference alone decides picks, factors and clocks."""
+    npz = {}
+    meta = {"shapes": GOSSIP_SHAPES, "cases": [], "order": "update_send, step, update_wait",
+            "nodes": "w1 and w1-self at one host:port (the learner's own RxThread)"}
+    n = sum(int(np.prod(s_)) for s_ in GOSSIP_SHAPES)
+    T = 10
+    for ci, (interp, val, thr, fp) in enumerate(GOSSIP_SELF_CASES):
+        port = 51000 + ci
+        nodes = [{"name": "w1", "host": "localhost", "port": port},
+                 {"name": "w1-self", "host": "localhost", "port": port}]
+        ADDR2NAME[("localhost", port)] = "w1-self"      # only w1 dials, and only w1-self is its peer
+        cfg = os.path.join(tmp, "gossip_self_%d.yaml" % ci)
+        write_config(cfg, nodes, fp, interp, thr, extra=val)
+        rng = np.random.default_rng(500 + ci)
+        init = rng.standard_normal((1, n)).astype(np.float32)
+        deltas = (0.01 * rng.standard_normal((T, 1, n))).astype(np.float32)
+        lrng = random.Random(455 + ci)
+        send_loss = [[2 * math.exp(-r / 3.0) + 0.05 * lrng.random()] for r in range(T)]
+        wait_loss = [[2 * math.exp(-(r + 0.5) / 3.0) + 0.05 * lrng.random()] for r in range(T)]
+        net = Net(GOSSIP_SHAPES)
+        load_flat(net, init[0])
+        seed = 5000 + ci
+        conn = new_connection(cfg, "w1", seed, real_tx=True)
+        adapter = adapter_for(net, conn)
+
+        def reply(peer):
+            rx = FakeRx.registry[("localhost", port)]
+            with rx.lock:
+                return copy.deepcopy(rx.state), rx.payload
+
+        ENV.connect_fn = lambda peer: "ok"
+        ENV.request_fn = lambda peer: "payload"
+        ENV.reply_fn = reply
+        ENV.gate = None
+        params = np.zeros((T, 1, n), np.float32)
+        clocks = np.zeros((T, 1), np.float64)
+        factors = np.zeros((T, 1), np.float64)
+        fetching = np.zeros((T, 1), np.bool_)
+        picks = [[None] for _ in range(T)]
+        for r in range(T):
+            RNG.set_current("w1")
+            ENV.logs["w1"] = []
+            adapter.update_send(send_loss[r][0])
+            fetching[r, 0] = conn.fetching
+            with torch.no_grad():                        # the "training step"
+                off = 0
+                for _, p_ in net.named_parameters():
+                    k = p_.numel()
+                    p_.data.add_(torch.from_numpy(deltas[r, 0, off:off + k]).view(p_.shape))
+                    off += k
+            holder = {}
+            orig = conn.update_wait
+
+            def wrapped(loss, orig=orig, holder=holder):
+                res = orig(loss)
+                holder["factor"] = res[1]
+                return res
+
+            conn.update_wait = wrapped
+            adapter.update_wait(wait_loss[r][0])
+            del conn.update_wait
+            factors[r, 0] = holder["factor"]
+            clocks[r, 0] = conn.clock
+            params[r, 0] = flat_params(net)
+            picks[r][0] = [a["peer"] for a in ENV.logs["w1"]]
+        conn.tx._queue.put(False)
+        key = "c%d" % ci
+        npz[key + "_init"] = init
+        npz[key + "_deltas"] = deltas
+        npz[key + "_params"] = params
+        npz[key + "_clocks"] = clocks
+        npz[key + "_factors"] = factors
+        npz[key + "_fetching"] = fetching
+        meta["cases"].append({"key": key, "interpolation": interp, "value": val, "divergence_threshold": thr,
+                              "fetch_probability": fp, "G": 1, "names": ["w1"], "nodes": ["w1", "w1-self"],
+                              "serves": {"w1-self": 0}, "seeds": [seed], "send_loss": send_loss,
+                              "wait_loss": wait_loss, "picks": picks})
+    np.savez_compressed(os.path.join(OUT, "gossip_self.npz"), **npz)
+    with open(os.path.join(OUT, "gossip_self.json"), "wt") as f:
+        json.dump(meta, f, indent=0)
+    print("gossip_self: %d cases" % len(meta["cases"]))
+
+
 # ----------------------------------------------------------------------------
 # F. wire frames
 # ----------------------------------------------------------------------------
@@ -829,6 +923,7 @@ def main():
         gen_peer_add(tmp)
         gen_gossip(tmp)
         gen_gossip_step_after_wait(tmp)
+        gen_gossip_self(tmp)
         gen_wire()
         gen_wire_adapter()
         gen_config(tmp)

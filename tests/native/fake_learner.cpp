@@ -4,7 +4,9 @@
 // and the sanitizers, and driven from a CPU test against the oracle policy
 // (tests/test_node_host.py).  Nothing here touches a GPU: a "pull" is a record; whether it
 // stalls is scripted per learner (fake_stall): a stalled pull never lands, so update_wait judges
-// it timed out, and a stalled rescue pull keeps its lane taken until fake_land_all().
+// it timed out, and a stalled rescue pull keeps its lane taken until fake_land_all() -- or, with
+// every lane taken, until the node has polled for a free lane `land_after` times (fake_lanes; the
+// lane cap there also stands in for a lane allocation that fails).
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -33,7 +35,7 @@ int set_error(int code, const char *fmt, ...)
 using dpwa::set_error;
 
 namespace {
-constexpr int kLanes = 3;   // as learner.cpp kRescueLanes
+constexpr int kMaxLanes = 8;   // as learner.cpp kMaxRescueLanes
 }
 
 struct dpwa_learner {
@@ -44,6 +46,9 @@ struct dpwa_learner {
     bool fetch_stalled = false;
     int lanes = 0;               // rescue lanes allocated
     int lanes_stalled = 0;       // of them, holding a stalled pull
+    int cap = kMaxLanes;         // lanes that can be made (a lower cap: the next allocation fails)
+    int land_after = -1;         // with every lane stalled: one lands after this many polls (-1 never)
+    int polls = 0;               // rescue_free polls that found no lane since the last landing
     int peer = -1;
     uint64_t peer_version = 0;
     int pulls = 0, rescue_pulls = 0, averages = 0, relocations = 0;
@@ -66,6 +71,15 @@ int fake_land_all(dpwa_learner *l)      // every stalled pull lands (the end of 
     if (!l) return DPWA_ERR_ARG;
     l->lanes_stalled = 0;
     l->fetch_stalled = false;
+    return DPWA_OK;
+}
+
+int fake_lanes(dpwa_learner *l, int cap, int land_after)   // lane cap; polls until a stalled lane lands
+{
+    if (!l || cap < 0 || cap > kMaxLanes) return DPWA_ERR_ARG;
+    l->cap = cap < l->lanes ? l->lanes : cap;
+    l->land_after = land_after;
+    l->polls = 0;
     return DPWA_OK;
 }
 
@@ -135,9 +149,8 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
     const bool stalled = l->stall_next > 0;
     if (stalled) l->stall_next--;
     if (flags & DPWA_FETCH_RESCUE) {
-        const bool free_lane = l->lanes_stalled < l->lanes || l->lanes < kLanes;
-        if (!free_lane) return set_error(DPWA_ERR_STATE, "fetch: all rescue lanes are still pulling");
-        if (l->lanes_stalled == l->lanes) l->lanes++;   // none free: a new lane
+        // as learner.cpp: rescue_free made a lane when none was free, so one is free here
+        if (l->lanes_stalled >= l->lanes) return set_error(DPWA_ERR_STATE, "fetch: no free rescue lane");
         if (stalled) l->lanes_stalled++;
         l->rescue_pulls++;
     }
@@ -159,7 +172,20 @@ int dpwa_learner_fetch_state(dpwa_learner *l, int64_t, int *state)
 int dpwa_learner_rescue_free(dpwa_learner *l, int *free_out)
 {
     if (!l || !free_out) return set_error(DPWA_ERR_ARG, "rescue_free");
-    *free_out = (l->lanes < kLanes || l->lanes_stalled < l->lanes) ? 1 : 0;
+    *free_out = 1;
+    if (l->lanes_stalled < l->lanes) return DPWA_OK;          // a lane's pull landed
+    if (l->lanes < l->cap) {                                   // make one (learner.cpp rescue_lane)
+        l->lanes++;
+        return DPWA_OK;
+    }
+    // every lane still pulling: one lands after `land_after` polls (a transport that was held up),
+    // or never (a stuck one: the node gives up after DPWA_RESCUE_WAIT_MS)
+    if (l->land_after >= 0 && ++l->polls > l->land_after) {
+        l->lanes_stalled--;
+        l->polls = 0;
+        return DPWA_OK;
+    }
+    *free_out = 0;
     return DPWA_OK;
 }
 

@@ -2,9 +2,10 @@
 // update_wait, dpwa.py:104-156, with TxThread's fetch loop, conn.py:277-315) over the host-only
 // fake learner (fake_learner.cpp) and the real scheduler (sched.cpp), built with the sanitizers.
 // G lock-step learners, `rounds` rounds; in every round each learner's first `stall` pulls stall
-// (the count drawn from a seeded generator, 0-5, mostly 0): the node must judge the side pull
-// timed out, re-select into rescue lanes, keep re-selecting while a lane's pull stalls too, and end
-// the round without data only when every lane is stalled.  Prints one JSON object per
+// (the count drawn from a seeded generator, 0-12, mostly 0): the node must judge the side pull
+// timed out, re-select into rescue lanes, keep re-selecting while a lane's pull stalls too -- with
+// every lane taken (8, or 3 where lane allocations fail) waiting for one to land, and ending the
+// round without data only when no lane lands within DPWA_RESCUE_WAIT_MS (a stuck transport).  Prints one JSON object per
 // (round, learner) -- the script and what the node did -- for tests/test_node_host.py to replay in
 // oracle/policy.py, and checks invariants on the way.
 #include <cstdint>
@@ -18,6 +19,7 @@ extern "C" {
 int fake_stall(dpwa_learner *l, int n);
 int fake_land_all(dpwa_learner *l);
 int fake_counts(dpwa_learner *l, int *out);
+int fake_lanes(dpwa_learner *l, int cap, int land_after);
 }
 
 static uint64_t g_rng = 0;
@@ -72,12 +74,21 @@ int main(int argc, char **argv)
     printf("[\n");
     bool first = true;
     for (int r = 0; r < rounds; ++r) {
-        std::vector<int> stall(G), fetching(G);
+        std::vector<int> stall(G), fetching(G), cap(G), stuck(G);
         std::vector<std::vector<int>> fault(G, std::vector<int>(G - 1, -1));
         for (int g = 0; g < G; ++g) {
             const uint64_t u = next_u64() % 100;
-            stall[g] = u < 70 ? 0 : u < 80 ? 1 : u < 87 ? 2 : u < 92 ? 3 : u < 96 ? 4 : 5;
+            stall[g] = u < 60 ? 0 : u < 70 ? 1 : u < 76 ? 2 : u < 81 ? 3 : u < 85 ? 4 : u < 89 ? 5 :
+                       u < 94 ? 6 + (int)(next_u64() % 4) : 10 + (int)(next_u64() % 3);
             CHECK(fake_stall(learners[g], stall[g]));
+            // odd learners: lane allocations fail after 3 lanes; a quarter of the rounds with every
+            // lane stalled have a stuck transport (no lane ever lands), the rest a held-up one
+            int lanes_now[5];
+            CHECK(fake_counts(learners[g], lanes_now));
+            cap[g] = (g % 2) ? 3 : 8;
+            if (cap[g] < lanes_now[2]) cap[g] = lanes_now[2];
+            stuck[g] = (next_u64() % 4) == 0;
+            CHECK(fake_lanes(learners[g], cap[g], stuck[g] ? -1 : 2));
             for (int k = 0; k < G - 1; ++k) {   // what a request to peer k meets this round
                 if ((int)(next_u64() % 100) < fault_pct) {
                     const uint64_t v = next_u64() % 100;
@@ -111,14 +122,14 @@ int main(int argc, char **argv)
             CHECK(dpwa_node_info(nodes[g], &f, &fp_, &fv, &att));
             EXPECT(peer >= -1 && peer < G - 1);
             EXPECT(after[3] - before[3] == (peer >= 0 ? 1 : 0));            // averaged iff data
-            EXPECT(after[2] <= 3);                                           // at most 3 rescue lanes
+            EXPECT(after[2] <= cap[g]);                                      // lanes within the cap
             EXPECT(fetching[g] || peer < 0);
             if (!fetching[g]) att = 0;                                       // (info keeps the last fetch's count)
             EXPECT(after[0] - before[0] <= att);                             // a pull per attempt at most
             printf("%s{\"round\": %d, \"learner\": %d, \"stall\": %d, \"fetching\": %d, \"peer\": %d, \"attempts\": %d, "
-                   "\"pulls\": %d, \"rescue_pulls\": %d, \"lanes\": %d, \"scores\": [",
+                   "\"pulls\": %d, \"rescue_pulls\": %d, \"lanes\": %d, \"cap\": %d, \"stuck\": %d, \"scores\": [",
                    first ? "" : ",\n", r, g, stall[g], fetching[g], peer, att, after[0] - before[0],
-                   after[1] - before[1], after[2]);
+                   after[1] - before[1], after[2], cap[g], stuck[g]);
             first = false;
             for (int k = 0; k < G - 1; ++k) {
                 int sc = 0;

@@ -29,7 +29,7 @@ def test_parity_transports_cover_every_trial_and_the_fd_shared_path():
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
     import bench
-    assert bench.parity_transports(1) == ["local", "local+res"]
+    assert bench.parity_transports(1) == ["self", "local", "local+res"]
     t = bench.parity_transports(8)
     assert "lockstep/relay-avg:32+vmm" in t and "async/copy+vmm" in t
     assert "lockstep/relay-avg:32+res+vmm" in t and "async/copy+res+vmm" in t
@@ -132,3 +132,39 @@ def test_committed_pmc_traffic_is_found_for_the_line_kernels():
         assert tb and src.startswith("profiles/traffic_"), (publish, learners)
         assert abs(tb / (learners * per * n * 4) - 1) < 1e-3, (publish, learners, tb)
     assert bench.pmc_traffic(None, "resident", 2, n + 1, "f32", "cold") == (None, None)
+
+
+def test_scaling_basis_has_one_schema_at_every_n():
+    """`scaling_basis` (raw and weak rounds/s, one learner per GPU) carries the same keys at N=1, 2 and
+    8, with and without the overlap leg, so the driver's per-N lines compare like with like."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    ov = {"gossip_rounds_per_s": 800.0, "ms_per_step": 1.2, "compute_only_ms_per_step": 1.19,
+          "gossip_overhead_frac": 0.008}
+    shapes = set()
+    for world in (1, 2, 8):
+        for overlap in (ov, None):
+            sb = bench.scaling_basis(world, 1, "write-through", 20.0 * world, 0.001, 5000.0, overlap)
+            shapes.add((tuple(sorted(sb)), tuple(sorted(sb["raw"])), tuple(sorted(sb["weak"]))))
+            assert sb["learners"] == world and sb["raw"]["gossip_rounds_per_s"] == 20000.0 * world
+            assert sb["raw"]["gossip_rounds_per_s_per_learner"] == 20000.0
+            if overlap:
+                assert sb["weak"]["gossip_rounds_per_s_per_learner"] == round(800.0 / world, 1)
+            else:
+                assert sb["weak"]["gossip_rounds_per_s"] is None
+    assert len(shapes) == 1
+
+
+def test_self_peer_config_is_the_reference_schema(tmp_path):
+    """bench's configs[1] YAML: the learner and a second entry at its own host:port; parsed by the
+    reference-schema reader, the learner's only peer is that entry, at the learner's own address."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    from dpwa_amd.dpwa import DpwaConfiguration
+    cfg = tmp_path / "c.yaml"
+    bench.write_config(str(cfg), ["w1"], "constant", self_peer=True, base_port=45123)
+    nodes = DpwaConfiguration(str(cfg)).get_nodes()
+    assert [n["name"] for n in nodes] == ["w1", "w1-self"]
+    assert {(n["host"], n["port"]) for n in nodes} == {("127.0.0.1", 45123)}

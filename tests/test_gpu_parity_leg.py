@@ -76,5 +76,5 @@ def test_parity_leg_local_one_process():
         sys.path.insert(0, ROOT)
     import bench
     with tempfile.TemporaryDirectory() as tmp:
-        res = bench.parity_leg(1, 0, 0, torch.device("cuda", 0), tmp, ["local"], "nccl")
-    assert res == {"local": True}
+        res = bench.parity_leg(1, 0, 0, torch.device("cuda", 0), tmp, ["self", "local"], "nccl")
+    assert res == {"self": True, "local": True}

@@ -152,6 +152,29 @@ def test_gossip_step_after_wait_trajectories_match_reference():
         assert not olerp.bits_equal(other["params"], z[k + "_params"]), k
 
 
+def test_self_peer_trajectories_match_reference():
+    """configs[1]'s self-peer (make_golden.py gen_gossip_self: the real adapter, connection and
+    TxThread of one learner whose YAML lists a second node entry at its own host:port, so every
+    fetch reaches its own RxThread, conn.py:246-251 -> 98-110) against oracle/gossip.py with that
+    node list, bit for bit -- constant, clock and loss interpolation, fetch_probability 1 and 0.7."""
+    meta = load_json("gossip_self.json")
+    z = load_npz("gossip_self.npz")
+    assert meta["order"] == "update_send, step, update_wait"
+    assert {c["interpolation"] for c in meta["cases"]} == {"constant", "clock", "loss"}
+    for case in meta["cases"]:
+        k = case["key"]
+        assert case["nodes"] == ["w1", "w1-self"] and case["serves"] == {"w1-self": 0}
+        res = ogossip.simulate(case["names"], z[k + "_init"], z[k + "_deltas"], case["send_loss"],
+                               case["wait_loss"], case["interpolation"], case["value"],
+                               case["divergence_threshold"], case["fetch_probability"], case["seeds"],
+                               nodes=case["nodes"], serves=case["serves"])
+        assert res["picks"] == case["picks"], k
+        assert np.array_equal(res["fetching"], z[k + "_fetching"]), k
+        assert np.array_equal(res["factors"], z[k + "_factors"]), k
+        assert np.array_equal(res["clocks"], z[k + "_clocks"]), k
+        assert olerp.bits_equal(res["params"], z[k + "_params"]), k
+
+
 def test_fixture_files_are_data_only():
     """Fixtures are inputs/outputs (json/npz), never reference source."""
     import os
