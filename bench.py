@@ -487,6 +487,7 @@ def cpu_baseline(numel, seconds, rows=True):
 # against the oracle (oracle/ is imported only here and by the cpu_baseline leg, as the
 # checker -- never on the measured path).
 PARITY_N, PARITY_T, PARITY_FP = 1_000_003, 12, 0.7
+OVERLAP_PAIRS = 4               # interleaved (step alone, step + gossip) pairs of the overlap leg
 PARITY_ASYNC_T = 16
 PARITY_PHASE_S = 180.0          # watchdog budget of one parity transport
 
@@ -1772,25 +1773,36 @@ def main(argv=None):
         o_wt = True if resident_main else wt_main
         progress("overlap: %d GEMMs per step, %s learners" % (k_gemm, "write-through" if o_wt else "full"))
         learners[:] = wt_set
-        t_compute = run_overlap(o_steps, 3, compute, False, o_wt, update)
         o_trials = {}
         o_mode = sel_mode
+        modes_o = [o_mode]
         if world > 1 and o_mode != "copy" and args.pull == "auto":
             # the copy engine leaves every CU to the training step: try it beside the
             # pure-loop winner and keep the cheaper overlap
-            for m in [m for m in (o_mode, "copy")
-                      if verified(("async/" + m + ("+wt" if o_wt else "")) if sel_async else m)]:
-                set_pull(m)
-                o_trials[m] = run_overlap(o_steps, 3, compute, True, o_wt, update)
-            o_mode = min(o_trials, key=o_trials.get)
-            t_both = o_trials[o_mode]
+            modes_o = [m for m in (o_mode, "copy")
+                       if verified(("async/" + m + ("+wt" if o_wt else "")) if sel_async else m)] or [o_mode]
+        # interleaved pairs (step alone, step + gossip) per mode; the first pair is dropped (a run's
+        # first phase meets different clocks) and the medians of the rest are compared
+        t_c, t_b = [], {m: [] for m in modes_o}
+        for _ in range(OVERLAP_PAIRS):
+            t_c.append(run_overlap(o_steps, 3, compute, False, o_wt, update))
+            for m in modes_o:
+                if len(modes_o) > 1:
+                    set_pull(m)
+                t_b[m].append(run_overlap(o_steps, 3, compute, True, o_wt, update))
+        t_compute = float(np.median(t_c[1:]))
+        o_trials = {m: float(np.median(v[1:])) for m, v in t_b.items()}
+        o_mode = min(o_trials, key=o_trials.get)
+        t_both = o_trials[o_mode]
+        if len(modes_o) > 1:
             set_pull(sel_mode)
         else:
-            t_both = run_overlap(o_steps, 3, compute, True, o_wt, update)
+            o_trials = {}
         learners[:] = main_set
         overlap = {
             "compute": "%d x bf16 GEMM 4096^3 per learner per step (%.1f us each)" % (k_gemm, gemm_us),
             "steps": o_steps,
+            "pairs": "%d interleaved (step alone, step + gossip) pairs, the first dropped, medians" % OVERLAP_PAIRS,
             "compute_only_ms_per_step": round(1e3 * t_compute / o_steps, 4),
             "ms_per_step": round(1e3 * t_both / o_steps, 4),
             "gossip_overhead_frac": round(t_both / t_compute - 1.0, 4),

@@ -79,6 +79,25 @@ class DpwaPyTorchAdapter:
         self._guard_set = False
         self._versions = None
         self._sent = None           # resident: the version counters at the last update_send
+        self._warned_rehome = False
+
+    def _warn_rehome(self, moved):
+        """Once per adapter: the caller re-homed a parameter (``param.data = ...``), so its loop
+        works on ``param.data`` -- and in-place writes through ``.data`` move no version counter.
+        When the device reuse guard has not caught any such write so far (its sampled words all
+        matched), say plainly where write-through snapshots can go stale (this re-home itself is
+        seen: this round publishes in full).  Reading the guard's count synchronises the device,
+        once."""
+        self._warned_rehome = True
+        hits = self.reuse_guard_hits if self._reuse_guard else 0
+        if hits == 0:
+            LOGGER.warning(
+                "DpwaPyTorchAdapter(%s): %d parameter(s) were re-homed through param.data. Write-through "
+                "snapshots (the default) are reused when no version counter moved; in-place writes through "
+                "param.data move none and are caught only if they change one of the %d words the reuse guard "
+                "samples. A loop that writes parameters sparsely through param.data between update_wait and "
+                "update_send must pass write_through=False, or peers may average with a snapshot that lacks "
+                "those writes.", self._conn.name, moved, 4096)
 
     def _param_versions(self):
         return [p._version for p in self._flat.params] + [self._flat.buffer._version]
@@ -108,6 +127,8 @@ class DpwaPyTorchAdapter:
             self._sent = self._param_versions()
             return
         moved = self._flat.resync()
+        if moved and self._write_through and not self._warned_rehome:
+            self._warn_rehome(moved)
         reuse = (self._write_through and moved == 0 and self._versions is not None
                  and self._versions == self._param_versions())
         self._versions = None

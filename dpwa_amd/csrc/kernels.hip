@@ -801,11 +801,13 @@ hipError_t launch_average_batch(int32_t dtype, bool dual, const AvgBatch &b, hip
         const int64_t gi = (e.n / per) / kStreamBlock + 1;   // as launch_blocks: last span may be empty
         if (gi > 0x7fffffffLL) return hipErrorInvalidValue;
     }
+    int64_t total = 0;   // in 64 bits: up to 8 entries of up to 2^31 - 1 workgroups each
     for (int i = 0; i < x.count; ++i) {
-        x.begin[i] = g;
-        g += (uint32_t)((x.e[i].n / per) / kStreamBlock + 1);
+        x.begin[i] = (uint32_t)total;
+        total += (x.e[i].n / per) / kStreamBlock + 1;
+        if (total > 0x7fffffffLL) return hipErrorInvalidValue;
     }
-    if (g > 0x7fffffffu) return hipErrorInvalidValue;
+    g = (uint32_t)total;
     for (int i = x.count; i < kMaxAvgBatch; ++i) x.begin[i] = 0xffffffffu;
     // span order: see batch_order()
     bool same = true;

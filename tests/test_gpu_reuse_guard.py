@@ -121,3 +121,79 @@ def test_reuse_guard_compares_the_tail_bytes(tmp_path):
         hits.append(h.value)
         c.close()
     assert hits == [T - 1, 0], hits
+
+
+def _sparse_round(tmp_path, write_through):
+    """Learner a writes ONE element through param.data between update_wait and update_send, at a
+    16-B word the guard does not sample (n16 = 25,008 words, samples every ~6.1 words: word 3 lies
+    between samples 0 and 1).  Learner b averages with constant 1.0, so after the next round b's
+    parameters ARE the snapshot a served.  Returns (b's element, the written value, a's element
+    before the write, reuse guard hits of a)."""
+    n = 100_032
+    rng = np.random.default_rng(31)
+    init = rng.standard_normal((2, n)).astype(np.float32)
+    cfg = tmp_path / ("sparse_%d.yaml" % write_through)
+    write_cfg(cfg, ["a", "b"], 1.0, "constant", 0.0, 1.0)
+    group = LocalGroup()
+    nets, ads = [], []
+    for g, nm in enumerate(("a", "b")):
+        net = Net([(n,)]).to(DEV)
+        load_flat(net, init[g])
+        nets.append(net)
+        ads.append(DpwaPyTorchAdapter(net, nm, str(cfg), seed=40 + g, group=group, write_through=write_through))
+    for ad in ads:
+        ad.update_send(1.0)
+    for ad in ads:
+        ad.update_wait(1.0)
+    k = 3 * 4 + 1                          # an fp32 element of 16-B word 3 (not sampled)
+    before = float(nets[0].p0.detach()[k].item())
+    with torch.no_grad():
+        nets[0].p0.data[k] = 123.25        # in place through .data: no version counter moves
+    for ad in ads:
+        ad.update_send(1.0)
+    for ad in ads:
+        ad.update_wait(1.0)
+    got = float(nets[1].p0.detach()[k].item())
+    hits = ads[0].reuse_guard_hits
+    for ad in ads:
+        ad.connection.close()
+    return got, 123.25, before, hits
+
+
+def test_sparse_data_write_missing_the_samples_is_stale_under_write_through(tmp_path):
+    """The documented limit of the write-through default (adapter docstring, README quick-start):
+    a sparse write through param.data between update_wait and update_send that changes none of the
+    guard's sampled words is NOT in the next snapshot -- the peer averages with the value before
+    the write (the reference would have published it, pytorch.py:49-53); with write_through=False
+    every publish copies the parameters and the peer gets the written value."""
+    got, written, before, hits = _sparse_round(tmp_path, True)
+    assert hits == 0 and got == before and got != written
+    got, written, before, hits = _sparse_round(tmp_path, False)
+    assert got == written
+
+
+def test_rehomed_parameter_warns_once(tmp_path, caplog):
+    """A parameter re-homed through param.data (``p.data = ...``) is folded back into the flat buffer
+    and published in full, and the write-through adapter warns once -- while its guard has caught
+    nothing -- where such loops can meet stale snapshots (the previous test's case)."""
+    import logging
+    n = 4096
+    cfg = tmp_path / "rehome.yaml"
+    write_cfg(cfg, ["a", "b"], 1.0, "constant", 0.0, 0.5)
+    group = LocalGroup()
+    nets, ads = [], []
+    for g, nm in enumerate(("a", "b")):
+        net = Net([(n,)]).to(DEV)
+        nets.append(net)
+        ads.append(DpwaPyTorchAdapter(net, nm, str(cfg), seed=60 + g, group=group))
+    with caplog.at_level(logging.WARNING, logger="dpwa_amd.adapters.pytorch"):
+        for r in range(3):
+            nets[0].p0.data = torch.full((n,), float(r), device=DEV)     # re-homed every round
+            for ad in ads:
+                ad.update_send(1.0)
+            for ad in ads:
+                ad.update_wait(1.0)
+    warned = [rec for rec in caplog.records if "re-homed" in rec.getMessage()]
+    assert len(warned) == 1 and "write_through=False" in warned[0].getMessage()
+    for ad in ads:
+        ad.connection.close()

@@ -203,18 +203,25 @@ def test_board_pull_times_out_and_the_rescue_pull_reads_a_whole_snapshot(tmp_pat
     assert seen == exp, (seen, exp)
 
 
-def _stalled_rescue(_rank, tmp):
+def _stalled_rescue(_rank, tmp, mode):
     """See test_stalled_rescue_pulls_take_the_next_lane.  Rounds (learner 0): 1: its side stream
     held -> timeout, the re-selected pull on rescue lane 0 -> data; 2: side stream and lane 0 held
     -> two timeouts, lane 1 -> data; 3: side, lanes 0 and 1 held -> three timeouts, lane 2 ->
-    data; 4: side and all three lanes held -> four timeouts, then no lane is free within the
-    timeout: that request times out and the round ends without data (five timeouts)."""
+    data; 4: side and all three lanes held -> four timeouts, then
+      mode "grow":   a fourth lane is made -> data (TxThread keeps re-selecting, conn.py:286-313);
+      mode "capped": the lane count is capped at 3 (dpwa_learner_set_rescue_cap, as after a failed
+                     allocation): the request waits for lane 0's pull to land, then goes out -> data;
+      mode "stuck":  capped, and DPWA_RESCUE_WAIT_MS is shorter than the holds: no lane lands in
+                     time, that request times out and the round ends without data (five timeouts)."""
+    import os
     import pathlib
     import time
+    if mode == "stuck":
+        os.environ["DPWA_RESCUE_WAIT_MS"] = "50"        # read at node creation
     tmp_path = pathlib.Path(tmp)
     G = 3
     names = ["x%d" % g for g in range(G)]
-    cfg = tmp_path / "stall.yaml"
+    cfg = tmp_path / ("stall_%s.yaml" % mode)
     write_cfg(cfg, names, timeout_ms=TIMEOUT_MS)
     rng = np.random.default_rng(5)
     n, T = 50_003, 5
@@ -222,7 +229,8 @@ def _stalled_rescue(_rank, tmp):
     send = [[1.0 + g + r for g in range(G)] for r in range(T)]
     wait = [[2.0 + g + r for g in range(G)] for r in range(T)]
     seeds = [90 + g for g in range(G)]
-    timeouts = {1: 1, 2: 2, 3: 3, 4: 5}        # learner 0: its first k requests of round r time out
+    stuck = mode == "stuck"
+    timeouts = {1: 1, 2: 2, 3: 3, 4: 5 if stuck else 4}   # learner 0: its first k requests of round r time out
     idx = {nm: i for i, nm in enumerate(names)}
     L = [OracleLearner(names[g], [x for x in names if x != names[g]], 1.0, "clock", None, 0.0, seeds[g])
          for g in range(G)]
@@ -242,7 +250,7 @@ def _stalled_rescue(_rank, tmp):
                 return "payload", states[idx[peer]], snaps[idx[peer]]
 
             state, payload, attempts = L[g].fetch(lambda p: "ok", request,
-                                                  max_attempts=5 if (g == 0 and r == 4) else None)
+                                                  max_attempts=5 if (g == 0 and r == 4 and stuck) else None)
             averaged, factor = L[g].update_wait(wait[r][g], state, payload is not None)
             if averaged:
                 params[g] = olerp.lerp_f32(params[g], payload, factor)
@@ -261,14 +269,21 @@ def _stalled_rescue(_rank, tmp):
             holds += [Hold(s, HOLD_S + (j + 1) * 0.3) for j, s in enumerate(lanes[:r - 1])]
         for g in range(G):
             conns[g].update_send(flats[g], send[r][g])
+        if r == 1 and mode != "grow":                # bound by now: at most three lanes from here on
+            _lib.call("dpwa_learner_set_rescue_cap", conns[0]._learner.handle, 3)
         if r >= 1:
             time.sleep(HOST_WAIT_S)
+        t_wait = time.perf_counter()
         got = [conns[g].update_wait_average(flats[g], wait[r][g]) for g in range(G)]
-        if 1 <= r <= 3:   # the stream the rescue pull that delivered ran on: a new lane
-            s = ctypes.c_void_p()
-            _lib.call("dpwa_learner_fetch_stream", conns[0]._learner.handle, ctypes.byref(s))
+        t_wait = time.perf_counter() - t_wait
+        s = ctypes.c_void_p()
+        _lib.call("dpwa_learner_fetch_stream", conns[0]._learner.handle, ctypes.byref(s))
+        if 1 <= r <= 3 or (r == 4 and mode == "grow"):   # the rescue pull that delivered: a new lane
             assert s.value not in [x.cuda_stream for x in lanes] + [side_stream(conns[0]).cuda_stream], r
             lanes.append(torch.cuda.ExternalStream(s.value, device=DEV))
+        elif r == 4 and mode == "capped":                # ... or, capped, the lane that landed first
+            assert s.value == lanes[0].cuda_stream
+            assert t_wait >= 0.5, t_wait                 # it waited for that lane's hold, well past 3 timeouts
         torch.cuda.synchronize()
         if holds:
             holds[0].check(HOST_WAIT_S)
@@ -277,24 +292,71 @@ def _stalled_rescue(_rank, tmp):
         p_exp, c_exp, s_exp, pk_exp = exp[r]
         for g in range(G):
             peer = got[g][0].peer if got[g][0] is not None else ""
-            want = pk_exp[g][-1] if (g or r != 4) else ""
+            want = pk_exp[g][-1] if (g or r != 4 or not stuck) else ""
             assert (peer, conns[g].last_fetch_attempts) == (want, len(pk_exp[g])), \
                 (r, g, peer, conns[g].last_fetch_attempts, pk_exp[g])
             assert conns[g].flow_control_scores() == dict(zip([x for x in names if x != names[g]], s_exp[g])), (r, g)
             assert olerp.bits_equal(flats[g].cpu().numpy(), p_exp[g]), (r, g)
             assert conns[g].clock == c_exp[g], (r, g)
-    assert len(lanes) == 3
+    nl, cap = ctypes.c_int(), ctypes.c_int()
+    _lib.call("dpwa_learner_rescue_lanes", conns[0]._learner.handle, ctypes.byref(nl), ctypes.byref(cap))
+    assert (nl.value, cap.value) == ((4, 8) if mode == "grow" else (3, 3)), (nl.value, cap.value)
     for c in conns:
         c.close()
 
 
-def test_stalled_rescue_pulls_take_the_next_lane(tmp_path):
+@pytest.mark.parametrize("mode", ["grow", "capped", "stuck"])
+def test_stalled_rescue_pulls_take_the_next_lane(tmp_path, mode):
     """TxThread keeps re-selecting after a timeout until data, no peer, or every peer removed
     (conn.py:286-313).  Here a re-selected pull whose rescue lane is stalled times out too and the
-    next pick goes to another lane: with the side stream and one, then two rescue lanes held, the
-    round still ends with data from the next pick -- peers, attempts, scores, clocks and parameters
-    as the oracle policy with those requests scripted as timeouts.  Only with all three lanes held
-    (the learner's own transport stuck) does the next request time out and the round end without
-    data: five timeouts, -100 each.  Runs in a fresh process (a stream map of its own)."""
+    next pick goes to another lane: with the side stream and one, two, then all three rescue lanes
+    held, the round still ends with data from the next pick -- on a fourth lane made for it, or,
+    with the lanes capped at three (as after a lane allocation that failed), on the first lane whose
+    pull lands -- peers, attempts, scores, clocks and parameters as the oracle policy with those
+    requests scripted as timeouts.  Only a transport stuck for DPWA_RESCUE_WAIT_MS (here 50 ms,
+    shorter than the holds) gives the request up: five timeouts, -100 each, no data.  Each mode
+    runs in a fresh process (a stream map of its own)."""
     import torch.multiprocessing as mp
-    mp.spawn(_stalled_rescue, args=(str(tmp_path),), nprocs=1, join=True)
+    mp.spawn(_stalled_rescue, args=(str(tmp_path), mode), nprocs=1, join=True)
+
+
+def test_backlog_on_the_callers_stream_is_not_the_peers_delay(tmp_path):
+    """The reference's timeout bounds only the wait for the reply (conn.py:249).  Work the caller
+    queued on its own stream before update_send -- here a spin several times timeout_ms long --
+    holds back a local peer's pull (it is ordered after that stream), but the request has not gone
+    out until the stream gets there: the healthy peer is data, scored +10, never -100 -- the
+    oracle's rounds with no timeout, every round, at 2 and 3 learners."""
+    import time
+    for G in (2, 3):
+        names = ["b%d" % g for g in range(G)]
+        cfg = tmp_path / ("backlog_%d.yaml" % G)
+        write_cfg(cfg, names, timeout_ms=TIMEOUT_MS)
+        rng = np.random.default_rng(6 + G)
+        n, T = 100_003, 3
+        init = rng.standard_normal((G, n)).astype(np.float32)
+        send = [[1.0 + g + r for g in range(G)] for r in range(T)]
+        wait = [[2.0 + g + r for g in range(G)] for r in range(T)]
+        seeds = [70 + g for g in range(G)]
+        exp = expected(names, init, send, wait, seeds, {})
+        group = LocalGroup(prefetch=True, zero_copy=False)
+        conns = [DpwaConnection(names[g], str(cfg), seed=seeds[g], group=group) for g in range(G)]
+        flats = [torch.from_numpy(init[g]).to(DEV) for g in range(G)]
+        for r in range(T):
+            hold = Hold(torch.cuda.current_stream(DEV)) if r >= 1 else None   # the caller's backlog
+            for g in range(G):
+                conns[g].update_send(flats[g], send[r][g])
+            if hold is not None:
+                time.sleep(HOST_WAIT_S)                  # past the deadline as the host counts it
+            for g in range(G):
+                conns[g].update_wait_average(flats[g], wait[r][g])
+            torch.cuda.synchronize()
+            if hold is not None:
+                hold.check(HOST_WAIT_S)                  # the backlog outlasted the judging point
+            params, clocks, scores, row = exp[r]
+            for g in range(G):
+                assert conns[g].last_fetch_attempts == 1, (G, r, g)
+                assert conns[g].flow_control_scores() == dict(zip([x for x in names if x != names[g]], scores[g]))
+                assert olerp.bits_equal(flats[g].cpu().numpy(), params[g]), (G, r, g)
+                assert conns[g].clock == clocks[g]
+        for c in conns:
+            c.close()

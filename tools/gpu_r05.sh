@@ -2,6 +2,9 @@
 # Round-5 evidence script: one parameterised GPU session (replaces round 4's per-lease gpu_r04*.sh).
 #   tools/gpu_r05.sh <tag> <steps...>
 # steps: smoke | tests:<pytest-args> | bench[:<bench args>] | rocprof[:<bench args>] | pmc:<cold_sweep args>
+#        | rehearse:<N>[ <bench args>]  (the N>1 line self-launched on one GPU over gloo)
+#        | py:<script + args>
+# e.g. gpurun --timeout 1200 -- bash tools/gpu_r05.sh r05b smoke "tests:-m gpu tests" "bench:--steps 20 --warmup 5"
 # Every step runs under its own timeout; the script stops at the first failing step.
 set -o pipefail
 tag=$1; shift
@@ -26,6 +29,11 @@ for step in "$@"; do
       for ctr in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace -d "$GRAFT_REPO_ROOT/$out/pmc_${i}_$ctr" -o run -- python3 "$GRAFT_REPO_ROOT/tools/cold_sweep.py" $arg > "$GRAFT_REPO_ROOT/$out/pmc_${i}_$ctr.log" 2>&1) || { echo "pmc $ctr failed" >&2; tail -20 "$out/pmc_${i}_$ctr.log" >&2; exit 1; }
       done ;;
+    rehearse)
+      n=${arg%% *}; rest=${arg#"$n"}
+      timeout -k 10 900 python -u bench.py --gpus $n --dist-backend gloo --steps 20 --warmup 5 \
+          --dist-sweep-max-numel 100000000 $rest > "$out/rehearse_n$n.json" 2> "$out/rehearse_n$n.err" \
+          || { echo "rehearsal n=$n failed" >&2; tail -40 "$out/rehearse_n$n.err" >&2; exit 1; } ;;
     py)
       timeout -k 10 600 python -u $arg > "$out/py_$i.log" 2>&1 || { echo "py failed" >&2; tail -40 "$out/py_$i.log" >&2; exit 1; } ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
