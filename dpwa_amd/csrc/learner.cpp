@@ -309,7 +309,7 @@ constexpr int kMaxRescueLanes = 8;
 // fetch_state: a backlog on the caller's stream longer than this no longer defers the timeout (a
 // stream that never reaches update_send is stuck, not slow); a probe waits at most kProbeWaitUs
 constexpr int64_t kMaxBacklogMs = 60000;
-constexpr int64_t kProbeWaitUs = 5000;
+constexpr int64_t kProbeWaitUs = 2000;
 constexpr size_t kRescueReserve = (size_t)1 << 30;
 struct RescueLane {
     char *buf = nullptr;
@@ -372,7 +372,7 @@ struct dpwa_learner {
     // the fetch in flight waits for ev_issue (the caller's stream at update_send): its deadline runs
     // from when that point is reached, not from the host's enqueue (fetch_state)
     bool issue_evented = false;
-    hipStream_t probe_stream = nullptr; // greatest priority, only ever holds ev_probe (fetch_state)
+    hipStream_t probe_stream = nullptr; // only ever holds ev_probe (fetch_state)
     hipEvent_t ev_probe = nullptr;
     hipStream_t fetch_stream = nullptr; // stream the fetch in flight moves its bytes on
     int stage_next = 0;
@@ -1851,15 +1851,16 @@ int dpwa_learner_copy_fetched(dpwa_learner *l, void *dst_dev, dpwa_stream_t stre
 }
 
 // Milliseconds since the (completed, timing) event `since`, on the device's clock: an event
-// recorded now on the probe stream -- a stream of the greatest priority that holds nothing else --
-// and the two timestamps' difference.  DPWA_ERR_STATE when the probe does not complete within
-// kProbeWaitUs (the probe's hardware queue is held up: no measurement).
+// recorded now on the probe stream -- a stream that holds nothing else -- and the two timestamps'
+// difference.  DPWA_ERR_STATE when the probe does not complete within kProbeWaitUs (its hardware
+// queue is held up by another stream mapped to it: no measurement).  The probe stream has the
+// normal priority: the greatest-priority hardware queues are left to the rescue lanes (streams are
+// dealt round-robin onto a few queues per priority, so a probe there would push a lane onto a
+// queue another lane already uses).
 static int probe_since(dpwa_learner *l, hipEvent_t since, float *ms)
 {
     if (!l->probe_stream) {
-        int least = 0, greatest = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(hipStreamCreateWithPriority(&l->probe_stream, hipStreamNonBlocking, greatest));
+        HIP_TRY(hipStreamCreateWithFlags(&l->probe_stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreate(&l->ev_probe));
     }
     HIP_TRY(hipEventRecord(l->ev_probe, l->probe_stream));
