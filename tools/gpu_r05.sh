@@ -24,10 +24,10 @@ for step in "$@"; do
     bench)
       timeout -k 10 900 python -u bench.py $arg > "$out/bench_$i.json" 2> "$out/bench_$i.err" || { echo "bench failed" >&2; tail -40 "$out/bench_$i.err" >&2; exit 1; } ;;
     rocprof)
-      (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$out/rocprof_$i" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" $arg > "$GRAFT_REPO_ROOT/$out/rocprof_bench_$i.json" 2> "$GRAFT_REPO_ROOT/$out/rocprof_bench_$i.err") || { echo "rocprof failed" >&2; tail -40 "$out/rocprof_bench_$i.err" >&2; exit 1; } ;;
+      (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$out/rocprof_$i" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" $arg > "$GRAFT_REPO_ROOT/$out/rocprof_bench_$i.json" 2> "$GRAFT_REPO_ROOT/$out/rocprof_bench_$i.err") || { echo "rocprof failed" >&2; tail -40 "$out/rocprof_bench_$i.err" >&2; exit 1; } ;;
     pmc)
       for ctr in FETCH_SIZE WRITE_SIZE; do
-        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace -d "$GRAFT_REPO_ROOT/$out/pmc_${i}_$ctr" -o run -- python3 "$GRAFT_REPO_ROOT/tools/cold_sweep.py" $arg > "$GRAFT_REPO_ROOT/$out/pmc_${i}_$ctr.log" 2>&1) || { echo "pmc $ctr failed" >&2; tail -20 "$out/pmc_${i}_$ctr.log" >&2; exit 1; }
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$out/pmc_${i}_$ctr" -o run -- python3 "$GRAFT_REPO_ROOT/tools/cold_sweep.py" $arg > "$GRAFT_REPO_ROOT/$out/pmc_${i}_$ctr.log" 2>&1) || { echo "pmc $ctr failed" >&2; tail -20 "$out/pmc_${i}_$ctr.log" >&2; exit 1; }
       done ;;
     rehearse)
       n=${arg%% *}; rest=${arg#"$n"}
