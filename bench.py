@@ -1168,6 +1168,44 @@ def cold_rounds(device, cfg_dir, numel, dtype, steps, warmup=2, publish="write-t
                      "HBM" % (K, (K - 1) * per / 1e9)}
 
 
+def adapter_loop(device, cfg_dir, numel, dtype, steps, warmup=5):
+    """The drop-in itself: DpwaPyTorchAdapter (pytorch.py:37-68's API) over a model holding one
+    parameter of `numel` elements, configs[1]'s self-peer YAML, the adapter's defaults
+    (write-through, reuse guard on) -- update_send, update_wait per round, no training step -- and
+    the same with reuse_guard=False.  What the connection-level line costs through the adapter:
+    its host work per call and, with the guard, the two small kernels per update_send that check
+    sampled words of the parameters against the snapshot the average wrote."""
+    from dpwa_amd import DpwaPyTorchAdapter
+    from dpwa_amd.group import LocalGroup
+    esize = 4 if dtype == torch.float32 else 2
+    out = {}
+    for key, guard in (("default", True), ("no_guard", False)):
+        cfg = os.path.join(cfg_dir, "adapter_%s.yaml" % key)
+        write_config(cfg, ["a1"], "constant", self_peer=True, base_port=45400 + guard)
+        net = torch.nn.Module()
+        g = torch.Generator(device=device).manual_seed(0)
+        net.register_parameter("w", torch.nn.Parameter(torch.randn(numel, device=device, generator=g).to(dtype)))
+        ad = DpwaPyTorchAdapter(net, "a1", cfg, seed=3000, group=LocalGroup(), reuse_guard=guard)
+        for _ in range(warmup):
+            ad.update_send(1.0)
+            ad.update_wait(1.0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ad.update_send(1.0)
+            ad.update_wait(1.0)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        out[key] = {"value": round(steps * 3 * numel * esize / el / 1e9, 2), "ms_per_step": round(1e3 * el / steps, 4),
+                    "reuse_guard": guard, "guard_hits": ad.reuse_guard_hits}
+        ad.connection.close()
+        del ad, net
+        torch.cuda.empty_cache()
+    out["note"] = ("DpwaPyTorchAdapter(net, name, config) over one %d-element parameter, self-peer config, "
+                   "update_send -> update_wait, %d steps; value = 3*N*s per averaging / wall time" % (numel, steps))
+    return out
+
+
 def co_resident_pair(device, cfg_dir, numel, dtype, steps, warmup=5, cold=True):
     """Round 4's N=1 line, kept as an extra: two resident learners co-resident on one GPU that
     average with each other (each the other's only peer), both averages in one dispatch
@@ -1833,7 +1871,10 @@ def main(argv=None):
         wd.enter("value_cold", 600.0)
         value_cold = cold_rounds(device, tmp, args.numel, dtype, args.steps, publish=form)
     pair = None
+    adapter = None
     if world == 1 and not args.no_secondary:
+        wd.enter("adapter loop", 600.0)
+        adapter = adapter_loop(device, tmp, args.numel, dtype, args.steps, warmup=args.warmup)
         wd.enter("co-resident pair", 600.0)
         pair = co_resident_pair(device, tmp, args.numel, dtype, args.steps, warmup=args.warmup, cold=not args.no_cold)
 
@@ -1989,6 +2030,8 @@ def main(argv=None):
             out["roofline"]["vs_mix_ceiling"] = dict(MIX_CEILING_11M, kernel_frac_over_ceiling=round(
                 achieved / HBM_PEAK_GBS / MIX_CEILING_11M["frac"], 4),
                 note="the chip's cold ceiling for one 11.17M-element 2R:2W launch")
+        if adapter is not None:
+            out["adapter_loop"] = adapter
         if pair is not None:
             out["co_resident_pair"] = pair
         if publish_fallback:

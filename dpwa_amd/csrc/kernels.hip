@@ -1287,22 +1287,35 @@ hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *c
 // sees the same verdict: one workgroup compares and writes *dirty (and counts it in *hits), the
 // copy's workgroups return at once when it is clear.
 constexpr int kGuardSamples = 4096;
+// One workgroup of 1,024 lanes, kGuardPer samples each, every load issued before any compare: the
+// check costs one memory latency, not one per sample (it sits between the average and the peers'
+// reads of the snapshot on the stream, once per round).
+constexpr int kGuardBlock = 1024;
+constexpr int kGuardPer = kGuardSamples / kGuardBlock;
 
 template <bool VEC>
-__global__ __launch_bounds__(kBlock) void k_guard_compare(const char *__restrict__ flat,
-                                                          const char *__restrict__ payload, int64_t nbytes,
-                                                          int32_t *__restrict__ dirty, uint32_t *__restrict__ hits)
+__global__ __launch_bounds__(kGuardBlock) void k_guard_compare(const char *__restrict__ flat,
+                                                               const char *__restrict__ payload, int64_t nbytes,
+                                                               int32_t *__restrict__ dirty, uint32_t *__restrict__ hits)
 {
     const int64_t n16 = nbytes >> 4;
     const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
     int diff = 0;
-    for (int64_t k = threadIdx.x; k < samples; k += kBlock) {
-        const int64_t o = (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4;   // 0 .. n16-1
-        if (VEC) {
-            const u32x4 a = *reinterpret_cast<const u32x4 *>(flat + o);
-            const u32x4 b = *reinterpret_cast<const u32x4 *>(payload + o);
-            diff |= (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
-        } else {
+    if (VEC && samples > 0) {
+        u32x4 a[kGuardPer], b[kGuardPer];
+#pragma unroll
+        for (int i = 0; i < kGuardPer; ++i) {
+            const int64_t k = threadIdx.x + (int64_t)i * kGuardBlock;
+            const int64_t o = k < samples ? (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4 : 0;   // 0 .. n16-1
+            a[i] = *reinterpret_cast<const u32x4 *>(flat + o);
+            b[i] = *reinterpret_cast<const u32x4 *>(payload + o);
+        }
+#pragma unroll
+        for (int i = 0; i < kGuardPer; ++i)
+            diff |= (a[i].x != b[i].x) | (a[i].y != b[i].y) | (a[i].z != b[i].z) | (a[i].w != b[i].w);
+    } else if (!VEC) {
+        for (int64_t k = threadIdx.x; k < samples; k += kGuardBlock) {
+            const int64_t o = (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4;
             for (int j = 0; j < 16; ++j) diff |= flat[o + j] != payload[o + j];
         }
     }
@@ -1340,12 +1353,12 @@ hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes,
     if (aligned16(flat) && aligned16(payload)) {
         int64_t g = ((nbytes >> 4) + kBlock * 4 - 1) / (kBlock * 4);
         g = g < 1 ? 1 : g > 2048 ? 2048 : g;
-        hipLaunchKernelGGL(k_guard_compare<true>, dim3(1), dim3(kBlock), 0, s, src, payload, nbytes, dirty, hits);
+        hipLaunchKernelGGL(k_guard_compare<true>, dim3(1), dim3(kGuardBlock), 0, s, src, payload, nbytes, dirty, hits);
         hipLaunchKernelGGL(k_copy_if<true>, dim3((uint32_t)g), dim3(kBlock), 0, s, payload, src, nbytes, dirty);
     } else {
         int64_t g = blocks_for(nbytes);
         g = g > 2048 ? 2048 : g;
-        hipLaunchKernelGGL(k_guard_compare<false>, dim3(1), dim3(kBlock), 0, s, src, payload, nbytes, dirty, hits);
+        hipLaunchKernelGGL(k_guard_compare<false>, dim3(1), dim3(kGuardBlock), 0, s, src, payload, nbytes, dirty, hits);
         hipLaunchKernelGGL(k_copy_if<false>, dim3((uint32_t)g), dim3(kBlock), 0, s, payload, src, nbytes, dirty);
     }
     return hipGetLastError();
