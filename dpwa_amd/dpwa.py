@@ -206,6 +206,7 @@ class DpwaConnection:
                 self._peer_node_index.append(i)
         self.me   # AttributeError for a name that is not in the config, as the reference
         self._peer_index = {p.name: k for k, p in enumerate(self.peers)}
+        self._peer_wiring = [(0, None)] * len(self.peers)     # (DPWA_NODE_PEER_*, serving node) per peer
 
         # Interpolation method (dpwa.py:75-80)
         interpolation_method, interpolation_config = self.config.get_interpolation()
@@ -515,6 +516,7 @@ class DpwaConnection:
 
     def _set_peer(self, k, kind, other):
         _lib.call("dpwa_node_set_peer", self._node, k, kind, other._node if other is not None else None)
+        self._peer_wiring[k] = (kind, other.name if other is not None else None)
 
     def _info(self):
         fetching, peer, att = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

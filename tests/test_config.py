@@ -182,3 +182,33 @@ def test_pull_modes_are_validated_before_binding(tmp_path):
     for bad in ("rccl", "relay_avg", "push:32", ""):
         with pytest.raises(ValueError, match="relay-avg"):
             conn.set_pull(bad)
+
+
+def test_local_group_reaches_peers_by_address(tmp_path):
+    """LocalGroup wires a peer entry to the learner that serves its address, as the reference's
+    TxThread reaches whatever RxThread listens at (host, port) (conn.py:246-251): the self-peer
+    (a node entry at the learner's own address), an alias of another learner, a name match, and a
+    node nobody serves (refused); wiring follows learners joining and leaving."""
+    from dpwa_amd import DpwaConnection, _lib
+    from dpwa_amd.group import LocalGroup
+    cfg = tmp_path / "alias.yaml"
+    cfg.write_text("- nodes:\n"
+                   "  - {name: a, host: localhost, port: 46100}\n"
+                   "  - {name: b, host: 127.0.0.1, port: 46101}\n"
+                   "  - {name: a-self, host: 127.0.0.1, port: 46100}\n"
+                   "  - {name: ghost, host: localhost, port: 46199}\n"
+                   "- fetch_probability: 1\n- timeout_ms: 2500\n- interpolation: constant\n"
+                   "- divergence_threshold: 0\n- constant: { value: 0.5 }\n- clock: 0\n- loss: 0\n")
+    group = LocalGroup()
+    a = DpwaConnection("a", str(cfg), seed=1, group=group)
+    L, U = _lib.NODE_PEER_LOCAL, _lib.NODE_PEER_UNSET
+    # a's peers: b (not there yet), a-self (a itself), ghost (nobody)
+    assert [p.name for p in a.peers] == ["b", "a-self", "ghost"]
+    assert a._peer_wiring == [(U, None), (L, "a"), (U, None)]
+    b = DpwaConnection("b", str(cfg), seed=2, group=group)
+    assert a._peer_wiring == [(L, "b"), (L, "a"), (U, None)]
+    # b's peers: a, a-self (a's address: a), ghost
+    assert b._peer_wiring == [(L, "a"), (L, "a"), (U, None)]
+    a.close()
+    assert b._peer_wiring == [(U, None), (U, None), (U, None)]
+    b.close()
