@@ -181,3 +181,52 @@ def test_configs1_self_peer_full_size_reference_order(tmp_path):
     olerp.c_lerp_f32_(host, snap, 0.5)
     assert olerp.bits_equal(flat.cpu().numpy(), host)
     conn.close()
+
+
+@pytest.mark.parametrize("form", ["bf16-write-through", "f32-resident", "bf16-resident"])
+def test_self_peer_other_forms_match_oracle(tmp_path, form):
+    """The self-peer in bf16 (torch-eager two-rounding lerp) with write-through rounds in the
+    reference order, and with resident parameters (the published slot is both the parameters and
+    the peer; the step after update_wait, as a resident loop runs) -- 12 rounds, clock
+    interpolation, fetch_probability 0.7 (rounds without an average publish in full / relocate),
+    ragged size, against oracle/gossip.py with the self-peer node list."""
+    from tests.test_gpu_kernels import from_u16, to_u16
+    bf16 = form.startswith("bf16")
+    resident = form.endswith("resident")
+    rng = np.random.default_rng(43)
+    n, T = 100_003, 12
+    init32 = rng.standard_normal((1, n)).astype(np.float32)
+    d32 = (0.01 * rng.standard_normal((T, 1, n))).astype(np.float32)
+    if bf16:
+        init, deltas = olerp.f32_to_bf16(init32), olerp.f32_to_bf16(d32)
+        to_dev, to_host, kw = from_u16, to_u16, dict(lerp=olerp.lerp_bf16, add=ogossip.add_bf16)
+    else:
+        init, deltas = init32, d32
+        to_dev, to_host, kw = (lambda a: torch.from_numpy(a).to(DEV)), (lambda t: t.cpu().numpy()), {}
+    send = [[1.0 + 0.1 * r] for r in range(T)]
+    wait = [[0.9 + 0.1 * r] for r in range(T)]
+    exp = ogossip.simulate(["w1"], init, deltas, send, wait, "clock", None, 0.0, 0.7, [19], train_after_wait=resident,
+                           nodes=["w1", "w1-self"], serves={"w1-self": 0}, **kw)
+    cfg = tmp_path / ("%s.yaml" % form)
+    write_self_cfg(cfg, 0.7, "clock", 0.0, None)
+    conn = DpwaConnection("w1", str(cfg), seed=19, group=LocalGroup())
+    flat = to_dev(init[0].copy())
+    if resident:
+        conn.make_resident(flat)
+        for r in range(T):
+            conn.update_send(conn.parameters, send[r][0])
+            conn.update_wait_average(conn.parameters, wait[r][0])
+            assert conn.clock == exp["clocks"][r, 0], r
+            assert np.array_equal(to_host(conn.parameters).view(np.uint32 if not bf16 else np.uint16),
+                                  exp["params"][r, 0].view(np.uint32 if not bf16 else np.uint16)), r
+            conn.parameters.add_(to_dev(deltas[r, 0]))                  # the step, after update_wait
+    else:
+        reuse = False
+        for r in range(T):
+            conn.update_send(flat, send[r][0], reuse_snapshot=reuse)
+            flat.add_(to_dev(deltas[r, 0]))                             # the step, between the two
+            payload, _ = conn.update_wait_average(flat, wait[r][0], write_through=True)
+            reuse = payload is not None
+            assert conn.clock == exp["clocks"][r, 0], r
+            assert np.array_equal(to_host(flat).view(np.uint16), exp["params"][r, 0].view(np.uint16)), r
+    conn.close()
