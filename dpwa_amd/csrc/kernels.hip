@@ -1284,54 +1284,50 @@ hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *c
 // published as is, kGuardSamples 16-B words spread evenly over the parameters (first and last
 // included) and their tail bytes are compared with it.  Any difference makes the publish a full
 // one: the payload is copied from the parameters.  Two launches, so every workgroup of the copy
-// sees the same verdict: one workgroup compares and writes *dirty (and counts it in *hits), the
-// copy's workgroups return at once when it is clear.
+// sees the same verdict.  The compare runs one sample per lane over kGuardSamples / 64 one-wave
+// workgroups -- spread over as many CUs, each sample one memory latency -- and a workgroup that
+// finds a difference stamps the verdict word with this publish's generation `gen` (a word that
+// never needs clearing; the first stamp of a generation counts a hit).  The copy's workgroups, one
+// per CU, return at once unless the word carries `gen`.  (Round 4's single-workgroup compare,
+// 4,096 dependent-latency loads on one CU, cost ~19 us per update_send: bench `adapter_loop`.)
 constexpr int kGuardSamples = 4096;
-// One workgroup of 1,024 lanes, kGuardPer samples each, every load issued before any compare: the
-// check costs one memory latency, not one per sample (it sits between the average and the peers'
-// reads of the snapshot on the stream, once per round).
-constexpr int kGuardBlock = 1024;
-constexpr int kGuardPer = kGuardSamples / kGuardBlock;
+constexpr int kGuardWave = 64;
+constexpr int kGuardCopyBlocks = 256;
 
 template <bool VEC>
-__global__ __launch_bounds__(kGuardBlock) void k_guard_compare(const char *__restrict__ flat,
-                                                               const char *__restrict__ payload, int64_t nbytes,
-                                                               int32_t *__restrict__ dirty, uint32_t *__restrict__ hits)
+__global__ __launch_bounds__(kGuardWave) void k_guard_compare(const char *__restrict__ flat,
+                                                              const char *__restrict__ payload, int64_t nbytes,
+                                                              int32_t *__restrict__ dirty, uint32_t *__restrict__ hits,
+                                                              int32_t gen)
 {
     const int64_t n16 = nbytes >> 4;
     const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
+    const int64_t k = (int64_t)blockIdx.x * kGuardWave + threadIdx.x;
     int diff = 0;
-    if (VEC && samples > 0) {
-        u32x4 a[kGuardPer], b[kGuardPer];
-#pragma unroll
-        for (int i = 0; i < kGuardPer; ++i) {
-            const int64_t k = threadIdx.x + (int64_t)i * kGuardBlock;
-            const int64_t o = k < samples ? (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4 : 0;   // 0 .. n16-1
-            a[i] = *reinterpret_cast<const u32x4 *>(flat + o);
-            b[i] = *reinterpret_cast<const u32x4 *>(payload + o);
-        }
-#pragma unroll
-        for (int i = 0; i < kGuardPer; ++i)
-            diff |= (a[i].x != b[i].x) | (a[i].y != b[i].y) | (a[i].z != b[i].z) | (a[i].w != b[i].w);
-    } else if (!VEC) {
-        for (int64_t k = threadIdx.x; k < samples; k += kGuardBlock) {
-            const int64_t o = (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4;
+    if (k < samples) {
+        const int64_t o = (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4;   // 0 .. n16-1
+        if (VEC) {
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(flat + o);
+            const u32x4 b = *reinterpret_cast<const u32x4 *>(payload + o);
+            diff = (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
+        } else {
             for (int j = 0; j < 16; ++j) diff |= flat[o + j] != payload[o + j];
         }
     }
-    if (threadIdx.x < (nbytes & 15)) diff |= flat[(n16 << 4) + threadIdx.x] != payload[(n16 << 4) + threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x < (nbytes & 15))
+        diff |= flat[(n16 << 4) + threadIdx.x] != payload[(n16 << 4) + threadIdx.x];
     diff = __syncthreads_or(diff);
-    if (threadIdx.x == 0) {
-        *dirty = diff;
-        if (diff) *hits += 1;
+    if (diff && threadIdx.x == 0) {
+        const int32_t old = atomicExch(dirty, gen);
+        if (old != gen) atomicAdd(hits, 1u);
     }
 }
 
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_copy_if(char *__restrict__ dst, const char *__restrict__ src,
-                                                    int64_t nbytes, const int32_t *__restrict__ dirty)
+                                                    int64_t nbytes, const int32_t *__restrict__ dirty, int32_t gen)
 {
-    if (*dirty == 0) return;
+    if (*dirty != gen) return;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     const int64_t first = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (VEC) {
@@ -1346,20 +1342,23 @@ __global__ __launch_bounds__(kBlock) void k_copy_if(char *__restrict__ dst, cons
 }
 
 hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes, int32_t *dirty, uint32_t *hits,
-                                hipStream_t s)
+                                int32_t gen, hipStream_t s)
 {
     if (nbytes <= 0) return hipSuccess;
     const char *src = (const char *)flat;
+    const int64_t n16 = nbytes >> 4;
+    const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
+    const uint32_t gc = (uint32_t)((samples + kGuardWave - 1) / kGuardWave + (samples == 0 ? 1 : 0));
     if (aligned16(flat) && aligned16(payload)) {
-        int64_t g = ((nbytes >> 4) + kBlock * 4 - 1) / (kBlock * 4);
-        g = g < 1 ? 1 : g > 2048 ? 2048 : g;
-        hipLaunchKernelGGL(k_guard_compare<true>, dim3(1), dim3(kGuardBlock), 0, s, src, payload, nbytes, dirty, hits);
-        hipLaunchKernelGGL(k_copy_if<true>, dim3((uint32_t)g), dim3(kBlock), 0, s, payload, src, nbytes, dirty);
+        hipLaunchKernelGGL(k_guard_compare<true>, dim3(gc), dim3(kGuardWave), 0, s, src, payload, nbytes, dirty, hits,
+                           gen);
+        hipLaunchKernelGGL(k_copy_if<true>, dim3(kGuardCopyBlocks), dim3(kBlock), 0, s, payload, src, nbytes, dirty,
+                           gen);
     } else {
-        int64_t g = blocks_for(nbytes);
-        g = g > 2048 ? 2048 : g;
-        hipLaunchKernelGGL(k_guard_compare<false>, dim3(1), dim3(kGuardBlock), 0, s, src, payload, nbytes, dirty, hits);
-        hipLaunchKernelGGL(k_copy_if<false>, dim3((uint32_t)g), dim3(kBlock), 0, s, payload, src, nbytes, dirty);
+        hipLaunchKernelGGL(k_guard_compare<false>, dim3(gc), dim3(kGuardWave), 0, s, src, payload, nbytes, dirty, hits,
+                           gen);
+        hipLaunchKernelGGL(k_copy_if<false>, dim3(kGuardCopyBlocks), dim3(kBlock), 0, s, payload, src, nbytes, dirty,
+                           gen);
     }
     return hipGetLastError();
 }

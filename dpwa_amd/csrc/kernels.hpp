@@ -129,7 +129,7 @@ hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *c
 // the last average wrote; on a difference the payload is copied from `flat` and *hits += 1
 // (*dirty: the verdict, device memory; both written by the device).
 hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes, int32_t *dirty, uint32_t *hits,
-                                hipStream_t s);
+                                int32_t gen, hipStream_t s);
 
 // A system-scope L2 write-back on every XCD after the work already on `s` (a publish whose
 // bytes were written by an earlier kernel, read by other devices).

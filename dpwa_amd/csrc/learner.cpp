@@ -251,7 +251,8 @@ struct Ctl {            // device control block
                         // write-through average also writes the next publish's clock+1 into
                         // clock[cur+2], which that publish then selects without a kernel
     dpwa_coef coef;
-    int32_t guard_dirty;   // reuse guard: the last header-only publish found the parameters changed
+    int32_t guard_dirty;   // reuse guard: the generation (publish number) of the last publish that found
+                           // the parameters changed (kernels.hip k_guard_compare)
     uint32_t guard_hits;   // ... and how many publishes did
 };
 
@@ -686,7 +687,7 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
         }
         if (l->reuse_guard && !l->resident)
             HIP_TRY(launch_guard_payload(slot + kPayloadOff, flat, (int64_t)l->payload_bytes, &l->ctl->guard_dirty,
-                                         &l->ctl->guard_hits, s));
+                                         &l->ctl->guard_hits, (int32_t)(l->version + 1), s));
         if (l->exported) HIP_TRY(launch_release_system(s));
         l->cur = (l->cur + 1) & 3;
     } else if (header_only) {
@@ -697,7 +698,7 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
         }
         if (l->reuse_guard && !l->resident)
             HIP_TRY(launch_guard_payload(slot + kPayloadOff, flat, (int64_t)l->payload_bytes, &l->ctl->guard_dirty,
-                                         &l->ctl->guard_hits, s));
+                                         &l->ctl->guard_hits, (int32_t)(l->version + 1), s));
         HIP_TRY(launch_publish_header(slot, l->n, l->dtype, &l->ctl->clock[l->cur], loss, loss_dev, l->loss_f32,
                                       l->version + 1, l->exported, s));
     } else {
