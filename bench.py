@@ -1150,7 +1150,7 @@ def cold_rounds(device, cfg_dir, numel, dtype, steps, warmup=2, publish="write-t
 
     for i in range(warmup * K):
         step(i)
-    n = max(steps, 4 * K)
+    n = max(steps, 20 * K)          # every learner set at least 20 times
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     averaged = sum(step(i) for i in range(n))
