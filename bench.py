@@ -2014,6 +2014,8 @@ def main(argv=None):
                 "frac_moved_bytes_cold": round(achieved / HBM_PEAK_GBS, 4),
                 "scaling_raw_rounds_per_s": sb["raw"]["gossip_rounds_per_s"],
                 "scaling_weak_rounds_per_s": sb["weak"]["gossip_rounds_per_s"],
+                "adapter_loop_value": adapter["default"]["value"] if adapter else None,
+                "co_resident_pair_value": pair["value"] if pair else None,
                 "parallelism": "gossip x%d" % int(rounds / args.steps),
                 "streams": args.streams,
             },
