@@ -640,9 +640,19 @@ static hipError_t launch_mode(void *param, const void *peer, int64_t n, const Le
             case 40: return launch_blocks<Ops, MODE, DUAL, 64, 40>(param, peer, n, args, s, timing);
             default: return launch_blocks<Ops, MODE, DUAL, 64>(param, peer, n, args, s, timing);
             }
-        case 128: return launch_blocks<Ops, MODE, DUAL, 128>(param, peer, n, args, s, timing);
-        case 512: return launch_blocks<Ops, MODE, DUAL, 512>(param, peer, n, args, s, timing);
-        default: return launch_blocks<Ops, MODE, DUAL, 256>(param, peer, n, args, s, timing);
+        // (tuning sizes: the product policy, or policy 0 when DPWA_LERP_POLICY says so)
+        case 128:
+            return lerp_policy() == kProductPolicy
+                       ? launch_blocks<Ops, MODE, DUAL, 128, kProductPolicy>(param, peer, n, args, s, timing)
+                       : launch_blocks<Ops, MODE, DUAL, 128>(param, peer, n, args, s, timing);
+        case 512:
+            return lerp_policy() == kProductPolicy
+                       ? launch_blocks<Ops, MODE, DUAL, 512, kProductPolicy>(param, peer, n, args, s, timing)
+                       : launch_blocks<Ops, MODE, DUAL, 512>(param, peer, n, args, s, timing);
+        default:
+            return lerp_policy() == kProductPolicy
+                       ? launch_blocks<Ops, MODE, DUAL, 256, kProductPolicy>(param, peer, n, args, s, timing)
+                       : launch_blocks<Ops, MODE, DUAL, 256>(param, peer, n, args, s, timing);
         }
     } else {
         // (callers time only the aligned product kernel; an unaligned launch is not timed)
