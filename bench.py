@@ -1132,7 +1132,9 @@ def cold_rounds(device, cfg_dir, numel, dtype, steps, warmup=2, publish="write-t
     from dpwa_amd.group import LocalGroup
     esize = 4 if dtype == torch.float32 else 2
     per = 3 * numel * esize         # what one round touches: parameters, published slot, next slot
-    K = 1 if per >= min_bytes else max(2, int(np.ceil(min_bytes / per)) + 1)
+    # (at most 32 learners -- a stream and events each; small vectors then rotate less than
+    # min_bytes, and bytes_between_reuses says how much)
+    K = 1 if per >= min_bytes else min(32, max(2, int(np.ceil(min_bytes / per)) + 1))
     wt = publish == "write-through"
     conns, flats = [], []
     for k in range(K):
