@@ -981,6 +981,51 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
             "mutual_pair": pair}
 
 
+def mix_ceiling(numel, dtype, device, nr=2, nw=2, launches=64):
+    """The timed kernel's access mix alone (dpwa_stream_mix: nr loads and nw stores per 16-B item,
+    the product kernel's launch shape and cache policy, no factor and no lerp), cold over rotating
+    buffers exactly as cold_kernel times the product kernel: the ceiling that launch shape reaches
+    at this size on this chip, measured in the same run."""
+    from dpwa_amd import _lib
+    esize = 4 if dtype == torch.float32 else 2
+    nbytes = (numel * esize) // 16 * 16
+    per_set = (nr + nw) * nbytes
+    sets = 1 if per_set >= 1.2e9 else max(2, int(np.ceil(1.2e9 / per_set)))
+    launches = max(2 * sets, 4, min(launches, int(np.ceil(64 * 134e6 / per_set))))
+    bufs = [[torch.empty(nbytes // 4, dtype=torch.int32, device=device).random_() for _ in range(nr + nw)]
+            for _ in range(sets)]
+    ptrs = [((ctypes.c_void_p * 2)(*[b.data_ptr() for b in bs[nr:]]),
+             (ctypes.c_void_p * 2)(*[b.data_ptr() for b in bs[:nr]])) for bs in bufs]
+    lib = _lib.load()
+    s = _lib.stream_handle(None)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    for a, b in ev:
+        a.record()
+        b.record()
+
+    def run(i, timed):
+        dst, src = ptrs[i % sets]
+        ea, eb = (ev[i][0].cuda_event, ev[i][1].cuda_event) if timed else (None, None)
+        rc = lib.dpwa_stream_mix(dst, nw, src, nr, nbytes, s, ea, eb)
+        if rc:
+            raise _lib.DpwaError("dpwa_stream_mix", rc, lib.dpwa_last_error().decode())
+
+    for i in range(sets):
+        run(i, False)
+    torch.cuda._sleep(50_000_000)
+    for i in range(launches):
+        run(i, True)
+    torch.cuda.synchronize()
+    us = np.array([a.elapsed_time(b) * 1e3 for a, b in ev])
+    del bufs, ptrs
+    torch.cuda.empty_cache()
+    gbs = per_set / (float(us.mean()) * 1e-6) / 1e9
+    return {"mix": "%dR:%dW" % (nr, nw), "bytes_per_launch": per_set, "avg_launch_us": round(float(us.mean()), 2),
+            "median_launch_us": round(float(np.median(us)), 2), "achieved": round(gbs, 1),
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "launches": launches, "rotating_buffer_sets": sets,
+            "kernel": "dpwa::k_stream_mix<%d, %d> (dpwa_stream_mix)" % (nr, nw)}
+
+
 def round_sweep(device, cfg_dir, steps=20, warmup=3, rows=None, publish="write-through", min_s=0.25):
     """Whole gossip rounds of the N=1 line's form at every north_star size in its config's dtype:
     one learner whose peer is its own snapshot (configs[1]'s self-peer), constant 0.5,
@@ -1902,9 +1947,12 @@ def main(argv=None):
     # the same kernel alone, cold (rotating buffers, per-launch dispatch events): the roofline's basis
     cold = None
     forms_cold = {}         # every single-learner form at the workload size, cold
+    mix = None
     if not args.no_cold:
         wd.enter("cold kernel", 300.0)
         cold = cold_kernel(args.numel, dtype, device, wt_kernel, learners=per_launch, resident=resident_main)
+        if per_launch == 1:      # the same access mix with nothing else in it, same rotation
+            mix = mix_ceiling(args.numel, dtype, device, nr=2, nw=2 if wt_kernel else 1)
         for key, wt_, res_ in (("write_through", True, False), ("full", False, False), ("resident", False, True)):
             same = per_launch == 1 and res_ == resident_main and wt_ == wt_kernel
             c = cold if same else cold_kernel(args.numel, dtype, device, wt_, learners=1, resident=res_)
@@ -2030,10 +2078,17 @@ def main(argv=None):
                               "note": "untimed rounds before the timed steps: W, then more up to about warmup_s "
                                       "seconds in all, so the timed steps run at steady-state clocks"},
         })
+        if mix is not None:
+            out["roofline"]["mix_ceiling_frac"] = mix["frac"]
+            out["roofline"]["kernel_over_mix_ceiling"] = round(achieved / mix["achieved"], 4)
+            out["roofline"]["mix_ceiling"] = dict(mix, note=(
+                "the timed kernel's access mix alone, same launch shape, cache policy and cold rotation, no "
+                "factor or lerp: what one launch of this size reaches on this chip (kernel_over_mix_ceiling = "
+                "the product kernel's rate over it)"))
         if wt_kernel and args.numel == RESNET18_NUMEL and args.dtype == "f32":
             out["roofline"]["vs_mix_ceiling"] = dict(MIX_CEILING_11M, kernel_frac_over_ceiling=round(
                 achieved / HBM_PEAK_GBS / MIX_CEILING_11M["frac"], 4),
-                note="the chip's cold ceiling for one 11.17M-element 2R:2W launch")
+                note="round 2's stream_tune ceiling for one 11.17M-element 2R:2W launch (mix_ceiling: this run's)")
         if adapter is not None:
             out["adapter_loop"] = adapter
         if pair is not None:

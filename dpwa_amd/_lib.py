@@ -98,6 +98,7 @@ SIGNATURES = {
     "dpwa_learner_relocate": [_vp, _vp],
     "dpwa_node_set_resident": [_vp, _vp, _vp],
     "dpwa_learner_fetch_state": [_vp, _i64, _pint],
+    "dpwa_stream_mix": [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp],
     "dpwa_learner_rescue_free": [_vp, _pint],
     "dpwa_learner_rescue_lanes": [_vp, _pint, _pint],
     "dpwa_learner_set_rescue_cap": [_vp, ctypes.c_int],

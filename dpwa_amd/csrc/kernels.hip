@@ -1373,6 +1373,47 @@ hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes,
     return hipGetLastError();
 }
 
+// The access mix of an averaging kernel with nothing else in it, for measurement only
+// (dpwa_stream_mix, bench.py `roofline.mix_ceiling`): each one-wave workgroup loads the same
+// 1-KiB span of NR source buffers and stores one combination of them into the span of NW
+// destinations, with exactly the product kernel's instruction shapes and cache policy
+// (16-B buffer loads `nt`; the first destination stored as the parameters are, the others as the
+// snapshot is) but no factor and no arithmetic beyond one add per word: the ceiling that launch
+// shape reaches on this chip at a given size, timed in the same run as the product kernel.
+template <int NR, int NW>
+__global__ __launch_bounds__(kStreamBlock) void k_stream_mix(StreamMixArgs a)
+{
+    constexpr int SPAN = kStreamBlock * 16;
+    const int64_t span_off = (int64_t)blockIdx.x * SPAN;
+    const int lane_off = threadIdx.x * 16;
+    u32x4 v[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+        v[i] = __builtin_amdgcn_raw_buffer_load_b128(span_rsrc<SPAN>(a.src[i], span_off, a.nbytes), lane_off, 0,
+                                                     kAuxStream);
+    u32x4 r = v[0];
+#pragma unroll
+    for (int i = 1; i < NR; ++i) r = r + v[i];
+    __builtin_amdgcn_raw_buffer_store_b128(r, span_rsrc<SPAN>(a.dst[0], span_off, a.nbytes), lane_off, 0,
+                                           LerpPolicy<kProductPolicy>::store);
+    if (NW > 1)
+        __builtin_amdgcn_raw_buffer_store_b128(r, span_rsrc<SPAN>(a.dst[1], span_off, a.nbytes), lane_off, 0,
+                                               LerpPolicy<kProductPolicy>::snap_store);
+}
+
+hipError_t launch_stream_mix(const StreamMixArgs &a, hipStream_t s, const LaunchTiming *timing)
+{
+    if (a.nr < 1 || a.nr > 2 || a.nw < 1 || a.nw > 2 || a.nbytes < 0 || (a.nbytes & 15)) return hipErrorInvalidValue;
+    const uint32_t g = (uint32_t)(a.nbytes / (kStreamBlock * 16) + 1);
+    void (*k)(StreamMixArgs) = a.nr == 1 ? (a.nw == 1 ? k_stream_mix<1, 1> : k_stream_mix<1, 2>)
+                                         : (a.nw == 1 ? k_stream_mix<2, 1> : k_stream_mix<2, 2>);
+    if (timing)
+        hipExtLaunchKernelGGL(k, dim3(g), dim3(kStreamBlock), 0, s, timing->start, timing->stop, 0, a);
+    else
+        hipLaunchKernelGGL(k, dim3(g), dim3(kStreamBlock), 0, s, a);
+    return hipGetLastError();
+}
+
 // One 64-bit word into (host-mapped) memory after everything before it on the stream: a
 // system-scope release store, so the bytes written before it are visible first.  Used by
 // the gossip board (board.cpp) for versions and read marks.

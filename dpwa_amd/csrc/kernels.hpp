@@ -128,6 +128,15 @@ hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *c
 // Reuse guard of a header-only publish: sampled words of `flat` against the snapshot `payload`
 // the last average wrote; on a difference the payload is copied from `flat` and *hits += 1
 // (*dirty: the verdict, device memory; both written by the device).
+// dpwa_stream_mix: the averaging kernels' access mix alone (measurement only).
+struct StreamMixArgs {
+    const char *src[2];
+    char *dst[2];
+    int64_t nbytes;   // a multiple of 16
+    int32_t nr, nw;
+};
+hipError_t launch_stream_mix(const StreamMixArgs &a, hipStream_t s, const LaunchTiming *timing);
+
 hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes, int32_t *dirty, uint32_t *hits,
                                 int32_t gen, hipStream_t s);
 

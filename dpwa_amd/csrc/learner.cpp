@@ -530,6 +530,27 @@ int dpwa_average(int32_t dtype, void *param, const void *peer_slot, int64_t n, c
     return DPWA_OK;
 }
 
+int dpwa_stream_mix(void *const *dst, int nw, const void *const *src, int nr, int64_t nbytes, dpwa_stream_t stream,
+                    void *start_event, void *stop_event)
+{
+    if (!dst || !src || nr < 1 || nr > 2 || nw < 1 || nw > 2 || nbytes < 0 || (nbytes & 15) ||
+        (!start_event) != (!stop_event))
+        return set_error(DPWA_ERR_ARG, "dpwa_stream_mix: bad arguments");
+    StreamMixArgs a{};
+    for (int i = 0; i < nr; ++i) a.src[i] = (const char *)src[i];
+    for (int j = 0; j < nw; ++j) a.dst[j] = (char *)dst[j];
+    for (int i = 0; i < nr; ++i)
+        if (!a.src[i] || ((uintptr_t)a.src[i] & 15)) return set_error(DPWA_ERR_ARG, "dpwa_stream_mix: source %d", i);
+    for (int j = 0; j < nw; ++j)
+        if (!a.dst[j] || ((uintptr_t)a.dst[j] & 15)) return set_error(DPWA_ERR_ARG, "dpwa_stream_mix: destination %d", j);
+    a.nbytes = nbytes;
+    a.nr = nr;
+    a.nw = nw;
+    LaunchTiming t{(hipEvent_t)start_event, (hipEvent_t)stop_event};
+    HIP_TRY(launch_stream_mix(a, (hipStream_t)stream, start_event ? &t : nullptr));
+    return DPWA_OK;
+}
+
 int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype, const dpwa_interp *cfg)
 {
     if (!out || n < 0 || !cfg || dtype_size(dtype) == 0) return set_error(DPWA_ERR_ARG, "dpwa_learner_create: bad arguments");

@@ -158,6 +158,15 @@ int dpwa_factor(const dpwa_interp *cfg, double *clock_dev, const dpwa_header *pe
 typedef struct dpwa_learner dpwa_learner;
 
 int dpwa_learner_create(dpwa_learner **out, int device, int64_t n, int32_t dtype, const dpwa_interp *cfg);
+
+/* Measurement only (bench.py `roofline.mix_ceiling`; no reference interface): the averaging
+ * kernels' access mix with nothing else in it -- every 1-KiB span of `nr` (1-2) source buffers
+ * loaded and one sum of them stored into `nw` (1-2) destinations, `nbytes` (a multiple of 16)
+ * each, with the product kernel's launch shape and cache policy.  nr = 2, nw = 2 is the
+ * write-through average's mix (read parameters and snapshot, write parameters and next
+ * snapshot).  start/stop: optional dispatch begin/end events. */
+int dpwa_stream_mix(void *const *dst, int nw, const void *const *src, int nr, int64_t nbytes, dpwa_stream_t stream,
+                    void *start_event, void *stop_event);
 int dpwa_learner_destroy(dpwa_learner *l);
 
 /* update_send's publish half (dpwa.py:111-116 + pytorch.py:49-53): clock += 1 on the device,
