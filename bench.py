@@ -882,7 +882,8 @@ def _async_verdict(t, names, world, rank, check, err, ctl):
 
 
 # ---------------------------------------------------------------- kernel measurements
-def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners=1, resident=False, pair=False):
+def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners=1, resident=False, pair=False,
+                mix=False):
     """The product averaging kernel alone over rotating buffers (> 1.2 GB of other traffic
     between two uses of a buffer, so nothing is served from the 256 MiB Infinity Cache).  With
     learners == 1 it is dpwa_average (k_lerp<Ops, COEF_FUSED, write_through>: fp64 device
@@ -895,7 +896,13 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
     (dpwa_average_many_resident): the parameters are read from one snapshot payload and the result
     stored into another, nothing written back in place (3*N*s).  `pair` (resident, 2 learners): the
     two learners average with each other, as the N=1 loop's do -- entry 0 reads A's slot and B's,
-    entry 1 B's and A's -- so the dispatch is a mutual pair (k_lerp_pair: 4*N*s)."""
+    entry 1 B's and A's -- so the dispatch is a mutual pair (k_lerp_pair: 4*N*s).
+    `mix` (one learner, in place): every product launch is followed by one of its access mix alone
+    (dpwa_stream_mix: the same loads and stores, same addresses -- the parameters and the peer
+    payload read, the parameters and the snapshot written -- same launch shape and cache policy,
+    no factor, no lerp) over another set of the same rotation, each timed by its own dispatch
+    events: the ceiling of that mix measured interleaved with the product kernel, on its buffers,
+    returned under "mix"."""
     from dpwa_amd import _lib
     esize = 4 if dtype == torch.float32 else 2
     write_through = write_through or resident
@@ -962,6 +969,26 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
         if rc:
             raise _lib.DpwaError(name, rc, lib.dpwa_last_error().decode())
 
+    mix = mix and learners == 1 and not resident
+    nbytes = numel * esize // 16 * 16
+    if mix:
+        evm = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+        for a, b in evm:
+            a.record()
+            b.record()
+        mix_ptrs = []
+        for entries in bufs:
+            param, slot, snap = entries[0]
+            dst = [param.data_ptr()] + ([snap.data_ptr()] if snap is not None else [])
+            mix_ptrs.append(((ctypes.c_void_p * 2)(*dst), (ctypes.c_void_p * 2)(slot[hdr:].data_ptr(), param.data_ptr()),
+                             len(dst)))
+
+    def run_mix(i):
+        dst, src, nw = mix_ptrs[(i + sets // 2) % sets]     # half a rotation away from the product launch
+        rc = lib.dpwa_stream_mix(dst, nw, src, 2, nbytes, s, evm[i][0].cuda_event, evm[i][1].cuda_event)
+        if rc:
+            raise _lib.DpwaError("dpwa_stream_mix", rc, lib.dpwa_last_error().decode())
+
     for i in range(sets):
         run(i, False)
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -969,61 +996,28 @@ def cold_kernel(numel, dtype, device, write_through=False, launches=64, learners
     t0.record()
     for i in range(launches):
         run(i, True)
+        if mix:
+            run_mix(i)
     t1.record()
     torch.cuda.synchronize()
     us = np.array([a.elapsed_time(b) * 1e3 for a, b in ev])
     batch_us = t0.elapsed_time(t1) * 1e3 / launches
+    out = {"avg_launch_us": float(us.mean()), "median_launch_us": float(np.median(us)),
+           "min_launch_us": float(us.min()), "max_launch_us": float(us.max()), "launches": launches,
+           "rotating_buffer_sets": sets, "learners_per_launch": learners, "batch_bracket_us": float(batch_us),
+           "mutual_pair": pair}
+    if mix:
+        um = np.array([a.elapsed_time(b) * 1e3 for a, b in evm])
+        nw = mix_ptrs[0][2]
+        moved = (2 + nw) * nbytes
+        gbs = moved / (float(um.mean()) * 1e-6) / 1e9
+        out["mix"] = {"mix": "2R:%dW" % nw, "bytes_per_launch": moved, "avg_launch_us": round(float(um.mean()), 2),
+                      "median_launch_us": round(float(np.median(um)), 2), "achieved": round(gbs, 1),
+                      "frac": round(gbs / HBM_PEAK_GBS, 4), "launches": launches, "rotating_buffer_sets": sets,
+                      "interleaved": True, "kernel": "dpwa::k_stream_mix<2, %d> (dpwa_stream_mix)" % nw}
     del bufs, descs
     torch.cuda.empty_cache()
-    return {"avg_launch_us": float(us.mean()), "median_launch_us": float(np.median(us)),
-            "min_launch_us": float(us.min()), "max_launch_us": float(us.max()), "launches": launches,
-            "rotating_buffer_sets": sets, "learners_per_launch": learners, "batch_bracket_us": float(batch_us),
-            "mutual_pair": pair}
-
-
-def mix_ceiling(numel, dtype, device, nr=2, nw=2, launches=64):
-    """The timed kernel's access mix alone (dpwa_stream_mix: nr loads and nw stores per 16-B item,
-    the product kernel's launch shape and cache policy, no factor and no lerp), cold over rotating
-    buffers exactly as cold_kernel times the product kernel: the ceiling that launch shape reaches
-    at this size on this chip, measured in the same run."""
-    from dpwa_amd import _lib
-    esize = 4 if dtype == torch.float32 else 2
-    nbytes = (numel * esize) // 16 * 16
-    per_set = (nr + nw) * nbytes
-    sets = 1 if per_set >= 1.2e9 else max(2, int(np.ceil(1.2e9 / per_set)))
-    launches = max(2 * sets, 4, min(launches, int(np.ceil(64 * 134e6 / per_set))))
-    bufs = [[torch.empty(nbytes // 4, dtype=torch.int32, device=device).random_() for _ in range(nr + nw)]
-            for _ in range(sets)]
-    ptrs = [((ctypes.c_void_p * 2)(*[b.data_ptr() for b in bs[nr:]]),
-             (ctypes.c_void_p * 2)(*[b.data_ptr() for b in bs[:nr]])) for bs in bufs]
-    lib = _lib.load()
-    s = _lib.stream_handle(None)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
-    for a, b in ev:
-        a.record()
-        b.record()
-
-    def run(i, timed):
-        dst, src = ptrs[i % sets]
-        ea, eb = (ev[i][0].cuda_event, ev[i][1].cuda_event) if timed else (None, None)
-        rc = lib.dpwa_stream_mix(dst, nw, src, nr, nbytes, s, ea, eb)
-        if rc:
-            raise _lib.DpwaError("dpwa_stream_mix", rc, lib.dpwa_last_error().decode())
-
-    for i in range(sets):
-        run(i, False)
-    torch.cuda._sleep(50_000_000)
-    for i in range(launches):
-        run(i, True)
-    torch.cuda.synchronize()
-    us = np.array([a.elapsed_time(b) * 1e3 for a, b in ev])
-    del bufs, ptrs
-    torch.cuda.empty_cache()
-    gbs = per_set / (float(us.mean()) * 1e-6) / 1e9
-    return {"mix": "%dR:%dW" % (nr, nw), "bytes_per_launch": per_set, "avg_launch_us": round(float(us.mean()), 2),
-            "median_launch_us": round(float(np.median(us)), 2), "achieved": round(gbs, 1),
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "launches": launches, "rotating_buffer_sets": sets,
-            "kernel": "dpwa::k_stream_mix<%d, %d> (dpwa_stream_mix)" % (nr, nw)}
+    return out
 
 
 def round_sweep(device, cfg_dir, steps=20, warmup=3, rows=None, publish="write-through", min_s=0.25):
@@ -1950,9 +1944,10 @@ def main(argv=None):
     mix = None
     if not args.no_cold:
         wd.enter("cold kernel", 300.0)
-        cold = cold_kernel(args.numel, dtype, device, wt_kernel, learners=per_launch, resident=resident_main)
-        if per_launch == 1:      # the same access mix with nothing else in it, same rotation
-            mix = mix_ceiling(args.numel, dtype, device, nr=2, nw=2 if wt_kernel else 1)
+        # one learner: each timed launch interleaved with its access mix alone on the same buffers
+        cold = cold_kernel(args.numel, dtype, device, wt_kernel, learners=per_launch, resident=resident_main,
+                           mix=per_launch == 1)
+        mix = cold.get("mix")
         for key, wt_, res_ in (("write_through", True, False), ("full", False, False), ("resident", False, True)):
             same = per_launch == 1 and res_ == resident_main and wt_ == wt_kernel
             c = cold if same else cold_kernel(args.numel, dtype, device, wt_, learners=1, resident=res_)
@@ -2082,9 +2077,10 @@ def main(argv=None):
             out["roofline"]["mix_ceiling_frac"] = mix["frac"]
             out["roofline"]["kernel_over_mix_ceiling"] = round(achieved / mix["achieved"], 4)
             out["roofline"]["mix_ceiling"] = dict(mix, note=(
-                "the timed kernel's access mix alone, same launch shape, cache policy and cold rotation, no "
-                "factor or lerp: what one launch of this size reaches on this chip (kernel_over_mix_ceiling = "
-                "the product kernel's rate over it)"))
+                "the timed kernel's access mix alone (same loads and stores at the same addresses, same launch "
+                "shape and cache policy, no factor or lerp), each launch interleaved with a product launch in the "
+                "same cold rotation: what one launch of this size reaches on this chip (kernel_over_mix_ceiling "
+                "= the product kernel's rate over it)"))
         if wt_kernel and args.numel == RESNET18_NUMEL and args.dtype == "f32":
             out["roofline"]["vs_mix_ceiling"] = dict(MIX_CEILING_11M, kernel_frac_over_ceiling=round(
                 achieved / HBM_PEAK_GBS / MIX_CEILING_11M["frac"], 4),

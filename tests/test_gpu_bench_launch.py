@@ -141,6 +141,11 @@ def test_one_gpu_line_is_configs1_self_peer_within_the_roofline():
     assert r["bytes_per_launch"] == 4 * n * 4 and r["metric_bytes_per_averaging"] == 3 * n * 4
     assert 0 < r["frac"] <= 1.0 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert abs(r["achieved"] / (r["bytes_per_launch"] / (r["avg_launch_us"] * 1e-6) / 1e9) - 1) < 1e-3
+    # the same access mix alone, interleaved launch by launch on the same buffers: the product
+    # kernel (factor, lerp, tail) runs at its mix's rate (round 5: 0.98-1.01 in tools/product_tune)
+    mix = r["mix_ceiling"]
+    assert mix["interleaved"] and mix["mix"] == "2R:2W" and mix["bytes_per_launch"] == 4 * (n * 4 // 16 * 16)
+    assert 0 < mix["frac"] <= 1.0 and r["kernel_over_mix_ceiling"] >= 0.93, r
     vc = out["value_cold"]
     assert vc["bytes_between_reuses"] > 1.2e9 and 0 < vc["value"] <= 8000.0
     assert out["config"]["value_cold"] == vc["value"]

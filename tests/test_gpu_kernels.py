@@ -282,3 +282,31 @@ def test_fused_average_zero_division_still_writes_the_snapshot(dtype):
     assert _lib.Coef.from_buffer_copy(coef.cpu().numpy().tobytes()).status == _lib.STATUS_ZERO_DIVISION
     assert torch.equal(p, before) and torch.equal(snap, before)
     assert clock[1].item() == 2.0
+
+
+@pytest.mark.parametrize("nr,nw", [(1, 1), (1, 2), (2, 1), (2, 2)])
+def test_stream_mix_measurement_kernel(nr, nw):
+    """dpwa_stream_mix (bench.py's roofline.mix_ceiling, not a product path): every 32-bit word of
+    the destinations is the wrap-around sum of the sources' words, over an exact grid of 1-KiB
+    spans whose last one is partial; bytes past nbytes are untouched; the first destination may be
+    a source (in place, as the bench runs it)."""
+    nbytes = 5 * 1024 + 48
+    words = nbytes // 4
+    src = [torch.randint(-2**31, 2**31 - 1, (words + 16,), dtype=torch.int32, device=DEV) for _ in range(nr)]
+    dst = [torch.full((words + 16,), 7, dtype=torch.int32, device=DEV) for _ in range(nw)]
+    dst[0] = src[-1] if nr == 2 else dst[0]          # in place when two sources
+    want = src[0].cpu().numpy().astype(np.int64)[:words]
+    if nr == 2:
+        want = want + src[1].cpu().numpy().astype(np.int64)[:words]
+    want = ((want + 2**31) % 2**32 - 2**31).astype(np.int32)
+    tail = [d.cpu().numpy()[words:].copy() for d in dst]
+    d_arr = (ctypes.c_void_p * 2)(*[d.data_ptr() for d in dst])
+    s_arr = (ctypes.c_void_p * 2)(*[x.data_ptr() for x in src])
+    _lib.call("dpwa_stream_mix", d_arr, nw, s_arr, nr, nbytes, stream(), None, None)
+    torch.cuda.synchronize()
+    for d, t in zip(dst, tail):
+        got = d.cpu().numpy()
+        assert np.array_equal(got[:words], want)
+        assert np.array_equal(got[words:], t)
+    with pytest.raises(_lib.DpwaError):
+        _lib.call("dpwa_stream_mix", d_arr, nw, s_arr, nr, nbytes + 4, stream(), None, None)

@@ -58,6 +58,7 @@ struct Set {
     char *snap;          // [header | pad | n]  (the destination slot)
     double *clock;       // [2]
     dpwa_coef *coef;
+    float *other;        // n: a fourth buffer (the bare mix's distinct first destination)
 };
 
 struct Args {
@@ -68,6 +69,28 @@ struct Args {
     const double *clock;
     const double *hdr;   // the peer slot's header (clock, loss)
 };
+
+// the bare write-through stream: 2 reads, 2 writes -- the parameters in place (as the product
+// stores them, `nt sc1`) and the next snapshot (`sc1`); DISTINCT: the first store goes to a fourth
+// buffer instead (dpwa_stream_mix's shape); FACTOR: + the clock/header scalar loads
+template <bool DISTINCT, bool FACTOR>
+__global__ __launch_bounds__(64) void k_dual(Args a, float *other)
+{
+    const int64_t off = (int64_t)blockIdx.x * 1024;
+    const __amdgpu_buffer_rsrc_t rp = rsrc(a.param, off, a.bytes, 1024);
+    const f32x4 q = ld<NT>(rsrc(a.peer, off, a.bytes, 1024), threadIdx.x * 16);
+    const f32x4 p = ld<NT>(rp, threadIdx.x * 16);
+    float fa = 0.5f, fb = 0.5f;
+    if (FACTOR) {
+        const double c = *a.clock, pc = a.hdr[0];
+        const double f = (c + pc) > -1.0 ? 0.5 : 0.25;
+        fa = (float)f;
+        fb = (float)(1.0 - f);
+    }
+    const f32x4 r = fa * q + fb * p;
+    st<NT | SC1>(DISTINCT ? rsrc(other, off, a.bytes, 1024) : rp, threadIdx.x * 16, r);
+    st<SC1>(rsrc(a.snap, off, a.bytes, 1024), threadIdx.x * 16, r);
+}
 
 struct BigArgs {         // the same plus padding to the product's kernel-argument size
     Args a;
@@ -121,6 +144,7 @@ int main(int argc, char **argv)
     n = n / 4 * 4;
     const int64_t bytes = n * 4;
     const int sets = (int)std::max<int64_t>(3, (int64_t)(1.5e9 / (3.0 * bytes)) + 1);
+    const bool dual_only = getenv("TUNE_DUAL") != nullptr;
     std::vector<Set> S(sets);
     for (int i = 0; i < sets; ++i) {
         Set &s = S[i];
@@ -129,6 +153,7 @@ int main(int argc, char **argv)
         CHECK(hipMalloc(&s.snap, kOff + bytes));
         CHECK(hipMalloc(&s.clock, 2 * sizeof(double)));
         CHECK(hipMalloc(&s.coef, sizeof(dpwa_coef)));
+        CHECK(hipMalloc(&s.other, bytes));
         CHECK(hipMemset(s.slot, 0, kOff));
         CHECK(hipMemset(s.snap, 0, kOff));
         CHECK(hipMemset(s.clock, 0, 2 * sizeof(double)));
@@ -160,6 +185,22 @@ int main(int argc, char **argv)
                  exit(1);
              }
          }},
+        {"bare dual in place", 4.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             hipExtLaunchKernelGGL((k_dual<false, false>), dim3(grid), dim3(64), 0, st, e0, e1, 0, args_of(s), s.other); }},
+        {"bare dual distinct (4 buffers)", 4.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             hipExtLaunchKernelGGL((k_dual<true, false>), dim3(grid), dim3(64), 0, st, e0, e1, 0, args_of(s), s.other); }},
+        {"bare dual in place + factor loads", 4.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             hipExtLaunchKernelGGL((k_dual<false, true>), dim3(grid), dim3(64), 0, st, e0, e1, 0, args_of(s), s.other); }},
+        {"dpwa_stream_mix 2R:2W (4 buffers)", 4.0, [bytes](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             void *dst[2] = {s.other, s.snap + kOff};
+             const void *src[2] = {s.slot + kOff, s.param};
+             if (dpwa_stream_mix(dst, 2, src, 2, bytes, st, e0, e1)) { fprintf(stderr, "%s\n", dpwa_last_error()); exit(1); }
+         }},
+        {"dpwa_stream_mix 2R:2W in place", 4.0, [bytes](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             void *dst[2] = {s.param, s.snap + kOff};
+             const void *src[2] = {s.slot + kOff, s.param};
+             if (dpwa_stream_mix(dst, 2, src, 2, bytes, st, e0, e1)) { fprintf(stderr, "%s\n", dpwa_last_error()); exit(1); }
+         }},
         {"bare oop sc1", 3.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
              hipExtLaunchKernelGGL(k_oop<SC1>, dim3(grid), dim3(64), 0, st, e0, e1, 0, args_of(s)); }},
         {"bare oop sc0+sc1", 3.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
@@ -177,6 +218,12 @@ int main(int argc, char **argv)
              b.a = args_of(s);
              hipExtLaunchKernelGGL(k_oop_bigarg<SC1 | SC0>, dim3(grid), dim3(64), 0, st, e0, e1, 0, b); }},
     };
+    if (dual_only) {   // TUNE_DUAL: the write-through rows only
+        std::vector<Variant> keep;
+        for (auto &v : vs)
+            if (v.factor == 4.0) keep.push_back(v);
+        vs.swap(keep);
+    }
     hipStream_t st;
     CHECK(hipStreamCreate(&st));
     const int reps = 6;
