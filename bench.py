@@ -1215,18 +1215,22 @@ def adapter_loop(device, cfg_dir, numel, dtype, steps, warmup=5):
     (write-through, reuse guard on) -- update_send, update_wait per round, no training step -- and
     the same with reuse_guard=False.  What the connection-level line costs through the adapter:
     its host work per call and, with the guard, the two small kernels per update_send that check
-    sampled words of the parameters against the snapshot the average wrote."""
+    sampled words of the parameters against the snapshot the average wrote.  Also the
+    resident adapter (resident=True) with and without its window guard (the reuse_guard flag there:
+    sampled words saved at update_send, compared at update_wait), the learner its own peer
+    as in the line."""
     from dpwa_amd import DpwaPyTorchAdapter
     from dpwa_amd.group import LocalGroup
     esize = 4 if dtype == torch.float32 else 2
     out = {}
-    for key, guard in (("default", True), ("no_guard", False)):
+    for i, (key, guard, resident) in enumerate((("default", True, False), ("no_guard", False, False),
+                                                 ("resident", True, True), ("resident_no_guard", False, True))):
         cfg = os.path.join(cfg_dir, "adapter_%s.yaml" % key)
-        write_config(cfg, ["a1"], "constant", self_peer=True, base_port=45400 + guard)
+        write_config(cfg, ["a1"], "constant", self_peer=True, base_port=45400 + 2 * i)
         net = torch.nn.Module()
         g = torch.Generator(device=device).manual_seed(0)
         net.register_parameter("w", torch.nn.Parameter(torch.randn(numel, device=device, generator=g).to(dtype)))
-        ad = DpwaPyTorchAdapter(net, "a1", cfg, seed=3000, group=LocalGroup(), reuse_guard=guard)
+        ad = DpwaPyTorchAdapter(net, "a1", cfg, seed=3000, group=LocalGroup(), reuse_guard=guard, resident=resident)
         for _ in range(warmup):
             ad.update_send(1.0)
             ad.update_wait(1.0)
@@ -1238,12 +1242,15 @@ def adapter_loop(device, cfg_dir, numel, dtype, steps, warmup=5):
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         out[key] = {"value": round(steps * 3 * numel * esize / el / 1e9, 2), "ms_per_step": round(1e3 * el / steps, 4),
-                    "reuse_guard": guard, "guard_hits": ad.reuse_guard_hits}
+                    "reuse_guard": guard, "resident": resident,
+                    "guard_hits": ad.window_guard_hits if resident else ad.reuse_guard_hits}
         ad.connection.close()
         del ad, net
         torch.cuda.empty_cache()
     out["note"] = ("DpwaPyTorchAdapter(net, name, config) over one %d-element parameter, self-peer config, "
-                   "update_send -> update_wait, %d steps; value = 3*N*s per averaging / wall time" % (numel, steps))
+                   "update_send -> update_wait, %d steps; value = 3*N*s per averaging / wall time. The resident "
+                   "rows' learner reads its parameters and its peer from the same slot (it is its own peer), so "
+                   "their kernel moves 2*N*s and their value is no HBM rate" % (numel, steps))
     return out
 
 

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("DPWA_HIP_LIB", os.path.join(_HERE, "libdpwa_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dpwa_hip.h")
 
 # Constants mirrored from include/dpwa_hip.h
-ABI_VERSION = 6
+ABI_VERSION = 7
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_NOMEM = 0, -1, -2, -3, -4
 F32, BF16, F64 = 0, 1, 2
 INTERP_CONSTANT, INTERP_CLOCK, INTERP_LOSS = 0, 1, 2
@@ -93,6 +93,7 @@ SIGNATURES = {
     "dpwa_learner_set_header_publish": [_vp, _int],
     "dpwa_learner_set_reuse_guard": [_vp, _int],
     "dpwa_learner_reuse_guard_hits": [_vp, ctypes.POINTER(ctypes.c_uint32)],
+    "dpwa_learner_window_hits": [_vp, ctypes.POINTER(ctypes.c_uint32)],
     "dpwa_learner_set_resident": [_vp, _vp, _vp],
     "dpwa_learner_resident_params": [_vp, ctypes.POINTER(_vp), _pint],
     "dpwa_learner_relocate": [_vp, _vp],

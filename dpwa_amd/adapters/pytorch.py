@@ -43,7 +43,7 @@ class DpwaPyTorchAdapter:
     they are in after each update_send and update_wait -- a publish moves no bytes and an
     average moves 3*N*s (the write-through form 4*N*s), for one ``.data`` assignment per
     parameter per round on the host.  Writes through ``param.data`` are then always part of the
-    next snapshot (no reuse guard is needed).  The price is the loop order: between update_send
+    next snapshot (no snapshot-reuse check is needed).  The price is the loop order: between update_send
     and update_wait the parameters ARE the snapshot peers read, so nothing may write them
     there.  The reference's loop trains exactly there (README.md:18-29,
     examples/pytorch-cifar/main.py:130-145: update_send, step, update_wait) and keeps the
@@ -51,7 +51,12 @@ class DpwaPyTorchAdapter:
     step then comes after the round's average instead of before it).  update_wait raises
     DpwaError when a parameter's (or the flat buffer's) version counter moved since update_send
     -- an optimizer step, ``param.add_``, ``load_state_dict`` in the window.  Writes through
-    ``param.data`` bypass version counters and are not caught.  Code that keeps raw data
+    ``param.data`` bypass version counters; for them the reuse guard (``reuse_guard``) is a window
+    guard here: every update_send runs one small kernel that compares the parameters published at
+    the previous update_send with 4096 words sampled then, and samples the new ones (no host
+    wait); a window found written makes a later update_send (the first that sees the device's
+    count) raise DpwaError without publishing (``window_guard_hits`` counts them, checking the last
+    check).  Writes that change none of the sampled words are not seen.  Code that keeps raw data
     pointers of the parameters across rounds (a captured HIP graph of the training step) must
     not use it."""
 
@@ -119,6 +124,8 @@ class DpwaPyTorchAdapter:
             if self._conn.parameters is None:          # first round: into the learner's slot 0
                 self._flat.resync()
                 self._flat.rehome(self._conn.make_resident(self._flat.buffer))
+                if self._reuse_guard:                      # the window guard (see the class doc)
+                    _lib.call("dpwa_learner_set_reuse_guard", self._conn._learner.handle, 1)
             self._flat.resync()                        # a parameter re-homed by the caller
             self._conn.update_send(self._flat.buffer, loss)
             # a publish with no average since the last one moved the parameters into the slot it
@@ -189,6 +196,16 @@ class DpwaPyTorchAdapter:
             return 0
         hits = ctypes.c_uint32()
         _lib.call("dpwa_learner_reuse_guard_hits", self._conn._learner.handle, ctypes.byref(hits))
+        return hits.value
+
+    @property
+    def window_guard_hits(self):
+        """Resident form: rounds whose parameters the window guard found written between
+        update_send and update_wait (waits for the last check; 0 before the first publish)."""
+        if self._conn._learner is None:
+            return 0
+        hits = ctypes.c_uint32()
+        _lib.call("dpwa_learner_window_hits", self._conn._learner.handle, ctypes.byref(hits))
         return hits.value
 
     @property

@@ -1315,7 +1315,7 @@ __global__ __launch_bounds__(kGuardWave) void k_guard_compare(const char *__rest
     const int64_t k = (int64_t)blockIdx.x * kGuardWave + threadIdx.x;
     int diff = 0;
     if (k < samples) {
-        const int64_t o = (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4;   // 0 .. n16-1
+        const int64_t o = (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4;   // 0 .. n16-1 (guard_offset)
         if (VEC) {
             const u32x4 a = *reinterpret_cast<const u32x4 *>(flat + o);
             const u32x4 b = *reinterpret_cast<const u32x4 *>(payload + o);
@@ -1370,6 +1370,65 @@ hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes,
         hipLaunchKernelGGL(k_copy_if<false>, dim3(kGuardCopyBlocks), dim3(kBlock), 0, s, payload, src, nbytes, dirty,
                            gen);
     }
+    return hipGetLastError();
+}
+
+// Window guard of resident parameters.  Between update_send and update_wait the resident
+// parameters ARE the snapshot peers read; writes through `param.data` there move no version
+// counter.  One launch per publish: the payload published last time -- untouched since its
+// window closed, until the average after this publish overwrites that slot -- is compared with the
+// samples saved when it was published (same offsets as k_guard_compare), then the samples of the
+// payload published now are saved in their place.  Each lane owns one sample, so the compare and
+// the save of a sample are in one lane, in order.  `old` NULL: save only; `cur` NULL: compare only.
+static_assert(kWindowSampleBytes == (kGuardSamples + 1) * 16, "window sample layout");
+
+__device__ __forceinline__ int64_t guard_offset(int64_t k, int64_t samples, int64_t n16)
+{
+    return (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4;
+}
+
+__global__ __launch_bounds__(kGuardWave) void k_window_roll(const char *__restrict__ old, const char *__restrict__ cur,
+                                                            int64_t nbytes, char *__restrict__ sample,
+                                                            int32_t *__restrict__ dirty, uint32_t *__restrict__ hits,
+                                                            uint32_t *__restrict__ host, int32_t gen)
+{
+    const int64_t n16 = nbytes >> 4;
+    const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
+    const int64_t k = (int64_t)blockIdx.x * kGuardWave + threadIdx.x;
+    const bool tail = blockIdx.x == 0 && threadIdx.x < (nbytes & 15);
+    char *const tail_sample = sample + kGuardSamples * 16 + threadIdx.x;
+    u32x4 *const sk = reinterpret_cast<u32x4 *>(sample) + k;
+    int diff = 0;
+    if (old) {
+        if (k < samples) {
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(old + guard_offset(k, samples, n16));
+            const u32x4 b = *sk;
+            diff = (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
+        }
+        if (tail) diff |= old[(n16 << 4) + threadIdx.x] != *tail_sample;
+    }
+    if (cur) {
+        if (k < samples) *sk = *reinterpret_cast<const u32x4 *>(cur + guard_offset(k, samples, n16));
+        if (tail) *tail_sample = cur[(n16 << 4) + threadIdx.x];
+    }
+    if (!old) return;
+    diff = __syncthreads_or(diff);
+    if (diff && threadIdx.x == 0) {
+        const int32_t prev = atomicExch(dirty, gen);
+        if (prev != gen) *host = atomicAdd(hits, 1u) + 1u;   // one workgroup per window
+    }
+}
+
+hipError_t launch_window_roll(const char *old, const char *cur, int64_t nbytes, char *sample, int32_t *dirty,
+                              uint32_t *hits, uint32_t *host, int32_t gen, hipStream_t s)
+{
+    if (nbytes <= 0 || (!old && !cur)) return hipSuccess;
+    if (!aligned16(old) || !aligned16(cur) || !aligned16(sample)) return hipErrorInvalidValue;
+    const int64_t n16 = nbytes >> 4;
+    const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
+    const uint32_t g = (uint32_t)((samples + kGuardWave - 1) / kGuardWave + (samples == 0 ? 1 : 0));
+    hipLaunchKernelGGL(k_window_roll, dim3(g), dim3(kGuardWave), 0, s, old, cur, nbytes, sample, dirty, hits, host,
+                       gen);
     return hipGetLastError();
 }
 

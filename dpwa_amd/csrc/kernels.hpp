@@ -140,6 +140,15 @@ hipError_t launch_stream_mix(const StreamMixArgs &a, hipStream_t s, const Launch
 hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes, int32_t *dirty, uint32_t *hits,
                                 int32_t gen, hipStream_t s);
 
+// Window guard of resident parameters (learner.cpp): one launch per publish compares the payload
+// published last time (`old`) with the samples saved then -- on a difference stamping *dirty with
+// `gen`, counting the window in *hits and mirroring the count into the host-mapped word *host --
+// and saves the samples of the payload published now (`cur`) into `sample` (kWindowSampleBytes).
+// Payloads 16-B aligned; either may be NULL.
+constexpr int64_t kWindowSampleBytes = (4096 + 1) * 16;
+hipError_t launch_window_roll(const char *old, const char *cur, int64_t nbytes, char *sample, int32_t *dirty,
+                              uint32_t *hits, uint32_t *host, int32_t gen, hipStream_t s);
+
 // A system-scope L2 write-back on every XCD after the work already on `s` (a publish whose
 // bytes were written by an earlier kernel, read by other devices).
 hipError_t launch_release_system(hipStream_t s);

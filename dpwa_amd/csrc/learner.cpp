@@ -254,6 +254,8 @@ struct Ctl {            // device control block
     int32_t guard_dirty;   // reuse guard: the generation (publish number) of the last publish that found
                            // the parameters changed (kernels.hip k_guard_compare)
     uint32_t guard_hits;   // ... and how many publishes did
+    int32_t window_dirty;  // window guard (resident): the generation of the last window found written
+    uint32_t window_hits;  // ... and how many windows were
 };
 
 
@@ -392,6 +394,18 @@ struct dpwa_learner {
     // move to the other slot at every average (or relocate)
     bool resident = false;
     int res_slot = 0;
+    // window guard (resident, with reuse_guard): each publish checks the payload published last
+    // time against the samples saved then and saves the new payload's (kernels.hip k_window_roll);
+    // written windows are counted on the device and mirrored into a host-mapped word the next
+    // publishes read without waiting
+    char *window_sample = nullptr;      // kWindowSampleBytes, allocated at first use
+    uint32_t *window_host = nullptr;    // mapped pinned: windows found written (device-written)
+    uint32_t *window_host_dev = nullptr;
+    const char *window_src = nullptr;   // payload the samples were taken from (NULL: none)
+    hipStream_t window_stream = nullptr;    // stream of the last roll
+    hipEvent_t ev_window = nullptr;     // orders a roll after the last one on another stream
+    int32_t window_gen = 0;
+    uint32_t window_reported = 0;
     const void *wt_flat = nullptr;
     hipStream_t wt_stream = nullptr;
     hipEvent_t ev_wt = nullptr;
@@ -637,6 +651,9 @@ int dpwa_learner_destroy(dpwa_learner *l)
     if (l->ev_wt) (void)hipEventDestroy(l->ev_wt);
     if (l->ev_read) (void)hipEventDestroy(l->ev_read);
     if (l->ev_relay) (void)hipEventDestroy(l->ev_relay);
+    if (l->ev_window) (void)hipEventDestroy(l->ev_window);
+    if (l->window_sample) (void)hipFree(l->window_sample);
+    if (l->window_host) (void)hipHostFree(l->window_host);
     for (auto &t : l->timing) {
         (void)hipEventDestroy(t.start);
         (void)hipEventDestroy(t.stop);
@@ -679,6 +696,79 @@ static int wait_slot_readers(dpwa_learner *l, int k, hipStream_t s)
 
 static int relocate_impl(dpwa_learner *l, hipStream_t s);
 
+// ---------------------------------------------------------------- window guard (resident)
+// Between update_send and update_wait resident parameters ARE the snapshot peers read (the
+// reference snapshots at update_send, pytorch.py:49-53, so a step in that window never reaches a
+// peer there).  The adapter catches optimizer steps by version counter; writes through
+// `param.data` move none, so with the reuse guard on every publish runs one small kernel
+// (kernels.hip k_window_roll): the payload published last time -- its window closed at the
+// average, which wrote the other slot, and nothing writes it again before the average after this
+// publish -- is compared with the reuse guard's 4,096 sampled words saved when it was published,
+// and the new payload's samples are saved.  A written window is counted on the device and
+// mirrored into a host-mapped word; a publish that finds the count grown (never waiting for a
+// check) fails with DPWA_ERR_STATE before publishing, and the one after proceeds.  Writes that
+// change none of the sampled words are not seen.
+static int window_alloc(dpwa_learner *l)
+{
+    if (l->window_sample) return DPWA_OK;
+    char *sample = nullptr;
+    uint32_t *host = nullptr, *host_dev = nullptr;
+    hipEvent_t ev = nullptr;
+    hipError_t e = hipMalloc(&sample, kWindowSampleBytes);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&host, sizeof(uint32_t), hipHostMallocMapped);
+    if (e == hipSuccess) {
+        *host = 0;
+        e = hipHostGetDevicePointer((void **)&host_dev, host, 0);
+    }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        if (sample) (void)hipFree(sample);
+        if (host) (void)hipHostFree(host);
+        if (ev) (void)hipEventDestroy(ev);
+        return set_error(DPWA_ERR_HIP, "window guard: %s", hipGetErrorString(e));
+    }
+    l->window_sample = sample;
+    l->window_host = host;
+    l->window_host_dev = host_dev;
+    l->ev_window = ev;
+    l->window_reported = 0;
+    return DPWA_OK;
+}
+
+// One roll on `s`: check the last window (if any), then sample `cur` (if not NULL).
+static int window_roll(dpwa_learner *l, const char *cur, hipStream_t s)
+{
+    int rc = window_alloc(l);
+    if (rc) return rc;
+    if (l->window_stream && l->window_stream != s) {
+        HIP_TRY(hipEventRecord(l->ev_window, l->window_stream));
+        HIP_TRY(hipStreamWaitEvent(s, l->ev_window, 0));
+    }
+    HIP_TRY(launch_window_roll(l->window_src, cur, (int64_t)l->payload_bytes, l->window_sample, &l->ctl->window_dirty,
+                               &l->ctl->window_hits, l->window_host_dev, l->window_gen, s));
+    l->window_stream = s;
+    if (cur) {
+        l->window_src = cur;
+        l->window_gen = (int32_t)(l->version + 1);
+    }
+    return DPWA_OK;
+}
+
+// Reports written windows counted since the last report; never waits for a check.
+static int window_report(dpwa_learner *l)
+{
+    if (!l->window_host) return DPWA_OK;
+    const uint32_t seen = __atomic_load_n(l->window_host, __ATOMIC_ACQUIRE);
+    if (seen == l->window_reported) return DPWA_OK;
+    const uint32_t newly = seen - l->window_reported;
+    l->window_reported = seen;
+    return set_error(DPWA_ERR_STATE,
+                     "resident parameters were written between update_send and update_wait (%u more window(s); "
+                     "through param.data, which moves no version counter): peers may have averaged with a partly "
+                     "written snapshot. With resident parameters the loop must run update_send -> update_wait -> "
+                     "step", newly);
+}
+
 static int publish_impl(dpwa_learner *l, const void *flat, double loss, const double *loss_dev, hipStream_t s,
                         bool reuse)
 {
@@ -686,12 +776,14 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
     const int k = (int)(l->version % 2);   // slot of publish number version+1
     char *slot = l->slots + (size_t)k * l->slot_stride;
     if (l->resident) {
+        int rc = window_report(l);
+        if (rc) return rc;
         // the parameters are the payload already: publish the header of the slot they are in
         // (after a publish with no average since, they first move on by one copy)
         if (flat != slot_payload(l, l->res_slot))
             return set_error(DPWA_ERR_ARG, "resident learner: publish the parameters where they are "
                                            "(dpwa_learner_resident_params)");
-        int rc = relocate_impl(l, s);
+        rc = relocate_impl(l, s);
         if (rc) return rc;
         flat = slot_payload(l, l->res_slot);
         reuse = true;
@@ -731,6 +823,10 @@ static int publish_impl(dpwa_learner *l, const void *flat, double loss, const do
     }
     l->wt_valid = false;
     l->wt_header = false;
+    if (l->resident && l->reuse_guard) {   // the last window's check; this window's samples
+        int rc = window_roll(l, (const char *)flat, s);
+        if (rc) return rc;
+    }
     std::lock_guard<std::mutex> g(l->pub_mu);
     l->publish_stream[k] = s;
     l->published[k] = true;
@@ -1398,6 +1494,7 @@ int dpwa_learner_set_reuse_guard(dpwa_learner *l, int on)
 {
     if (!l) return set_error(DPWA_ERR_ARG, "dpwa_learner_set_reuse_guard: NULL learner");
     l->reuse_guard = on != 0;
+    l->window_src = nullptr;   // a resident learner's window guard starts afresh at the next publish
     return DPWA_OK;
 }
 
@@ -1454,6 +1551,22 @@ int dpwa_learner_relocate(dpwa_learner *l, dpwa_stream_t stream)
     if (l->have_fetch) return set_error(DPWA_ERR_STATE, "dpwa_learner_relocate: a fetch is in flight (average it)");
     DeviceGuard dg(l->device);
     return relocate_impl(l, (hipStream_t)stream);
+}
+
+int dpwa_learner_window_hits(dpwa_learner *l, uint32_t *hits)
+{
+    if (!l || !hits) return set_error(DPWA_ERR_ARG, "dpwa_learner_window_hits: NULL argument");
+    DeviceGuard dg(l->device);
+    *hits = 0;
+    if (!l->window_sample) return DPWA_OK;
+    if (l->window_src) {   // check the window open now (or closed, not yet checked); keep its samples
+        hipStream_t s = l->window_stream;
+        HIP_TRY(launch_window_roll(l->window_src, nullptr, (int64_t)l->payload_bytes, l->window_sample,
+                                   &l->ctl->window_dirty, &l->ctl->window_hits, l->window_host_dev, l->window_gen, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    *hits = __atomic_load_n(l->window_host, __ATOMIC_ACQUIRE);
+    return DPWA_OK;
 }
 
 int dpwa_learner_reuse_guard_hits(dpwa_learner *l, uint32_t *hits)

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DPWA_ABI_VERSION 6
+#define DPWA_ABI_VERSION 7
 
 #define DPWA_OK 0
 #define DPWA_ERR_ARG (-1)     /* bad argument (API misuse)                          */
@@ -272,9 +272,17 @@ int dpwa_learner_publish_reuse(dpwa_learner *l, const void *flat, double loss, c
  * the written-through snapshot on the device, and copies the payload from `flat` when any
  * differs -- a write the caller's bookkeeping missed (pytorch.py:49-53 then holds anyway: the
  * snapshot is the parameters at update_send).  Two small launches, no host sync.
- * reuse_guard_hits: how many publishes found a difference (synchronises the device). */
+ * reuse_guard_hits: how many publishes found a difference (synchronises the device).
+ * On a resident learner (below) the same flag is the window guard: every publish runs one small
+ * kernel that compares the payload published last time with those words saved when it was
+ * published -- a write while peers could read it (update_send .. update_wait, through
+ * `param.data`, which the adapter's version counters miss) -- and saves the new payload's.  A
+ * written window is reported by the first publish that finds it counted (never waiting for a
+ * check): DPWA_ERR_STATE, nothing published; the publish after proceeds.  window_hits: windows
+ * found written so far, checking the last one now (synchronises its stream). */
 int dpwa_learner_set_reuse_guard(dpwa_learner *l, int on);
 int dpwa_learner_reuse_guard_hits(dpwa_learner *l, uint32_t *hits);
+int dpwa_learner_window_hits(dpwa_learner *l, uint32_t *hits);
 
 /* Resident parameters (extension; replaces the snapshot copy of pytorch.py:49-53 and
  * RxThread.set_current_state, conn.py:73-79, with no copy at all).  The learner's parameters live

@@ -156,3 +156,6 @@ def test_one_gpu_line_is_configs1_self_peer_within_the_roofline():
     ad = out["adapter_loop"]
     assert ad["default"]["reuse_guard"] and not ad["no_guard"]["reuse_guard"]
     assert ad["default"]["ms_per_step"] <= 1.35 * ad["no_guard"]["ms_per_step"], ad
+    # the resident adapter's window guard (a save at update_send, a compare at update_wait) likewise
+    assert ad["resident"]["resident"] and ad["resident"]["reuse_guard"] and ad["resident"]["guard_hits"] == 0
+    assert ad["resident"]["ms_per_step"] <= 1.35 * ad["resident_no_guard"]["ms_per_step"], ad

@@ -369,3 +369,65 @@ def test_resident_adapter_second_publish_without_wait_follows_the_parameters(tmp
     torch.cuda.synchronize()
     for ad in ads:
         ad.connection.close()
+
+
+@pytest.mark.parametrize("many", [False, True])
+def test_resident_window_guard_catches_data_writes(tmp_path, many):
+    """Writes through ``param.data`` in the send -> wait window move no version counter, so
+    _check_window cannot see them; the window guard (reuse_guard, on by default) compares the
+    published payload's sampled words at update_wait on the device.  These models are smaller than
+    4096 16-B words, so every word is sampled and a one-element write is caught: the learner that
+    wrote counts the window (window_guard_hits) and its next update_send raises DpwaError without
+    publishing; the one after proceeds, and the other learner is untouched.  With
+    reuse_guard=False nothing is checked."""
+    names = ["w0", "w1"]
+    cfg = tmp_path / "wg.yaml"
+    _write_cfg(cfg, names, 1.0, "constant")
+    torch.manual_seed(6)
+    for guard in (True, False):
+        nets = [torch.nn.Sequential(torch.nn.Linear(6, 9), torch.nn.Linear(9, 2)).to(DEV) for _ in names]
+        grp = LocalGroup()
+        ads = [DpwaPyTorchAdapter(nets[g], names[g], str(cfg), seed=70 + g, group=grp, resident=True,
+                                  reuse_guard=guard) for g in range(2)]
+        opts = [torch.optim.SGD(n.parameters(), lr=0.1) for n in nets]
+
+        def wait_all():
+            if many:
+                DpwaPyTorchAdapter.update_wait_many(ads, [1.0, 1.0])
+            else:
+                for ad in ads:
+                    ad.update_wait(1.0)
+
+        def steps():
+            for g in range(2):
+                opts[g].zero_grad()
+                nets[g](torch.randn(3, 6, device=DEV)).sum().backward()
+                opts[g].step()
+
+        for r in range(3):                  # the resident order, no window written
+            for ad in ads:
+                ad.update_send(1.0)
+            wait_all()
+            steps()
+        assert [ad.window_guard_hits for ad in ads] == [0, 0]
+        for ad in ads:
+            ad.update_send(1.0)
+        w = list(nets[1].parameters())[2]
+        w.data[0, 0] += 1.0                 # one element, through .data: no version counter moves
+        wait_all()                          # the version check passes; the device check does not
+        steps()
+        assert [ad.window_guard_hits for ad in ads] == ([0, 1] if guard else [0, 0])
+        ads[0].update_send(1.0)
+        if guard:
+            with pytest.raises(_lib.DpwaError, match="written between update_send and update_wait"):
+                ads[1].update_send(1.0)
+        ads[1].update_send(1.0)             # reported once: this publish proceeds
+        wait_all()
+        steps()
+        for ad in ads:
+            ad.update_send(1.0)
+        wait_all()
+        assert [ad.window_guard_hits for ad in ads] == ([0, 1] if guard else [0, 0])
+        torch.cuda.synchronize()
+        for ad in ads:
+            ad.connection.close()
