@@ -1995,8 +1995,13 @@ int dpwa_learner_copy_fetched(dpwa_learner *l, void *dst_dev, dpwa_stream_t stre
 static int probe_since(dpwa_learner *l, hipEvent_t since, float *ms)
 {
     if (!l->probe_stream) {
-        HIP_TRY(hipStreamCreateWithFlags(&l->probe_stream, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreate(&l->ev_probe));
+        hipStream_t ps = nullptr;
+        hipEvent_t pe = nullptr;
+        hipError_t e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
+        if (e == hipSuccess && (e = hipEventCreate(&pe)) != hipSuccess) (void)hipStreamDestroy(ps);
+        if (e != hipSuccess) return set_error(DPWA_ERR_HIP, "probe stream: %s", hipGetErrorString(e));
+        l->probe_stream = ps;
+        l->ev_probe = pe;
     }
     HIP_TRY(hipEventRecord(l->ev_probe, l->probe_stream));
     const int64_t t0 = now_ns();
