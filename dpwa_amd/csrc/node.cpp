@@ -499,8 +499,8 @@ int dpwa_node_update_wait_average(dpwa_node *n, void *flat, double loss, const d
             // the average rewrites the slot of the NEXT publish (that of publish v-1): the
             // board's publish rule -- our publish v is visible, no live reader holds v-1 --
             // must hold before the kernel is enqueued, not only before the next update_send
-            const int rc = dpwa_board_publish_wait(n->board, learner_version(n->learner) + 1, n->publish_timeout_ms);
-            if (rc) return rc;
+            if ((rc = dpwa_board_publish_wait(n->board, learner_version(n->learner) + 1, n->publish_timeout_ms)))
+                return rc;
         }
         return dpwa_learner_average_through(n->learner, flat, loss, loss_dev, stream);
     }
