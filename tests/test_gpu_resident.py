@@ -431,3 +431,65 @@ def test_resident_window_guard_catches_data_writes(tmp_path, many):
         torch.cuda.synchronize()
         for ad in ads:
             ad.connection.close()
+
+
+def test_resident_window_guard_samples_and_tail_bytes(tmp_path):
+    """The window guard's sampling on a model larger than its 4096 words: ragged bf16
+    (100003 elements: 12500 16-B words and 6 tail bytes), connection level with the guard set
+    through the C ABI.  A write to the tail bytes or to a sampled word is caught (window_hits
+    grows, the next update_send raises), a write to a word no sample covers is not -- the
+    documented limit -- and rounds with no write stay clean.  Writes go through a second view of
+    the resident memory, so no version counter of conn.parameters moves."""
+    from dpwa_amd.devview import device_tensor
+    names = ["t0", "t1"]
+    cfg = tmp_path / "tail.yaml"
+    _write_cfg(cfg, names, 1.0, "constant")
+    n = 100_003
+    n16 = n * 2 // 16
+    samples = 4096
+    sampled = {(k * (n16 - 1) // (samples - 1)) for k in range(samples)}
+    unsampled = next(w for w in range(1, n16) if w not in sampled)
+    group = LocalGroup()
+    conns = [DpwaConnection(names[g], str(cfg), seed=60 + g, group=group) for g in range(2)]
+    for g in range(2):
+        conns[g].make_resident(torch.randn(n, device=DEV).to(torch.bfloat16))
+        _lib.call("dpwa_learner_set_reuse_guard", conns[g]._learner.handle, 1)
+
+    def hits(c):
+        h = ctypes.c_uint32()
+        _lib.call("dpwa_learner_window_hits", c._learner.handle, ctypes.byref(h))
+        return h.value
+
+    def round_(write=None):
+        for c in conns:
+            c.update_send(c.parameters, 1.0)
+        if write is not None:
+            p = conns[1].parameters
+            alias = device_tensor(p.data_ptr(), n, torch.bfloat16, DEV)    # its own version counter
+            alias[write] += 1.0
+            del alias
+        for c in conns:
+            c.update_wait_average(c.parameters, 1.0)
+
+    round_()
+    round_()
+    assert [hits(c) for c in conns] == [0, 0]
+    expect = 0
+    for elem, caught in ((n - 1, True),                                  # a tail byte
+                         (sorted(sampled)[1] * 8 + 3, True),              # inside a sampled word
+                         (unsampled * 8 + 5, False)):                     # a word no sample covers
+        round_(write=elem)
+        expect += caught
+        assert hits(conns[1]) == expect and hits(conns[0]) == 0, elem
+        conns[0].update_send(conns[0].parameters, 1.0)
+        if caught:
+            with pytest.raises(_lib.DpwaError, match="written between update_send and update_wait"):
+                conns[1].update_send(conns[1].parameters, 1.0)
+        conns[1].update_send(conns[1].parameters, 1.0)
+        for c in conns:
+            c.update_wait_average(c.parameters, 1.0)
+        round_()
+        assert hits(conns[1]) == expect
+    torch.cuda.synchronize()
+    for c in conns:
+        c.close()
