@@ -169,6 +169,115 @@ def base_line(args, world):
             "data": "synthetic N(0,1) flat parameter vectors (no dataset needed)"}
 
 
+# ---------------------------------------------------------------- the result line
+# The driver keeps only the tail of stdout (about 9 KB): round 5's 21.7 KB line was cut and went
+# unparsed.  The line therefore carries scalars only and stays under LINE_MAX bytes; everything
+# else (sweeps, restatement rows, side loops, prose) goes to a detail file the line names.
+LINE_MAX = 6144
+_TOP = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "gossip_rounds_per_s", "gossip_rounds_per_s_per_learner", "averagings",
+        "publish_fallback", "error", "phase")
+_ROOFLINE = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_x", "bytes_per_launch",
+             "metric_bytes_per_averaging", "avg_launch_us", "kernel", "in_loop_frac", "in_loop_avg_launch_us",
+             "mix_ceiling_frac", "kernel_over_mix_ceiling", "learners_per_launch")
+_CPU = ("value", "unit", "cores", "kind", "ms_per_round", "numel")
+_XGMI = ("bytes_per_pull", "avg_pull_us", "achieved_gbs_per_pull", "peak_gbs", "frac", "ranks_share_device")
+_SCALAR = (int, float, bool, str, type(None))
+
+
+def _pick(d, keys, maxlen=160):
+    """The scalar entries of `d` named in `keys` (strings cut to maxlen)."""
+    out = {}
+    for k in keys:
+        v = (d or {}).get(k, None) if isinstance(d, dict) else None
+        if k not in (d or {}) or not isinstance(v, _SCALAR):
+            continue
+        out[k] = v[:maxlen] if isinstance(v, str) else v
+    return out
+
+
+def compact_line(full, detail=None):
+    """The driver's line from the full result: the contract keys and the scalar headline figures
+    (value, roofline, cpu_baseline, value_cold, scaling_basis raw/weak, parity verdicts), at most
+    LINE_MAX bytes.  `detail` = where the full result was written (named in the line)."""
+    out = _pick(full, _TOP, maxlen=240)
+    cfg = full.get("config")
+    if isinstance(cfg, dict):
+        out["config"] = {k: (v[:200] if isinstance(v, str) else v) for k, v in cfg.items()
+                         if isinstance(v, _SCALAR) and k not in ("loop_order", "peer")}
+    vc = full.get("value_cold")
+    out["value_cold"] = vc.get("value") if isinstance(vc, dict) else vc if isinstance(vc, _SCALAR) else None
+    rl = full.get("roofline")
+    if isinstance(rl, dict):
+        out["roofline"] = _pick(rl, _ROOFLINE)
+    cpu = full.get("cpu_baseline")
+    if isinstance(cpu, dict):
+        c = _pick(cpu, _CPU)
+        if isinstance(cpu.get("sample"), str):
+            c["sample"] = cpu["sample"][:360]
+        out["cpu_baseline"] = c
+    elif "cpu_baseline" in full:
+        out["cpu_baseline"] = None
+    sb = full.get("scaling_basis")
+    if isinstance(sb, dict):
+        s = _pick(sb, ("n_gpus", "learners_per_gpu", "learners", "publish"))
+        for part in ("raw", "weak"):
+            if isinstance(sb.get(part), dict):
+                s[part] = {k: v for k, v in sb[part].items() if isinstance(v, (int, float, bool, type(None)))}
+        out["scaling_basis"] = s
+    par = full.get("parity")
+    if isinstance(par, dict):
+        out["parity"] = {k: bool(v) for k, v in par.items() if k != "workload"}
+    pt = full.get("parity_of_timed_transport")
+    if isinstance(pt, dict):
+        out["parity_of_timed_transport"] = _pick(pt, ("transport", "ok"))
+    x = full.get("xgmi")
+    if isinstance(x, dict):
+        out["xgmi"] = _pick(x, _XGMI)
+        if isinstance(x.get("relay"), dict):
+            out["xgmi"]["relay_frac"] = x["relay"].get("frac")
+    pc = full.get("pull_choice")
+    if isinstance(pc, dict):
+        out["pull"] = pc.get("chosen")
+    if isinstance(full.get("trial_errors"), dict):
+        out["trial_errors"] = sorted(full["trial_errors"])
+    if detail:
+        out["detail"] = detail
+    # a hard bound whatever the content: shed the longest optional parts first
+    for drop in (("config", "workload"), ("cpu_baseline", "sample"), ("roofline", "kernel"), ("trial_errors",),
+                 ("config",), ("xgmi",), ("scaling_basis",), ("data",)):
+        if len(json.dumps(out)) <= LINE_MAX:
+            break
+        if len(drop) == 2 and isinstance(out.get(drop[0]), dict):
+            out[drop[0]].pop(drop[1], None)
+        else:
+            out.pop(drop[0], None)
+    if len(json.dumps(out)) > LINE_MAX and isinstance(out.get("parity"), dict):
+        p = out["parity"]
+        out["parity"] = {"all": all(p.values()), "failed": [k for k, v in p.items() if not v][:20]}
+    return out
+
+
+def detail_path(world):
+    """Where the full result goes: $DPWA_BENCH_DETAIL, else gpurun_out/bench_detail_n<N>.json."""
+    return os.environ.get("DPWA_BENCH_DETAIL") or os.path.join(ROOT, "gpurun_out", "bench_detail_n%d.json" % world)
+
+
+def emit_result(full, path):
+    """Writes the full result to `path` (best effort) and prints the compact line."""
+    try:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path + ".tmp", "w") as f:
+            json.dump(full, f, indent=1, default=str)
+        os.replace(path + ".tmp", path)
+        rel = os.path.relpath(path, ROOT)
+        where = rel if not rel.startswith("..") else path
+    except OSError as e:
+        progress("detail file not written: %s" % e)
+        where = None
+    emit(json.dumps(compact_line(full, where)))
+
+
 # ---------------------------------------------------------------- robustness of the N>1 run
 def self_launch(args, argv):
     """`--gpus N` (N > 1) without an external launcher: run torch.distributed.run as a CHILD
@@ -287,7 +396,7 @@ class Watchdog:
                     out = dict(held)
                     out["error"] = "watchdog: phase '%s' overran its budget (the line up to it)" % phase
                     out["phase"] = phase
-                    emit(json.dumps(out))
+                    emit_result(out, detail_path(self.world))
                 faulthandler.dump_traceback(all_threads=True)
                 sys.stderr.flush()
                 os._exit(held_rc)
@@ -299,7 +408,7 @@ class Watchdog:
                 if transport is not None:
                     parity[transport] = False
                 out["parity"] = parity
-                emit(json.dumps(out))
+                emit(json.dumps(compact_line(out)))
             faulthandler.dump_traceback(all_threads=True)
             sys.stderr.flush()
             os._exit(3)
@@ -1778,7 +1887,7 @@ def main(argv=None):
                 out["error"] = "no transport passed the parity check and its trials"
                 out["parity"] = parity
                 out["trial_errors"] = trial_errors
-                emit(json.dumps(out))
+                emit_result(out, detail_path(world))
             sys.exit(1)
         pull = max(medians, key=medians.get)
         if pull.startswith("async/"):
@@ -2184,7 +2293,7 @@ def main(argv=None):
                          rows=round_rows, resident=resident_main)
     wd.enter("result", 60.0)
     if out is not None:
-        emit(json.dumps(out))
+        emit_result(out, detail_path(world))
     wd.hold(None, 1 if parity_failed else 0)      # the line is out: an overrun now only exits
     wd.enter("shutdown", 300.0)
     for conn, _ in lockstep_learners + async_learners:

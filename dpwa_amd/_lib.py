@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("DPWA_HIP_LIB", os.path.join(_HERE, "libdpwa_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dpwa_hip.h")
 
 # Constants mirrored from include/dpwa_hip.h
-ABI_VERSION = 7
+ABI_VERSION = 8
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_NOMEM = 0, -1, -2, -3, -4
 F32, BF16, F64 = 0, 1, 2
 INTERP_CONSTANT, INTERP_CLOCK, INTERP_LOSS = 0, 1, 2
@@ -81,6 +81,9 @@ _pint = ctypes.POINTER(ctypes.c_int)
 SIGNATURES = {
     "dpwa_last_error": [],
     "dpwa_abi_version": [],
+    "dpwa_trace_enabled": [],
+    "dpwa_trace_push": [ctypes.c_char_p],
+    "dpwa_trace_pop": [],
     "dpwa_lerp_f32": [_vp, _vp, _i64, _vp, _vp],
     "dpwa_lerp_bf16": [_vp, _vp, _i64, _vp, _vp],
     "dpwa_lerp_f32_host": [_vp, _vp, _i64, _dbl, _vp],
@@ -219,6 +222,25 @@ def load():
         raise DpwaLibraryError(_load_error)
     _lib = lib
     return lib
+
+
+# roctx ranges (include/dpwa_hip.h dpwa_trace_*): read once, like the library does at load
+TRACE = os.environ.get("DPWA_ROCTX") == "1"
+
+
+class trace_range:
+    """A named roctx range over a `with` block (only used when TRACE is set)."""
+
+    def __init__(self, name):
+        self.name = name.encode()
+
+    def __enter__(self):
+        load().dpwa_trace_push(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        load().dpwa_trace_pop()
+        return False
 
 
 def call(name, *args):

@@ -34,9 +34,11 @@ class DpwaPyTorchAdapter:
     any of these forces a full publish.  In-place writes through ``param.data`` bypass version
     counters; for them the reuse guard (``reuse_guard``, on by default) compares 4096 16-byte
     words spread over the parameters with the snapshot on the device and publishes in full when
-    any differs (two small kernels per update_send, no host sync).  A write that changes none
-    of the sampled words is not seen: a loop that writes parameters sparsely through
-    ``param.data`` between update_wait and update_send should pass ``write_through=False``.
+    any differs (two small kernels per update_send, no host sync).  The sampled words move on by
+    one each publish, so every word is compared once in any ceil(N*s/16/4095) publishes: a sparse
+    write that one publish's samples miss is published late (by a later publish that samples it),
+    not never.  A loop that writes parameters sparsely through ``param.data`` between update_wait
+    and update_send and needs every snapshot exact should pass ``write_through=False``.
 
     resident (extension, off by default): the parameters live in the learner's own two snapshot
     slots (``DpwaConnection.make_resident``) and every ``param.data`` is re-pointed to the slot
@@ -56,7 +58,8 @@ class DpwaPyTorchAdapter:
     the previous update_send with 4096 words sampled then, and samples the new ones (no host
     wait); a window found written makes a later update_send (the first that sees the device's
     count) raise DpwaError without publishing (``window_guard_hits`` counts them, checking the last
-    check).  Writes that change none of the sampled words are not seen.  Code that keeps raw data
+    check).  The sampled words move on by one each publish (as the reuse guard's), so a sparse write
+    repeated every window is caught within ceil(N*s/16/4095) windows.  Code that keeps raw data
     pointers of the parameters across rounds (a captured HIP graph of the training step) must
     not use it."""
 
@@ -100,7 +103,7 @@ class DpwaPyTorchAdapter:
                 "DpwaPyTorchAdapter(%s): %d parameter(s) were re-homed through param.data. Write-through "
                 "snapshots (the default) are reused when no version counter moved; in-place writes through "
                 "param.data move none and are caught only if they change one of the %d words the reuse guard "
-                "samples. A loop that writes parameters sparsely through param.data between update_wait and "
+                "samples at that publish (the samples move on by one word per publish). A loop that writes parameters sparsely through param.data between update_wait and "
                 "update_send must pass write_through=False, or peers may average with a snapshot that lacks "
                 "those writes.", self._conn.name, moved, 4096)
 
@@ -120,6 +123,12 @@ class DpwaPyTorchAdapter:
 
     def update_send(self, loss):
         """pytorch.py:42-53: publish the parameters and maybe start a fetch."""
+        if _lib.TRACE:
+            with _lib.trace_range("adapter.update_send"):
+                return self._update_send(loss)
+        return self._update_send(loss)
+
+    def _update_send(self, loss):
         if self._resident:
             if self._conn.parameters is None:          # first round: into the learner's slot 0
                 self._flat.resync()
@@ -147,6 +156,12 @@ class DpwaPyTorchAdapter:
     def update_wait(self, loss):
         """pytorch.py:55-68: wait for the fetch and average in place (resident: into the other
         slot, where the parameters are re-pointed)."""
+        if _lib.TRACE:
+            with _lib.trace_range("adapter.update_wait"):
+                return self._update_wait(loss)
+        return self._update_wait(loss)
+
+    def _update_wait(self, loss):
         if self._resident:
             if self._conn.parameters is None:         # no update_send yet: nothing to average
                 return

@@ -1300,9 +1300,24 @@ hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *c
 // never needs clearing; the first stamp of a generation counts a hit).  The copy's workgroups, one
 // per CU, return at once unless the word carries `gen`.  (Round 4's single-workgroup compare,
 // 4,096 dependent-latency loads on one CU, cost ~19 us per update_send: bench `adapter_loop`.)
+// The sampled words move with the generation (guard_offset): sample k of generation g is word
+// base(k) + g mod W, W the widest gap between two bases, so over any W consecutive publishes every
+// word of the parameters is compared once -- a sparse write through `param.data` that the samples
+// of one publish miss is caught within W = ceil((n16-1)/4095) publishes, at the same per-publish cost.
 constexpr int kGuardSamples = 4096;
 constexpr int kGuardWave = 64;
 constexpr int kGuardCopyBlocks = 256;
+
+// Byte offset of sample k (of `samples`) over n16 16-B words at generation `gen`.
+__device__ __forceinline__ int64_t guard_offset(int64_t k, int64_t samples, int64_t n16, uint32_t gen)
+{
+    if (samples <= 1) return 0;
+    const int64_t base = k * (n16 - 1) / (samples - 1);             // 0 .. n16-1, ends included
+    const int64_t widest = (n16 - 1 + samples - 2) / (samples - 1);   // ceil((n16-1)/(samples-1)) >= 1
+    int64_t w = base + (int64_t)(gen % (uint64_t)widest);
+    if (w >= n16) w -= n16;                                           // the last base wraps to the front
+    return w << 4;
+}
 
 template <bool VEC>
 __global__ __launch_bounds__(kGuardWave) void k_guard_compare(const char *__restrict__ flat,
@@ -1315,7 +1330,7 @@ __global__ __launch_bounds__(kGuardWave) void k_guard_compare(const char *__rest
     const int64_t k = (int64_t)blockIdx.x * kGuardWave + threadIdx.x;
     int diff = 0;
     if (k < samples) {
-        const int64_t o = (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4;   // 0 .. n16-1 (guard_offset)
+        const int64_t o = guard_offset(k, samples, n16, (uint32_t)gen);
         if (VEC) {
             const u32x4 a = *reinterpret_cast<const u32x4 *>(flat + o);
             const u32x4 b = *reinterpret_cast<const u32x4 *>(payload + o);
@@ -1377,20 +1392,16 @@ hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes,
 // parameters ARE the snapshot peers read; writes through `param.data` there move no version
 // counter.  One launch per publish: the payload published last time -- untouched since its
 // window closed, until the average after this publish overwrites that slot -- is compared with the
-// samples saved when it was published (same offsets as k_guard_compare), then the samples of the
-// payload published now are saved in their place.  Each lane owns one sample, so the compare and
-// the save of a sample are in one lane, in order.  `old` NULL: save only; `cur` NULL: compare only.
+// samples saved when it was published (k_guard_compare's offsets of that publish's generation
+// `gen`), then the samples of the payload published now (generation `cur_gen`, the offsets moved on
+// by one) are saved in their place.  Each lane owns one sample, so the compare and the save of a
+// sample are in one lane, in order.  `old` NULL: save only; `cur` NULL: compare only.
 static_assert(kWindowSampleBytes == (kGuardSamples + 1) * 16, "window sample layout");
-
-__device__ __forceinline__ int64_t guard_offset(int64_t k, int64_t samples, int64_t n16)
-{
-    return (samples > 1 ? k * (n16 - 1) / (samples - 1) : 0) << 4;
-}
 
 __global__ __launch_bounds__(kGuardWave) void k_window_roll(const char *__restrict__ old, const char *__restrict__ cur,
                                                             int64_t nbytes, char *__restrict__ sample,
                                                             int32_t *__restrict__ dirty, uint32_t *__restrict__ hits,
-                                                            uint32_t *__restrict__ host, int32_t gen)
+                                                            uint32_t *__restrict__ host, int32_t gen, int32_t cur_gen)
 {
     const int64_t n16 = nbytes >> 4;
     const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
@@ -1401,14 +1412,14 @@ __global__ __launch_bounds__(kGuardWave) void k_window_roll(const char *__restri
     int diff = 0;
     if (old) {
         if (k < samples) {
-            const u32x4 a = *reinterpret_cast<const u32x4 *>(old + guard_offset(k, samples, n16));
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(old + guard_offset(k, samples, n16, (uint32_t)gen));
             const u32x4 b = *sk;
             diff = (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
         }
         if (tail) diff |= old[(n16 << 4) + threadIdx.x] != *tail_sample;
     }
     if (cur) {
-        if (k < samples) *sk = *reinterpret_cast<const u32x4 *>(cur + guard_offset(k, samples, n16));
+        if (k < samples) *sk = *reinterpret_cast<const u32x4 *>(cur + guard_offset(k, samples, n16, (uint32_t)cur_gen));
         if (tail) *tail_sample = cur[(n16 << 4) + threadIdx.x];
     }
     if (!old) return;
@@ -1420,7 +1431,7 @@ __global__ __launch_bounds__(kGuardWave) void k_window_roll(const char *__restri
 }
 
 hipError_t launch_window_roll(const char *old, const char *cur, int64_t nbytes, char *sample, int32_t *dirty,
-                              uint32_t *hits, uint32_t *host, int32_t gen, hipStream_t s)
+                              uint32_t *hits, uint32_t *host, int32_t gen, int32_t cur_gen, hipStream_t s)
 {
     if (nbytes <= 0 || (!old && !cur)) return hipSuccess;
     if (!aligned16(old) || !aligned16(cur) || !aligned16(sample)) return hipErrorInvalidValue;
@@ -1428,7 +1439,7 @@ hipError_t launch_window_roll(const char *old, const char *cur, int64_t nbytes, 
     const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
     const uint32_t g = (uint32_t)((samples + kGuardWave - 1) / kGuardWave + (samples == 0 ? 1 : 0));
     hipLaunchKernelGGL(k_window_roll, dim3(g), dim3(kGuardWave), 0, s, old, cur, nbytes, sample, dirty, hits, host,
-                       gen);
+                       gen, cur_gen);
     return hipGetLastError();
 }
 

@@ -147,7 +147,7 @@ hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes,
 // Payloads 16-B aligned; either may be NULL.
 constexpr int64_t kWindowSampleBytes = (4096 + 1) * 16;
 hipError_t launch_window_roll(const char *old, const char *cur, int64_t nbytes, char *sample, int32_t *dirty,
-                              uint32_t *hits, uint32_t *host, int32_t gen, hipStream_t s);
+                              uint32_t *hits, uint32_t *host, int32_t gen, int32_t cur_gen, hipStream_t s);
 
 // A system-scope L2 write-back on every XCD after the work already on `s` (a publish whose
 // bytes were written by an earlier kernel, read by other devices).

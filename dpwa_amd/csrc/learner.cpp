@@ -745,7 +745,7 @@ static int window_roll(dpwa_learner *l, const char *cur, hipStream_t s)
         HIP_TRY(hipStreamWaitEvent(s, l->ev_window, 0));
     }
     HIP_TRY(launch_window_roll(l->window_src, cur, (int64_t)l->payload_bytes, l->window_sample, &l->ctl->window_dirty,
-                               &l->ctl->window_hits, l->window_host_dev, l->window_gen, s));
+                               &l->ctl->window_hits, l->window_host_dev, l->window_gen, (int32_t)(l->version + 1), s));
     l->window_stream = s;
     if (cur) {
         l->window_src = cur;
@@ -772,7 +772,12 @@ static int window_report(dpwa_learner *l)
 static int publish_impl(dpwa_learner *l, const void *flat, double loss, const double *loss_dev, hipStream_t s,
                         bool reuse)
 {
+    TraceRange tr(reuse ? "dpwa.learner_publish.reuse" : "dpwa.learner_publish");
     l->timing_armed = false;   // armed for the last round's average, which did not happen
+    if (l->resident && l->reuse_guard) {   // the window guard's buffers, before anything is queued
+        int rc = window_alloc(l);
+        if (rc) return rc;
+    }
     const int k = (int)(l->version % 2);   // slot of publish number version+1
     char *slot = l->slots + (size_t)k * l->slot_stride;
     if (l->resident) {
@@ -1257,6 +1262,12 @@ static int average_prepare(dpwa_learner *l, void *flat, double loss, const doubl
         const int k = (int)(l->version % 2);   // slot of the next publish
         int rc = wait_slot_readers(l, k, s);
         if (rc) return rc;
+        if (l->resident && l->window_stream && l->window_stream != s) {
+            // the window guard's last roll (on the publish's stream) read the payload published
+            // before it -- slot k, which this average overwrites
+            HIP_TRY(hipEventRecord(l->ev_window, l->window_stream));
+            HIP_TRY(hipStreamWaitEvent(s, l->ev_window, 0));
+        }
         p.snap = slot_payload(l, k);
         p.snap_slot = k;
         if (l->cfg.method != DPWA_INTERP_LOSS && !l->header_on_publish) {   // peers never read this header's loss
@@ -1328,6 +1339,7 @@ static int average_launch(dpwa_learner *l, const AvgPlan &p, hipStream_t s)
 static int average_impl(dpwa_learner *l, void *flat, double loss, const double *loss_dev, hipStream_t s,
                         bool write_through)
 {
+    TraceRange tr("dpwa.average");
     AvgPlan p;
     int rc = average_prepare(l, flat, loss, loss_dev, s, write_through, p);
     if (rc) return rc;
@@ -1562,7 +1574,8 @@ int dpwa_learner_window_hits(dpwa_learner *l, uint32_t *hits)
     if (l->window_src) {   // check the window open now (or closed, not yet checked); keep its samples
         hipStream_t s = l->window_stream;
         HIP_TRY(launch_window_roll(l->window_src, nullptr, (int64_t)l->payload_bytes, l->window_sample,
-                                   &l->ctl->window_dirty, &l->ctl->window_hits, l->window_host_dev, l->window_gen, s));
+                                   &l->ctl->window_dirty, &l->ctl->window_hits, l->window_host_dev, l->window_gen, 0,
+                                   s));
         HIP_TRY(hipStreamSynchronize(s));
     }
     *hits = __atomic_load_n(l->window_host, __ATOMIC_ACQUIRE);

@@ -251,6 +251,7 @@ static int wait_pull(dpwa_node *n, int *state)
 // (conn.py:311-313) -- and never as a reply with data.
 static int fetch_loop(dpwa_node *n, int flags, dpwa_stream_t stream, bool rescue)
 {
+    TraceRange tr(rescue ? "dpwa.fetch_loop.rescue" : "dpwa.fetch_loop");
     int attempts = 0;
     int rc = DPWA_OK;
     while (attempts < kMaxFetchAttempts) {
@@ -373,6 +374,7 @@ int dpwa_node_publish(dpwa_node *n, const void *flat, double loss, const double 
                       dpwa_stream_t stream)
 {
     if (!n || !n->learner) return set_error(DPWA_ERR_STATE, "dpwa_node_publish: node not bound");
+    TraceRange tr("dpwa.publish");
     if (n->awaiting_lerp) {   // update_wait() was not followed by a lerp: abandon that fetch
         dpwa_learner_cancel(n->learner);
         n->awaiting_lerp = false;
@@ -415,6 +417,7 @@ int dpwa_node_gate(dpwa_node *n, int flags, dpwa_stream_t stream, int *fetching)
 int dpwa_node_update_send(dpwa_node *n, const void *flat, double loss, const double *loss_dev, int flags,
                           dpwa_stream_t stream, int *fetching)
 {
+    TraceRange tr("dpwa.update_send");
     int rc = dpwa_node_publish(n, flat, loss, loss_dev, flags, stream);
     if (rc) return rc;
     return dpwa_node_gate(n, flags, stream, fetching);
@@ -449,6 +452,7 @@ int dpwa_node_update_wait(dpwa_node *n, double loss, const double *loss_dev, int
                           int *peer)
 {
     if (!n || !n->learner || !peer) return set_error(DPWA_ERR_STATE, "dpwa_node_update_wait: node not bound");
+    TraceRange tr("dpwa.update_wait");
     if (resident_slot(n->learner) >= 0)
         return set_error(DPWA_ERR_STATE, "dpwa_node_update_wait: a resident node averages with update_wait_average");
     int rc = finish_fetch(n, flags, stream, peer);
@@ -490,6 +494,7 @@ int dpwa_node_update_wait_average(dpwa_node *n, void *flat, double loss, const d
                                   dpwa_stream_t stream, int *peer)
 {
     if (!n || !n->learner || !peer) return set_error(DPWA_ERR_STATE, "dpwa_node_update_wait_average: node not bound");
+    TraceRange tr("dpwa.update_wait_average");
     int rc = finish_fetch(n, flags, stream, peer);
     if (rc) return rc;
     const bool resident = resident_slot(n->learner) >= 0;
@@ -513,6 +518,7 @@ int dpwa_node_update_wait_average_many(dpwa_node *const *nodes, void *const *fla
 {
     if (count < 0 || (count > 0 && (!nodes || !flats || !loss || !peers)))
         return set_error(DPWA_ERR_ARG, "dpwa_node_update_wait_average_many: bad arguments");
+    TraceRange tr("dpwa.update_wait_average_many");
     std::vector<dpwa_learner *> ls;
     std::vector<void *> fl;
     std::vector<double> lo;

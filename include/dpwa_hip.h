@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DPWA_ABI_VERSION 7
+#define DPWA_ABI_VERSION 8
 
 #define DPWA_OK 0
 #define DPWA_ERR_ARG (-1)     /* bad argument (API misuse)                          */
@@ -91,6 +91,15 @@ typedef struct dpwa_interp {
 
 const char *dpwa_last_error(void);
 int dpwa_abi_version(void);
+
+/* roctx ranges on the round (the reference's LOGGER.debug sites dpwa.py:119,152-153,
+ * conn.py:242-243,296).  On only when DPWA_ROCTX=1 is set when the library loads: then
+ * dpwa.update_send / dpwa.publish / dpwa.fetch_loop / dpwa.update_wait_average / dpwa.average
+ * (and the learner's publish) are pushed as ranges that `rocprofv3 --marker-trace` records.
+ * dpwa_trace_push/pop let the layer above add its own (no-ops when off).  ABI version 8. */
+int dpwa_trace_enabled(void);
+int dpwa_trace_push(const char *name);
+int dpwa_trace_pop(void);
 
 /* ------------------------------------------------------------------------------------
  * Stateless kernels (the fused replacements of the ATen mul/mul/add behind pytorch.py:68)

@@ -109,3 +109,23 @@ class Hold:
                                       "deadline (spin rate %.3g cycles/s): the held pull may have landed before it "
                                       "was judged" % (1e3 * held, 1e3 * waited_s, TIMEOUT_MS, Hold.rate))
         return held
+
+
+GUARD_SAMPLES = 4096
+
+
+def guard_words(n16, gen, samples=GUARD_SAMPLES):
+    """The 16-B words the reuse / window guard compares at publish generation `gen` (a host
+    restatement of kernels.hip guard_offset): word base(k) + gen mod W, base(k) = k(n16-1)/(s-1),
+    W the widest gap between bases; every word is covered once in any W consecutive generations."""
+    s = min(n16, samples)
+    if s <= 1:
+        return {0}
+    widest = (n16 - 1 + s - 2) // (s - 1)
+    r = gen % widest
+    return {(k * (n16 - 1) // (s - 1) + r) % n16 for k in range(s)}
+
+
+def guard_period(n16, samples=GUARD_SAMPLES):
+    s = min(n16, samples)
+    return 1 if s <= 1 else (n16 - 1 + s - 2) // (s - 1)

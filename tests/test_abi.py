@@ -1,11 +1,14 @@
 """The C-ABI library: loads, exports every symbol include/dpwa_hip.h declares, and its
 structs match the header.  No compute calls (CPU container, no GPU)."""
 import ctypes
+import os
 import re
 
 import torch
 
 from dpwa_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_library_loads_and_abi_version():
@@ -70,3 +73,22 @@ def test_binding_arity_matches_header_declarations():
         count = 0 if params in ("", "void") else params.count(",") + 1
         assert name in _lib.SIGNATURES, name
         assert len(_lib.SIGNATURES[name]) == count, (name, count, len(_lib.SIGNATURES[name]))
+
+
+def test_trace_switch_is_read_at_load():
+    """roctx ranges (include/dpwa_hip.h dpwa_trace_*): off unless DPWA_ROCTX=1 when the library
+    loads; on, push/pop go through the profiler SDK's roctx (no-ops without a profiler), and the
+    Python layer's switch follows the same variable.  Separate processes: the switch is fixed at load."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from dpwa_amd import _lib; lib = _lib.load(); "
+            "print(lib.dpwa_trace_enabled(), lib.dpwa_trace_push(b'x'), lib.dpwa_trace_pop(), int(_lib.TRACE))"
+            % ROOT)
+    outs = []
+    for on in ("0", "1"):
+        env = dict(os.environ, DPWA_ROCTX=on)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+        assert r.returncode == 0, r.stderr
+        outs.append(r.stdout.split())
+    assert outs[0] == ["0", "0", "0", "0"]
+    assert outs[1] == ["1", "0", "0", "1"], outs[1]

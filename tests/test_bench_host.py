@@ -87,27 +87,33 @@ def test_partial_line_keeps_the_contract_keys():
     assert out["n_gpus"] == 8 and out["steps"] == 20 and out["value"] is None
 
 
-def _watchdog_child(held, rc):
+def _watchdog_child(held, rc, detail=None):
     """A process whose watchdog overruns a 0.05 s phase after hold(held, rc)."""
     import subprocess
+    env = dict(os.environ)
+    if detail:
+        env["DPWA_BENCH_DETAIL"] = str(detail)
     code = ("import sys, time, json; sys.path.insert(0, %r); import bench\n"
             "wd = bench.Watchdog(bench.parse(['--gpus', '1']), 1, 0)\n"
             "wd.hold(%s, %s)\n"
             "wd.enter('dist round sweep 7000000000 bf16', 0.05)\n"
             "time.sleep(30)\n" % (ROOT, held, rc))
-    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, env=env)
 
 
-def test_overrun_after_the_measurement_prints_the_finished_line():
+def test_overrun_after_the_measurement_prints_the_finished_line(tmp_path):
     """An overrun in the sweeps (after the timed measurement) prints the line built so far with
-    the error added and exits with the run's own status (0, or 1 for a failed parity check)."""
+    the error added and exits with the run's own status (0, or 1 for a failed parity check); the
+    sweep rows measured so far are in the detail file the line names."""
     import json
-    p = _watchdog_child("{'value': 5200.0, 'round_sweep': [{'numel': 11173962, 'value': 5100.0}]}", 0)
+    det = tmp_path / "detail.json"
+    p = _watchdog_child("{'value': 5200.0, 'round_sweep': [{'numel': 11173962, 'value': 5100.0}]}", 0, det)
     assert p.returncode == 0, p.stderr
     lines = [x for x in p.stdout.splitlines() if x.strip()]
     assert len(lines) == 1
     d = json.loads(lines[0])
-    assert d["value"] == 5200.0 and d["round_sweep"][0]["value"] == 5100.0
+    assert d["value"] == 5200.0 and "round_sweep" not in d and d["detail"] == str(det)
+    assert json.loads(det.read_text())["round_sweep"][0]["value"] == 5100.0
     assert "overran" in d["error"] and d["phase"].startswith("dist round sweep")
     p = _watchdog_child("None", 1)           # a rank other than 0 (no line), parity failed
     assert p.returncode == 1 and not p.stdout.strip()
@@ -168,3 +174,78 @@ def test_self_peer_config_is_the_reference_schema(tmp_path):
     nodes = DpwaConfiguration(str(cfg)).get_nodes()
     assert [n["name"] for n in nodes] == ["w1", "w1-self"]
     assert {(n["host"], n["port"]) for n in nodes} == {("127.0.0.1", 45123)}
+
+
+def _worst_case_result(world):
+    """A full result as large as the N>1 run can make it: every parity transport, every trial
+    key, an xGMI block with the relay, long notes and sweeps, a CPU baseline with rows."""
+    import bench
+    note = "x" * 900
+    parity = {t: True for t in bench.parity_transports(world)}
+    parity.update({"extra/transport-%02d" % i: (i % 3 != 0) for i in range(40)})
+    parity["workload"] = note
+    sweep = [{"numel": 7_000_000_000, "dtype": "bf16", "value": 1.0, "note": note} for _ in range(12)]
+    sb = bench.scaling_basis(world, 1, "write-through", 20.0 * world, 0.001, 5000.0,
+                             {"gossip_rounds_per_s": 800.0, "ms_per_step": 1.2, "compute_only_ms_per_step": 1.19,
+                              "gossip_overhead_frac": 0.008})
+    return {**bench.base_line(bench.parse(["--gpus", str(world)]), world),
+            "value": 1234.5, "ms_per_step": 0.5, "value_cold": {"value": 1000.0, "note": note},
+            "scaling_basis": sb, "gossip_rounds_per_s": 1.0, "gossip_rounds_per_s_per_learner": 1.0,
+            "averagings": 20, "round_sweep": sweep, "warmup_rounds": {"note": note},
+            "roofline": {"bound": "hbm", "achieved": 6000.0, "peak": 8000.0, "unit": "GB/s", "frac": 0.75,
+                         "traffic": 1.0e8, "traffic_x": 1.0, "bytes_per_launch": 178_783_392, "kernel": note,
+                         "avg_launch_us": 28.0, "in_loop_frac": 0.8, "mix_ceiling_frac": 0.77,
+                         "size_sweep": sweep, "in_loop": {"note": note}, "mix_ceiling": {"note": note}},
+            "config": {"workload": note, "numel": 11_173_962, "publish": "write-through", "peer": note,
+                       "loop_order": note, "learners": world},
+            "cpu_baseline": {"value": 2.4, "unit": "GB/s", "cores": 2, "kind": "port", "ms_per_round": 109.7,
+                             "sample": note, "rows": sweep, "restatement_rows": sweep, "phases_note": note},
+            "parity": parity, "parity_of_timed_transport": {"transport": "lockstep/copy", "ok": True},
+            "pull_trials_gbs": {"t%d" % i: [1.0] * 10 for i in range(30)},
+            "pull_choice": {"chosen": "relay-avg:128", "rule": note},
+            "trial_errors": {"t%d" % i: note for i in range(30)},
+            "xgmi": {"bytes_per_pull": 1, "avg_pull_us": 2.0, "achieved_gbs_per_pull": 50.0, "peak_gbs": 76.8,
+                     "frac": 0.6, "ranks_share_device": False, "note": note,
+                     "relay": {"frac": 0.5, "note": note}},
+            "overlap": {"note": note}, "secondary_publish": {"note": note}, "adapter_loop": {"note": note},
+            "co_resident_pair": {"note": note}, "publish_fallback": note}
+
+
+def test_result_line_is_bounded_scalar_and_keeps_the_headline():
+    """The line the driver parses (round 5's was cut at 21.7 KB): at most LINE_MAX bytes for the
+    largest result either N can build, scalar blocks only, the headline figures kept."""
+    import json
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    for world in (1, 2, 8):
+        full = _worst_case_result(world)
+        line = json.dumps(bench.compact_line(full, "gpurun_out/bench_detail_n%d.json" % world))
+        assert len(line.encode()) <= bench.LINE_MAX, (world, len(line))
+        d = json.loads(line)
+        assert d["value"] == 1234.5 and d["value_cold"] == 1000.0 and d["detail"].endswith(".json")
+        assert d["roofline"]["frac"] == 0.75 and d["roofline"]["traffic_x"] == 1.0
+        assert d["cpu_baseline"]["value"] == 2.4 and d["cpu_baseline"]["cores"] == 2
+        assert d["parity_of_timed_transport"]["ok"] is True
+        assert d["scaling_basis"]["raw"]["gossip_rounds_per_s"] == 20000.0 * world
+        for block in ("roofline", "config", "cpu_baseline", "xgmi"):
+            if block in d:
+                assert not any(isinstance(v, (dict, list)) for v in d[block].values()), block
+        assert "round_sweep" not in d and "adapter_loop" not in d
+
+
+def test_result_line_from_the_committed_round5_line():
+    """Round 5's own 21.7 KB line (profiles/r05q_bench.json), compacted: within the bound."""
+    import json
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    path = os.path.join(ROOT, "profiles", "r05q_bench.json")
+    if not os.path.exists(path):
+        return
+    full = json.load(open(path))
+    d = bench.compact_line(full, "x.json")
+    assert len(json.dumps(d)) <= 4096, len(json.dumps(d))
+    assert d["value"] == full["value"] and d["roofline"]["frac"] == full["roofline"]["frac"]
+    assert d["cpu_baseline"]["value"] == full["cpu_baseline"]["value"]
+    assert d["value_cold"] == full["value_cold"]["value"]

@@ -18,6 +18,7 @@ from dpwa_amd import DpwaConnection, DpwaPyTorchAdapter, _lib
 from dpwa_amd.group import LocalGroup
 from oracle import gossip as ogossip
 from oracle import lerp as olerp
+from tests.helpers import guard_period, guard_words
 from tests.test_gpu_kernels import from_u16, to_u16
 
 pytestmark = pytest.mark.gpu
@@ -436,19 +437,17 @@ def test_resident_window_guard_catches_data_writes(tmp_path, many):
 def test_resident_window_guard_samples_and_tail_bytes(tmp_path):
     """The window guard's sampling on a model larger than its 4096 words: ragged bf16
     (100003 elements: 12500 16-B words and 6 tail bytes), connection level with the guard set
-    through the C ABI.  A write to the tail bytes or to a sampled word is caught (window_hits
-    grows, the next update_send raises), a write to a word no sample covers is not -- the
-    documented limit -- and rounds with no write stay clean.  Writes go through a second view of
-    the resident memory, so no version counter of conn.parameters moves."""
+    through the C ABI.  A write to the tail bytes or to a word sampled at that publish's
+    generation is caught (window_hits grows, the next update_send raises), a write to a word that
+    generation's samples miss is not -- the samples move on by one word each publish, so a later
+    window covers it (next test) -- and rounds with no write stay clean.  Writes go through a
+    second view of the resident memory, so no version counter of conn.parameters moves."""
     from dpwa_amd.devview import device_tensor
     names = ["t0", "t1"]
     cfg = tmp_path / "tail.yaml"
     _write_cfg(cfg, names, 1.0, "constant")
     n = 100_003
     n16 = n * 2 // 16
-    samples = 4096
-    sampled = {(k * (n16 - 1) // (samples - 1)) for k in range(samples)}
-    unsampled = next(w for w in range(1, n16) if w not in sampled)
     group = LocalGroup()
     conns = [DpwaConnection(names[g], str(cfg), seed=60 + g, group=group) for g in range(2)]
     for g in range(2):
@@ -460,27 +459,38 @@ def test_resident_window_guard_samples_and_tail_bytes(tmp_path):
         _lib.call("dpwa_learner_window_hits", c._learner.handle, ctypes.byref(h))
         return h.value
 
+    def gen(c):
+        v = ctypes.c_uint64()
+        _lib.call("dpwa_learner_version", c._learner.handle, ctypes.byref(v))
+        return v.value
+
     def round_(write=None):
         for c in conns:
             c.update_send(c.parameters, 1.0)
         if write is not None:
             p = conns[1].parameters
             alias = device_tensor(p.data_ptr(), n, torch.bfloat16, DEV)    # its own version counter
-            alias[write] += 1.0
+            alias[write(gen(conns[1]))] += 1.0
             del alias
         for c in conns:
             c.update_wait_average(c.parameters, 1.0)
+
+    def sampled(g):
+        return sorted(guard_words(n16, g))[1] * 8 + 3                      # inside a word sampled at g
+
+    def unsampled(g):
+        return next(w for w in range(1, n16) if w not in guard_words(n16, g)) * 8 + 5
 
     round_()
     round_()
     assert [hits(c) for c in conns] == [0, 0]
     expect = 0
-    for elem, caught in ((n - 1, True),                                  # a tail byte
-                         (sorted(sampled)[1] * 8 + 3, True),              # inside a sampled word
-                         (unsampled * 8 + 5, False)):                     # a word no sample covers
+    for elem, caught in ((lambda g: n - 1, True),                        # a tail byte
+                         (sampled, True),
+                         (unsampled, False)):
         round_(write=elem)
         expect += caught
-        assert hits(conns[1]) == expect and hits(conns[0]) == 0, elem
+        assert hits(conns[1]) == expect and hits(conns[0]) == 0, caught
         conns[0].update_send(conns[0].parameters, 1.0)
         if caught:
             with pytest.raises(_lib.DpwaError, match="written between update_send and update_wait"):
@@ -493,3 +503,49 @@ def test_resident_window_guard_samples_and_tail_bytes(tmp_path):
     torch.cuda.synchronize()
     for c in conns:
         c.close()
+
+
+def test_resident_window_guard_rotation_catches_a_fixed_word(tmp_path):
+    """A loop that writes the same 16-B word in every send -> wait window (a word the first
+    window's samples miss): the window guard's samples move on by one word per publish, so the
+    window of publish generation g is caught exactly when the word is among generation g's
+    samples -- the first within W = ceil((n16-1)/4095) windows (4 here) -- and each caught window
+    makes the next update_send raise once."""
+    from dpwa_amd.devview import device_tensor
+    names = ["t0", "t1"]
+    cfg = tmp_path / "rot.yaml"
+    _write_cfg(cfg, names, 1.0, "constant")
+    n = 100_003
+    n16 = n * 2 // 16
+    W = guard_period(n16)
+    group = LocalGroup()
+    conns = [DpwaConnection(names[g], str(cfg), seed=90 + g, group=group) for g in range(2)]
+    for g in range(2):
+        conns[g].make_resident(torch.randn(n, device=DEV).to(torch.bfloat16))
+        _lib.call("dpwa_learner_set_reuse_guard", conns[g]._learner.handle, 1)
+    v = ctypes.c_uint64()
+    _lib.call("dpwa_learner_version", conns[1]._learner.handle, ctypes.byref(v))
+    w = next(x for x in range(1, n16) if x not in guard_words(n16, v.value + 1))
+    got, want = [], []
+    h = ctypes.c_uint32()
+    for r in range(2 * W + 1):
+        for c in conns:
+            try:
+                c.update_send(c.parameters, 1.0)
+            except _lib.DpwaError:            # the last window was caught: reported once
+                c.update_send(c.parameters, 1.0)
+        _lib.call("dpwa_learner_version", conns[1]._learner.handle, ctypes.byref(v))
+        want.append(int(w in guard_words(n16, v.value)))
+        p = conns[1].parameters
+        alias = device_tensor(p.data_ptr(), n, torch.bfloat16, DEV)
+        alias[w * 8 + 2] += 1.0
+        del alias
+        for c in conns:
+            c.update_wait_average(c.parameters, 1.0)
+        _lib.call("dpwa_learner_window_hits", conns[1]._learner.handle, ctypes.byref(h))
+        got.append(h.value)
+    torch.cuda.synchronize()
+    for c in conns:
+        c.close()
+    assert np.diff([0] + got).tolist() == want, (got, want)
+    assert want[0] == 0 and 1 <= want.index(1) <= W and sum(want) >= 2

@@ -11,6 +11,7 @@ import torch
 from dpwa_amd import DpwaPyTorchAdapter
 from dpwa_amd.group import LocalGroup
 from oracle import lerp as olerp
+from tests.helpers import guard_period, guard_words
 from tests.test_gpu_gossip import DEV, Net, load_flat, write_cfg
 
 pytestmark = pytest.mark.gpu
@@ -125,11 +126,13 @@ def test_reuse_guard_compares_the_tail_bytes(tmp_path):
 
 def _sparse_round(tmp_path, write_through):
     """Learner a writes ONE element through param.data between update_wait and update_send, at a
-    16-B word the guard does not sample (n16 = 25,008 words, samples every ~6.1 words: word 3 lies
-    between samples 0 and 1).  Learner b averages with constant 1.0, so after the next round b's
+    16-B word the guard does not sample at that publish (n16 = 25,008 words, samples every ~6.1
+    words, moved by the generation: the second publish compares words 2, 8, 14, ... -- word 3 is
+    not one of them).  Learner b averages with constant 1.0, so after the next round b's
     parameters ARE the snapshot a served.  Returns (b's element, the written value, a's element
     before the write, reuse guard hits of a)."""
     n = 100_032
+    assert 3 not in guard_words(n * 4 // 16, 2)
     rng = np.random.default_rng(31)
     init = rng.standard_normal((2, n)).astype(np.float32)
     cfg = tmp_path / ("sparse_%d.yaml" % write_through)
@@ -197,3 +200,43 @@ def test_rehomed_parameter_warns_once(tmp_path, caplog):
     assert len(warned) == 1 and "write_through=False" in warned[0].getMessage()
     for ad in ads:
         ad.connection.close()
+
+
+def test_reuse_guard_rotation_catches_a_fixed_unsampled_word(tmp_path):
+    """The guard's samples move with the publish generation (kernels.hip guard_offset), so a loop
+    that writes the same word through param.data every round -- a word the first guarded publish
+    does not sample -- is caught exactly at the publishes whose samples cover it, the first within
+    W = ceil((n16-1)/4095) publishes (7 here).  Round r's publish is generation r+1; each caught
+    publish copies the parameters in full, so the next round starts from an equal snapshot."""
+    n = 100_032
+    n16 = n * 4 // 16
+    W = guard_period(n16)
+    w = next(x for x in range(1, n16) if x not in guard_words(n16, 2))
+    k = w * 4 + 1
+    cfg = tmp_path / "rotate.yaml"
+    write_cfg(cfg, ["a", "b"], 1.0, "constant", 0.0, 0.5)
+    group = LocalGroup()
+    rng = np.random.default_rng(9)
+    nets, ads = [], []
+    for g, nm in enumerate(("a", "b")):
+        net = Net([(n,)]).to(DEV)
+        load_flat(net, rng.standard_normal(n).astype(np.float32))
+        nets.append(net)
+        ads.append(DpwaPyTorchAdapter(net, nm, str(cfg), seed=80 + g, group=group, write_through=True))
+    got, want = [], []
+    for r in range(2 * W + 1):
+        before = ads[0].reuse_guard_hits
+        for ad in ads:
+            ad.update_send(1.0)
+        got.append(ads[0].reuse_guard_hits - before)
+        want.append(int(r >= 1 and w in guard_words(n16, r + 1)))
+        for ad in ads:
+            ad.update_wait(1.0)
+        with torch.no_grad():
+            nets[0].p0.data[k] += 1.0          # the same element every round, no version counter moves
+    for ad in ads:
+        ad.connection.close()
+    assert got == want, (got, want)
+    first = want.index(1)
+    assert 1 <= first <= W, (first, W)
+    assert sum(want) >= 2                    # and again one period later

@@ -58,3 +58,35 @@ def test_gossip_board_under_asan_ubsan(tmp_path):
     r = subprocess.run([exe, "4", "2000"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "board stress ok" in r.stdout
+
+
+def _tsan_build(tmp_path):
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    exe = str(tmp_path / "node_tsan")
+    srcs = ["dpwa_amd/csrc/node.cpp", "dpwa_amd/csrc/sched.cpp", "dpwa_amd/csrc/trace.cpp",
+            "tests/native/fake_learner.cpp", "tests/native/node_tsan.cpp"]
+    cmd = [gxx, "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-fno-omit-frame-pointer", "-I",
+           os.path.join(ROOT, "include"), *[os.path.join(ROOT, s) for s in srcs], "-o", exe, "-ldl", "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0 and "tsan" in r.stderr:
+        pytest.skip("TSan runtime not installed: " + r.stderr[-200:])
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def test_node_and_scheduler_under_tsan(tmp_path):
+    """SURVEY §5 race detection: node.cpp + sched.cpp under ThreadSanitizer (the counterpart of the
+    reference's races at conn.py:106, 240, 259, 313).  Four threads each drive their own group of
+    four lock-step nodes over the host-only learner (tests/native/node_tsan.cpp: stalls, rescue
+    lanes, faults, flow control, the Bernoulli gate) for 2,000 rounds, with the roctx trace hooks
+    switched on -- the ABI's promise that calls are reentrant per handle.  TSan must stay silent;
+    the control (two threads bumping one plain int) shows the build is instrumented."""
+    exe = _tsan_build(tmp_path)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1", DPWA_ROCTX="1")
+    r = subprocess.run([exe, "racy"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "data race" in r.stderr, (r.returncode, r.stderr[-2000:])
+    r = subprocess.run([exe, "4", "4", "2000"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "node tsan ok" in r.stdout and "8000 rounds" in r.stdout

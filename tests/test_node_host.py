@@ -32,10 +32,10 @@ def node_stress(tmp_path_factory):
     if gxx is None:
         pytest.skip("no g++")
     exe = str(tmp_path_factory.mktemp("node") / "node_stress")
-    srcs = ["dpwa_amd/csrc/node.cpp", "dpwa_amd/csrc/sched.cpp", "tests/native/fake_learner.cpp",
-            "tests/native/node_stress.cpp"]
+    srcs = ["dpwa_amd/csrc/node.cpp", "dpwa_amd/csrc/sched.cpp", "dpwa_amd/csrc/trace.cpp",
+            "tests/native/fake_learner.cpp", "tests/native/node_stress.cpp"]
     cmd = [gxx, "-std=c++17", "-O1", "-g", *SAN, "-I", os.path.join(ROOT, "include"),
-           *[os.path.join(ROOT, s) for s in srcs], "-o", exe, "-lpthread"]
+           *[os.path.join(ROOT, s) for s in srcs], "-o", exe, "-ldl", "-lpthread"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     if r.returncode != 0 and ("asan" in r.stderr or "ubsan" in r.stderr):
         pytest.skip("sanitizer runtime not installed: " + r.stderr[-200:])

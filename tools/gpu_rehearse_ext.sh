@@ -14,7 +14,7 @@ for N in 8 2; do
       > gpurun_out/ext_${TAG}_n$N.json 2> gpurun_out/ext_${TAG}_n$N.err
   rc=$?
   echo "N=$N rc=$rc $(( $(date +%s) - t0 ))s stdout lines: $(wc -l < gpurun_out/ext_${TAG}_n$N.json)"
-  python3 -c "import json;d=json.load(open('gpurun_out/ext_${TAG}_n$N.json'));print(d['value'],d['pull_choice'],{k:v for k,v in d['parity'].items() if k!='workload'}, d['scaling_basis']['raw'], d['scaling_basis']['weak'])" || exit 1
+  python3 tools/check_line.py gpurun_out/ext_${TAG}_n$N.json || exit 1
   [ $rc -ne 0 ] && exit 1
 done
 exit 0
