@@ -1303,7 +1303,8 @@ hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *c
 // The sampled words move with the generation (guard_offset): sample k of generation g is word
 // base(k) + g mod W, W the widest gap between two bases, so over any W consecutive publishes every
 // word of the parameters is compared once -- a sparse write through `param.data` that the samples
-// of one publish miss is caught within W = ceil((n16-1)/4095) publishes, at the same per-publish cost.
+// of one publish miss is caught within W = ceil((n16-1)/4095) publishes, at the same per-publish
+// cost.  The first and the last word (and the tail bytes) are compared at every publish.
 constexpr int kGuardSamples = 4096;
 constexpr int kGuardWave = 64;
 constexpr int kGuardCopyBlocks = 256;
@@ -1341,6 +1342,16 @@ __global__ __launch_bounds__(kGuardWave) void k_guard_compare(const char *__rest
     }
     if (blockIdx.x == 0 && threadIdx.x < (nbytes & 15))
         diff |= flat[(n16 << 4) + threadIdx.x] != payload[(n16 << 4) + threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x < 2 && n16 > 0) {   // the first and the last word, always
+        const int64_t o = threadIdx.x ? (n16 - 1) << 4 : 0;
+        if (VEC) {
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(flat + o);
+            const u32x4 b = *reinterpret_cast<const u32x4 *>(payload + o);
+            diff |= (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
+        } else {
+            for (int j = 0; j < 16; ++j) diff |= flat[o + j] != payload[o + j];
+        }
+    }
     diff = __syncthreads_or(diff);
     if (diff && threadIdx.x == 0) {
         const int32_t old = atomicExch(dirty, gen);
@@ -1395,8 +1406,9 @@ hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes,
 // samples saved when it was published (k_guard_compare's offsets of that publish's generation
 // `gen`), then the samples of the payload published now (generation `cur_gen`, the offsets moved on
 // by one) are saved in their place.  Each lane owns one sample, so the compare and the save of a
-// sample are in one lane, in order.  `old` NULL: save only; `cur` NULL: compare only.
-static_assert(kWindowSampleBytes == (kGuardSamples + 1) * 16, "window sample layout");
+// sample are in one lane, in order.  `old` NULL: save only; `cur` NULL: compare only.  Layout of
+// `sample`: kGuardSamples words, the tail bytes, the first word, the last word.
+static_assert(kWindowSampleBytes == (kGuardSamples + 3) * 16, "window sample layout");
 
 __global__ __launch_bounds__(kGuardWave) void k_window_roll(const char *__restrict__ old, const char *__restrict__ cur,
                                                             int64_t nbytes, char *__restrict__ sample,
@@ -1409,6 +1421,10 @@ __global__ __launch_bounds__(kGuardWave) void k_window_roll(const char *__restri
     const bool tail = blockIdx.x == 0 && threadIdx.x < (nbytes & 15);
     char *const tail_sample = sample + kGuardSamples * 16 + threadIdx.x;
     u32x4 *const sk = reinterpret_cast<u32x4 *>(sample) + k;
+    // lanes 0 and 1 of workgroup 0 also own the first and the last word (fixed, every window)
+    const bool edge = blockIdx.x == 0 && threadIdx.x < 2 && n16 > 0;
+    const int64_t edge_off = threadIdx.x ? (n16 - 1) << 4 : 0;
+    u32x4 *const se = reinterpret_cast<u32x4 *>(sample) + kGuardSamples + 1 + threadIdx.x;
     int diff = 0;
     if (old) {
         if (k < samples) {
@@ -1417,10 +1433,16 @@ __global__ __launch_bounds__(kGuardWave) void k_window_roll(const char *__restri
             diff = (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
         }
         if (tail) diff |= old[(n16 << 4) + threadIdx.x] != *tail_sample;
+        if (edge) {
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(old + edge_off);
+            const u32x4 b = *se;
+            diff |= (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
+        }
     }
     if (cur) {
         if (k < samples) *sk = *reinterpret_cast<const u32x4 *>(cur + guard_offset(k, samples, n16, (uint32_t)cur_gen));
         if (tail) *tail_sample = cur[(n16 << 4) + threadIdx.x];
+        if (edge) *se = *reinterpret_cast<const u32x4 *>(cur + edge_off);
     }
     if (!old) return;
     diff = __syncthreads_or(diff);

@@ -145,7 +145,7 @@ hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes,
 // `gen`, counting the window in *hits and mirroring the count into the host-mapped word *host --
 // and saves the samples of the payload published now (`cur`) into `sample` (kWindowSampleBytes).
 // Payloads 16-B aligned; either may be NULL.
-constexpr int64_t kWindowSampleBytes = (4096 + 1) * 16;
+constexpr int64_t kWindowSampleBytes = (4096 + 3) * 16;   // samples, tail bytes, first and last word
 hipError_t launch_window_roll(const char *old, const char *cur, int64_t nbytes, char *sample, int32_t *dirty,
                               uint32_t *hits, uint32_t *host, int32_t gen, int32_t cur_gen, hipStream_t s);
 

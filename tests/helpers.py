@@ -117,13 +117,14 @@ GUARD_SAMPLES = 4096
 def guard_words(n16, gen, samples=GUARD_SAMPLES):
     """The 16-B words the reuse / window guard compares at publish generation `gen` (a host
     restatement of kernels.hip guard_offset): word base(k) + gen mod W, base(k) = k(n16-1)/(s-1),
-    W the widest gap between bases; every word is covered once in any W consecutive generations."""
+    W the widest gap between bases, plus the first and the last word at every generation; every
+    word is covered in any W consecutive generations."""
     s = min(n16, samples)
     if s <= 1:
-        return {0}
+        return {0, max(0, n16 - 1)}
     widest = (n16 - 1 + s - 2) // (s - 1)
     r = gen % widest
-    return {(k * (n16 - 1) // (s - 1) + r) % n16 for k in range(s)}
+    return {(k * (n16 - 1) // (s - 1) + r) % n16 for k in range(s)} | {0, n16 - 1}
 
 
 def guard_period(n16, samples=GUARD_SAMPLES):

@@ -2,6 +2,8 @@
 # Round-6 evidence script: one parameterised GPU session (same steps as gpu_r05.sh, plus "line" after a bench).
 #   tools/gpu_r06.sh <tag> <steps...>
 # steps: smoke | tests:<pytest-args> | bench[:<bench args>] | rocprof[:<bench args>] | pmc:<cold_sweep args>
+#        | marker[:<bench args>]  (DPWA_ROCTX=1 under rocprofv3 --marker-trace --kernel-trace)
+#        | markerpy:<repo script + args>  (the same for a script, then tools/marker_gaps.py)
 #        | rehearse:<N>[ <bench args>]  (the N>1 line self-launched on one GPU over gloo)
 #        | py:<script + args>
 # e.g. gpurun --timeout 1200 -- bash tools/gpu_r06.sh r05b smoke "tests:-m gpu tests" "bench:--steps 20 --warmup 5"
@@ -26,6 +28,11 @@ for step in "$@"; do
       python3 tools/check_line.py "$out/bench_$i.json" >&2 || exit 1 ;;
     rocprof)
       (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$out/rocprof_$i" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" $arg > "$GRAFT_REPO_ROOT/$out/rocprof_bench_$i.json" 2> "$GRAFT_REPO_ROOT/$out/rocprof_bench_$i.err") || { echo "rocprof failed" >&2; tail -40 "$out/rocprof_bench_$i.err" >&2; exit 1; } ;;
+    marker)
+      (cd /tmp && DPWA_ROCTX=1 timeout -k 10 900 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$out/marker_$i" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" $arg > "$GRAFT_REPO_ROOT/$out/marker_bench_$i.json" 2> "$GRAFT_REPO_ROOT/$out/marker_bench_$i.err") || { echo "marker failed" >&2; tail -40 "$out/marker_bench_$i.err" >&2; exit 1; } ;;
+    markerpy)
+      (cd /tmp && DPWA_ROCTX=1 timeout -k 10 600 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$out/markerpy_$i" -o run -- python3 $GRAFT_REPO_ROOT/$arg > "$GRAFT_REPO_ROOT/$out/markerpy_$i.log" 2>&1) || { echo "markerpy failed" >&2; tail -40 "$out/markerpy_$i.log" >&2; exit 1; }
+      python3 tools/marker_gaps.py "$out/markerpy_$i" > "$out/markerpy_${i}_gaps.json" || exit 1 ;;
     pmc)
       for ctr in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$out/pmc_${i}_$ctr" -o run -- python3 "$GRAFT_REPO_ROOT/tools/cold_sweep.py" $arg > "$GRAFT_REPO_ROOT/$out/pmc_${i}_$ctr.log" 2>&1) || { echo "pmc $ctr failed" >&2; tail -20 "$out/pmc_${i}_$ctr.log" >&2; exit 1; }
