@@ -8,6 +8,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -Iinclude -o tools/product_tune
 //        tools/product_tune.hip -Ldpwa_amd -ldpwa_hip -Wl,-rpath,'$ORIGIN/../dpwa_amd'
 // Run:   DPWA_LERP_POLICY=<p> tools/product_tune [numel] [rounds]
+//        (TUNE_DUAL=1: the write-through rows only; TUNE_ONLY="name;name;...": those rows, in that order)
 #pragma clang fp contract(off)
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
@@ -90,6 +91,56 @@ __global__ __launch_bounds__(64) void k_dual(Args a, float *other)
     const f32x4 r = fa * q + fb * p;
     st<NT | SC1>(DISTINCT ? rsrc(other, off, a.bytes, 1024) : rp, threadIdx.x * 16, r);
     st<SC1>(rsrc(a.snap, off, a.bytes, 1024), threadIdx.x * 16, r);
+}
+
+// The same write-through stream with its two reads by LDS-DMA (`global_load_lds_dwordx4`, no VGPR
+// destination; aux AUXL: 2 = nt): each wave DMAs its 1-KiB span of the peer snapshot and of the
+// parameters into its own LDS, waits for them (vmcnt(0)), reads them back with ds_read_b128, and
+// stores as k_dual.  WAVES one-wave spans per workgroup.  (the one load path
+// the averaging kernel had not tried.)  A span that does not fit whole takes the buffer loads.
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
+typedef __attribute__((address_space(1))) void *gbl_ptr_t;
+
+template <int AUXL, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_dual_glds(Args a)
+{
+    __shared__ f32x4 lds[WAVES][2][64];
+    const int w = WAVES == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int64_t off = ((int64_t)blockIdx.x * WAVES + w) * 1024;
+    if (off >= a.bytes) return;
+    f32x4 q, p;
+    if (off + 1024 <= a.bytes) {
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)((const char *)a.peer + off + lane * 16), (lds_ptr_t)&lds[w][0][0],
+                                         16, 0, AUXL);
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)((const char *)a.param + off + lane * 16),
+                                         (lds_ptr_t)&lds[w][1][0], 16, 0, AUXL);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        q = lds[w][0][lane];
+        p = lds[w][1][lane];
+    } else {
+        q = ld<NT>(rsrc(a.peer, off, a.bytes, 1024), lane * 16);
+        p = ld<NT>(rsrc(a.param, off, a.bytes, 1024), lane * 16);
+    }
+    const f32x4 r = 0.5f * q + 0.5f * p;
+    st<NT | SC1>(rsrc(a.param, off, a.bytes, 1024), lane * 16, r);
+    st<SC1>(rsrc(a.snap, off, a.bytes, 1024), lane * 16, r);
+}
+
+// Control for k_dual_glds: the same multi-wave workgroups with the product's buffer loads into VGPRs.
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_dual_wg(Args a)
+{
+    const int w = WAVES == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t off = ((int64_t)blockIdx.x * WAVES + w) * 1024;
+    if (off >= a.bytes) return;
+    const __amdgpu_buffer_rsrc_t rp = rsrc(a.param, off, a.bytes, 1024);
+    const f32x4 q = ld<NT>(rsrc(a.peer, off, a.bytes, 1024), lane * 16);
+    const f32x4 p = ld<NT>(rp, lane * 16);
+    const f32x4 r = 0.5f * q + 0.5f * p;
+    st<NT | SC1>(rp, lane * 16, r);
+    st<SC1>(rsrc(a.snap, off, a.bytes, 1024), lane * 16, r);
 }
 
 struct BigArgs {         // the same plus padding to the product's kernel-argument size
@@ -201,6 +252,20 @@ int main(int argc, char **argv)
              const void *src[2] = {s.slot + kOff, s.param};
              if (dpwa_stream_mix(dst, 2, src, 2, bytes, st, e0, e1)) { fprintf(stderr, "%s\n", dpwa_last_error()); exit(1); }
          }},
+        {"glds dual in place (nt, 1 wave/WG)", 4.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             hipExtLaunchKernelGGL((k_dual_glds<NT, 1>), dim3(grid), dim3(64), 0, st, e0, e1, 0, args_of(s)); }},
+        {"glds dual in place (default policy, 1 wave/WG)", 4.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             hipExtLaunchKernelGGL((k_dual_glds<0, 1>), dim3(grid), dim3(64), 0, st, e0, e1, 0, args_of(s)); }},
+        {"glds dual in place (nt, 2 waves/WG)", 4.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             hipExtLaunchKernelGGL((k_dual_glds<NT, 2>), dim3((grid + 1) / 2), dim3(128), 0, st, e0, e1, 0, args_of(s)); }},
+        {"glds dual in place (nt, 4 waves/WG)", 4.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             hipExtLaunchKernelGGL((k_dual_glds<NT, 4>), dim3((grid + 3) / 4), dim3(256), 0, st, e0, e1, 0, args_of(s)); }},
+        {"glds dual in place (nt, 8 waves/WG)", 4.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             hipExtLaunchKernelGGL((k_dual_glds<NT, 8>), dim3((grid + 7) / 8), dim3(512), 0, st, e0, e1, 0, args_of(s)); }},
+        {"vgpr dual in place (nt, 4 waves/WG)", 4.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             hipExtLaunchKernelGGL((k_dual_wg<4>), dim3((grid + 3) / 4), dim3(256), 0, st, e0, e1, 0, args_of(s)); }},
+        {"vgpr dual in place (nt, 2 waves/WG)", 4.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+             hipExtLaunchKernelGGL((k_dual_wg<2>), dim3((grid + 1) / 2), dim3(128), 0, st, e0, e1, 0, args_of(s)); }},
         {"bare oop sc1", 3.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
              hipExtLaunchKernelGGL(k_oop<SC1>, dim3(grid), dim3(64), 0, st, e0, e1, 0, args_of(s)); }},
         {"bare oop sc0+sc1", 3.0, [&](const Set &s, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
@@ -222,6 +287,22 @@ int main(int argc, char **argv)
         std::vector<Variant> keep;
         for (auto &v : vs)
             if (v.factor == 4.0) keep.push_back(v);
+        vs.swap(keep);
+    }
+    if (const char *only = getenv("TUNE_ONLY")) {   // ';'-separated name substrings, run in that order
+        std::vector<Variant> keep;
+        std::string list(only);
+        size_t pos = 0;
+        while (pos <= list.size()) {
+            const size_t end = std::min(list.find(';', pos), list.size());
+            const std::string key = list.substr(pos, end - pos);
+            for (auto &v : vs)
+                if (!key.empty() && v.name.find(key) != std::string::npos) {
+                    keep.push_back(v);
+                    break;
+                }
+            pos = end + 1;
+        }
         vs.swap(keep);
     }
     hipStream_t st;
