@@ -239,6 +239,8 @@ def compact_line(full, detail=None):
     pc = full.get("pull_choice")
     if isinstance(pc, dict):
         out["pull"] = pc.get("chosen")
+    if isinstance(full.get("parity_failed"), list):
+        out["parity_failed"] = full["parity_failed"][:24]
     if isinstance(full.get("trial_errors"), dict):
         out["trial_errors"] = sorted(full["trial_errors"])
     if detail:
@@ -2266,10 +2268,14 @@ def main(argv=None):
         if parity is not None:
             out["parity"] = parity
             out["parity_of_timed_transport"] = {"transport": used, "ok": bool(parity.get(used, False))}
+            out["parity_failed"] = sorted(k for k, v in parity.items() if k != "workload" and not v)
     # The sweeps over the north_star sizes come last: their rows go into the line as they are
     # measured, and a watchdog overrun in them prints the line built above (with the rows so
-    # far and the error) and exits as the run would have (1 only for a failed parity check).
-    parity_failed = parity is not None and any(not v for k, v in parity.items() if k != "workload")
+    # far and the error) and exits as the run would have.  Exit status: 1 when the timed
+    # transport itself failed its parity check; a failure of any other transport (left out of
+    # the trials, so never timed) is reported in the line's `parity` and on stderr, status 0, so
+    # the measured, verified line is not discarded with it.
+    parity_failed = parity is not None and not parity.get(used, False)
     size_rows, round_rows = [], []
     if out is not None and not args.no_sweep:
         if world == 1:
@@ -2304,9 +2310,11 @@ def main(argv=None):
     wd.idle()
     progress("done")
     if parity is not None:
-        failed = {k: v for k, v in parity.items() if k != "workload" and not v}
+        failed = sorted(k for k, v in parity.items() if k != "workload" and not v)
         if failed:
-            print("bench.py: parity check FAILED: %s" % failed, file=sys.stderr, flush=True)
+            print("bench.py: parity check FAILED for %s (timed transport %s: %s)"
+                  % (failed, used, "ok" if not parity_failed else "FAILED"), file=sys.stderr, flush=True)
+        if parity_failed:
             sys.exit(1)
 
 

@@ -306,9 +306,16 @@ static void close_endpoint(Endpoint &ep)
 // A rescue lane: where a fetch re-selected after a timed-out pull goes (conn.py:304-309) -- a
 // buffer and a stream of the greatest priority (a hardware queue no stalled normal-priority stream
 // shares), so no stalled pull ahead of it can hold it up.  Lanes are made at first use, up to
-// kMaxRescueLanes and only while the device keeps kRescueReserve free beyond the new buffer; an
-// allocation that fails caps the count where it is (rescue_cap) instead of failing the round.
+// kMaxRescueLanes, only while the device keeps kRescueReserve free beyond the new buffer and all
+// lanes together stay within 1/kRescueShare of the device's memory (7B bf16: two 14 GB lanes on a
+// 288 GB GPU); an allocation that fails caps the count where it is (rescue_cap) instead of failing
+// the round.  Lanes beyond the first kKeepRescueLanes are given back once they have been idle for
+// kLaneIdleRounds fetch rounds (trim_lanes), so a burst of stalled pulls does not hold HBM outside
+// PyTorch's allocator for the rest of the process.
 constexpr int kMaxRescueLanes = 8;
+constexpr int kKeepRescueLanes = 2;
+constexpr uint64_t kLaneIdleRounds = 8;
+constexpr size_t kRescueShare = 8;
 // fetch_state: a backlog on the caller's stream longer than this no longer defers the timeout (a
 // stream that never reaches update_send is stuck, not slow); a probe waits at most kProbeWaitUs
 constexpr int64_t kMaxBacklogMs = 60000;
@@ -321,6 +328,7 @@ struct RescueLane {
     hipEvent_t ev_done = nullptr;       // the last reader of its buffer is done
     bool used = false;                  // a pull was issued into it
     bool read = false;                  // ev_done recorded
+    uint64_t last_round = 0;            // fetch round of its last pull
 };
 
 void destroy_lane(RescueLane &r)
@@ -371,6 +379,7 @@ struct dpwa_learner {
     RescueLane rescue[kMaxRescueLanes];
     int rescue_lanes = 0;
     int rescue_cap = kMaxRescueLanes;   // lowered when a lane's allocation fails
+    uint64_t fetch_rounds = 0;          // first (non-rescue) pulls issued: the lanes' idle clock
     int64_t fetch_issue_ns = 0;         // host time the fetch in flight was issued (its timeout clock)
     // the fetch in flight waits for ev_issue (the caller's stream at update_send): its deadline runs
     // from when that point is reached, not from the host's enqueue (fetch_state)
@@ -1011,7 +1020,8 @@ static int rescue_lane(dpwa_learner *l, int *lane)
     int rc = free_lane(l, lane);
     if (rc || *lane >= 0 || l->rescue_lanes >= l->rescue_cap) return rc;
     size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < l->slot_stride + kRescueReserve) {
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < l->slot_stride + kRescueReserve ||
+        (size_t)(l->rescue_lanes + 1) * l->slot_stride > total_b / kRescueShare) {
         (void)hipGetLastError();
         l->rescue_cap = l->rescue_lanes;
         return DPWA_OK;
@@ -1035,6 +1045,23 @@ static int rescue_lane(dpwa_learner *l, int *lane)
     l->rescue[l->rescue_lanes] = r;
     *lane = l->rescue_lanes++;
     return DPWA_OK;
+}
+
+// Gives back the lanes beyond the first kKeepRescueLanes, last first, once idle for kLaneIdleRounds
+// fetch rounds: their pull landed and the last reader of their buffer is done (event queries, no
+// wait).  Called at a round's first pull, the normal path, where it costs one comparison.
+static void trim_lanes(dpwa_learner *l)
+{
+    while (l->rescue_lanes > kKeepRescueLanes) {
+        const int j = l->rescue_lanes - 1;
+        RescueLane &r = l->rescue[j];
+        if (l->fetch_rounds - r.last_round < kLaneIdleRounds || l->src_stage == 2 + j) return;
+        if (r.used && hipEventQuery(r.ev_landed) != hipSuccess) break;
+        if (r.read && hipEventQuery(r.ev_done) != hipSuccess) break;
+        destroy_lane(r);
+        l->rescue_lanes--;
+    }
+    (void)hipGetLastError();   // a not-ready query leaves no error behind
 }
 
 int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int flags, dpwa_stream_t stream)
@@ -1066,6 +1093,10 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
     l->fetch_issue_ns = now_ns();
     l->fetch_stream = l->side;
     l->issue_evented = false;
+    if (!(flags & DPWA_FETCH_RESCUE)) {
+        l->fetch_rounds++;
+        if (l->rescue_lanes > kKeepRescueLanes) trim_lanes(l);
+    }
     if (flags & DPWA_FETCH_RESCUE) {
         // re-selected after a timed-out pull: a free lane (its own stream and buffer), ordered
         // after the publish of the snapshot (above, local peers) and after the last reader of the
@@ -1092,6 +1123,7 @@ int dpwa_learner_fetch(dpwa_learner *l, int peer_id, uint64_t peer_version, int 
         HIP_TRY(hipEventRecord(r.ev_landed, r.stream));
         HIP_TRY(hipEventRecord(l->ev_fetched, r.stream));
         r.used = true;
+        r.last_round = l->fetch_rounds;
         l->fetch_stream = r.stream;
         l->src = r.buf;
         l->src_copied = true;
@@ -2065,7 +2097,9 @@ int dpwa_learner_rescue_free(dpwa_learner *l, int *free_out)
     if (!l || !free_out) return set_error(DPWA_ERR_ARG, "dpwa_learner_rescue_free: NULL argument");
     DeviceGuard dg(l->device);
     int lane = -1;
-    const int rc = rescue_lane(l, &lane);     // makes a lane now if one is needed and can be made
+    // makes a lane now if one is needed and can be made: at most one allocation per wait (the
+    // node's poll ends as soon as a lane is free); with the lanes at their cap a poll only queries
+    const int rc = rescue_lane(l, &lane);
     *free_out = lane >= 0 ? 1 : 0;
     return rc;
 }

@@ -2,7 +2,7 @@
 GPU): `python bench.py --gpus 2` with no launcher starts torch.distributed.run as a child and
 must print exactly one result line, every parity transport true; an exception injected at the
 end of one transport on one rank must turn into that transport's `false` with the line still
-printed and exit status 1."""
+printed; the exit status is 1 only when the timed transport itself failed."""
 import json
 import os
 import subprocess
@@ -111,9 +111,11 @@ def test_two_ranks_report_scaling_basis_and_a_shared_device_xgmi_line(tmp_path):
 def test_injected_transport_failure_is_isolated(tmp_path):
     # the timed rounds run write-through learners (the default publish form): their transport fails
     rc, lines, err = _bench(tmp_path, {"DPWA_BENCH_INJECT": "lockstep/kernel:256@1:end"})
-    assert rc == 1, err[-3000:]
+    assert rc == 0, err[-3000:]          # the timed transport passed: the verified line stands
+    assert "parity check FAILED for ['lockstep/kernel:256']" in err
     out = _line(lines)
-    assert out["parity"]["lockstep/kernel:256"] is False
+    assert out["parity"]["lockstep/kernel:256"] is False and out["parity_failed"] == ["lockstep/kernel:256"]
+    assert out["parity_of_timed_transport"]["ok"]
     assert all(v for k, v in out["parity"].items() if k != "lockstep/kernel:256")
     assert out["value"] > 0 and not any(k.startswith("kernel") for k in _detail(out)["pull_trials_gbs"])
 
@@ -121,12 +123,14 @@ def test_injected_transport_failure_is_isolated(tmp_path):
 def test_resident_parity_failure_falls_back_to_write_through(tmp_path):
     """If no resident transport passes the parity check (here injected failures in every lock-step
     `+res` transport of a --publish resident run), the timed run uses the verified write-through
-    form, says so in the line, and the run still exits 1 for the failed transports."""
+    form, says so in the line, and reports the failed transports (exit status 0: the timed one
+    passed)."""
     res = ["lockstep/copy+res", "lockstep/kernel:256+res", "lockstep/relay:32+res", "lockstep/relay-avg:32+res",
            "lockstep/relay-avg:32+res+vmm"]
     rc, lines, err = _bench(tmp_path, {"DPWA_BENCH_INJECT": ",".join("%s@1:end" % t for t in res)},
                             args=ARGS + ["--publish", "resident", "--gossip", "lockstep", "--pull", "copy", "--no-cold"])
-    assert rc == 1, err[-3000:]
+    assert rc == 0, err[-3000:]
+    assert "parity check FAILED" in err
     out = _line(lines)
     assert all(out["parity"][t] is False for t in res) and out["parity"]["lockstep/copy"] is True
     assert "publish_fallback" in out and out["config"]["publish"] == "write-through"

@@ -301,6 +301,17 @@ def _stalled_rescue(_rank, tmp, mode):
     nl, cap = ctypes.c_int(), ctypes.c_int()
     _lib.call("dpwa_learner_rescue_lanes", conns[0]._learner.handle, ctypes.byref(nl), ctypes.byref(cap))
     assert (nl.value, cap.value) == ((4, 8) if mode == "grow" else (3, 3)), (nl.value, cap.value)
+    if mode == "grow":
+        # lanes beyond the first two are given back once idle for 8 fetch rounds (learner.cpp
+        # trim_lanes): nine plain rounds later the learner holds two lanes again
+        for r in range(9):
+            for g in range(G):
+                conns[g].update_send(flats[g], 1.0)
+            for g in range(G):
+                conns[g].update_wait_average(flats[g], 1.0)
+        torch.cuda.synchronize()
+        _lib.call("dpwa_learner_rescue_lanes", conns[0]._learner.handle, ctypes.byref(nl), ctypes.byref(cap))
+        assert (nl.value, cap.value) == (2, 8), (nl.value, cap.value)
     for c in conns:
         c.close()
 
