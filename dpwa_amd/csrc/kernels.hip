@@ -26,6 +26,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -1291,40 +1292,108 @@ hipError_t launch_publish_header(char *slot, int64_t n, int32_t dtype, double *c
 
 // Reuse guard of a header-only publish (the adapter's write-through): writes
 // through `param.data` move no version counter, so before a snapshot the last average wrote is
-// published as is, kGuardSamples 16-B words spread evenly over the parameters (first and last
-// included) and their tail bytes are compared with it.  Any difference makes the publish a full
-// one: the payload is copied from the parameters.  Two launches, so every workgroup of the copy
-// sees the same verdict.  The compare runs one sample per lane over kGuardSamples / 64 one-wave
-// workgroups -- spread over as many CUs, each sample one memory latency -- and a workgroup that
-// finds a difference stamps the verdict word with this publish's generation `gen` (a word that
-// never needs clearing; the first stamp of a generation counts a hit).  The copy's workgroups, one
-// per CU, return at once unless the word carries `gen`.  (Round 4's single-workgroup compare,
-// 4,096 dependent-latency loads on one CU, cost ~19 us per update_send: bench `adapter_loop`.)
-// The sampled words move with the generation (guard_offset): sample k of generation g is word
-// base(k) + g mod W, W the widest gap between two bases, so over any W consecutive publishes every
-// word of the parameters is compared once -- a sparse write through `param.data` that the samples
-// of one publish miss is caught within W = ceil((n16-1)/4095) publishes, at the same per-publish
-// cost.  The first and the last word (and the tail bytes) are compared at every publish.
+// published as is, the parameters are compared with it at kGuardSamples 16-B words, and what
+// differs is copied.  The payload is cut into kGuardSamples chunks, chunk k = words [b(k), b(k+1))
+// with b(k) = k (n16-1) / (samples-1) (the last chunk is the last word alone); chunk k is sampled
+// at one word, b(k) + gen mod (its length), so the sampled word moves on by one each publish and
+// every word of the parameters is compared once in any W = ceil((n16-1)/4095) publishes -- a
+// sparse write through `param.data` that one publish's samples miss is published within W
+// publishes, at the same per-publish cost.  The first word (and the tail bytes) are compared at
+// every publish too.  A chunk whose sample differs is copied from the parameters into the
+// payload by the workgroup that sampled it, so one launch does the check and the copy: no
+// verdict has to reach other workgroups (round 5 ran a compare and a grid-wide conditional copy
+// as two launches).  A workgroup that finds a difference stamps the verdict word with this
+// publish's generation `gen` (never cleared; the first stamp of a generation counts a hit).
 constexpr int kGuardSamples = 4096;
 constexpr int kGuardWave = 64;
-constexpr int kGuardCopyBlocks = 256;
+constexpr int kGuardChunksPerBlock = 16;     // chunks sampled by one workgroup (lanes 0..15 of wave 0)
+constexpr int kGuardBlock = 256;             // 4 waves copy a dirty chunk
 
-// Byte offset of sample k (of `samples`) over n16 16-B words at generation `gen`.
-__device__ __forceinline__ int64_t guard_offset(int64_t k, int64_t samples, int64_t n16, uint32_t gen)
+__device__ __forceinline__ int64_t guard_base(int64_t k, int64_t samples, int64_t n16)
 {
-    if (samples <= 1) return 0;
-    const int64_t base = k * (n16 - 1) / (samples - 1);             // 0 .. n16-1, ends included
-    const int64_t widest = (n16 - 1 + samples - 2) / (samples - 1);   // ceil((n16-1)/(samples-1)) >= 1
-    int64_t w = base + (int64_t)(gen % (uint64_t)widest);
-    if (w >= n16) w -= n16;                                           // the last base wraps to the front
-    return w << 4;
+    return samples > 1 ? k * (n16 - 1) / (samples - 1) : 0;
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(kGuardWave) void k_guard_compare(const char *__restrict__ flat,
-                                                              const char *__restrict__ payload, int64_t nbytes,
-                                                              int32_t *__restrict__ dirty, uint32_t *__restrict__ hits,
-                                                              int32_t gen)
+// Byte offset of the word sampled in chunk k (of `samples`) over n16 16-B words at generation `gen`.
+__device__ __forceinline__ int64_t guard_offset(int64_t k, int64_t samples, int64_t n16, uint32_t gen)
+{
+    if (samples <= 1 || k >= samples - 1) return (samples > 1 ? n16 - 1 : 0) << 4;
+    const int64_t b = guard_base(k, samples, n16);
+    const int64_t len = guard_base(k + 1, samples, n16) - b;        // >= 1
+    return (b + (int64_t)(gen % (uint64_t)len)) << 4;
+}
+
+__global__ __launch_bounds__(kGuardBlock) void k_guard_publish(const char *__restrict__ flat,
+                                                               char *__restrict__ payload, int64_t nbytes,
+                                                               int32_t *__restrict__ dirty,
+                                                               uint32_t *__restrict__ hits, int32_t gen)
+{
+    __shared__ uint32_t s_mask;
+    const int64_t n16 = nbytes >> 4;
+    const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
+    const int64_t k0 = (int64_t)blockIdx.x * kGuardChunksPerBlock;
+    const int t = threadIdx.x;
+    if (t < kGuardWave) {
+        int diff = 0;
+        const int64_t k = k0 + t;
+        if (t < kGuardChunksPerBlock && k < samples) {
+            const int64_t o = guard_offset(k, samples, n16, (uint32_t)gen);
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(flat + o);
+            const u32x4 b = *reinterpret_cast<const u32x4 *>(payload + o);
+            diff = (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
+        }
+        if (blockIdx.x == 0 && t == kGuardChunksPerBlock && n16 > 0) {   // the first word, always: chunk 0
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(flat);
+            const u32x4 b = *reinterpret_cast<const u32x4 *>(payload);
+            if ((a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w)) diff = 1;
+        }
+        // bit c: chunk k0 + c differs (the first-word lane reports chunk 0)
+        const uint64_t ballot = __ballot(diff);
+        uint32_t mask = (uint32_t)(ballot & ((1u << kGuardChunksPerBlock) - 1u));
+        if (ballot >> kGuardChunksPerBlock) mask |= 1u;
+        if (t == 0) s_mask = mask;
+    }
+    // the tail bytes (past the last whole word) belong to workgroup 0: compared and copied in place
+    int tail_diff = 0;
+    if (blockIdx.x == 0 && t >= kGuardWave && t < kGuardWave + (nbytes & 15)) {
+        const int64_t j = (n16 << 4) + (t - kGuardWave);
+        if (flat[j] != payload[j]) {
+            payload[j] = flat[j];
+            tail_diff = 1;
+        }
+    }
+    tail_diff = __syncthreads_or(tail_diff);
+    const uint32_t mask = s_mask;
+    if ((mask || tail_diff) && t == 0) {
+        const int32_t old = atomicExch(dirty, gen);
+        if (old != gen) atomicAdd(hits, 1u);
+    }
+    for (uint32_t m = mask; m; m &= m - 1) {
+        const int64_t k = k0 + __builtin_ctz(m);
+        const int64_t lo = k >= samples - 1 ? (samples > 1 ? n16 - 1 : 0) : guard_base(k, samples, n16);
+        const int64_t hi = k >= samples - 1 ? n16 : guard_base(k + 1, samples, n16);
+        u32x4 *d = reinterpret_cast<u32x4 *>(payload);
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(flat);
+        int64_t i = lo + t;
+        for (; i + 3 * kGuardBlock < hi; i += 4 * kGuardBlock) {   // four loads in flight per lane
+            const u32x4 v0 = src[i], v1 = src[i + kGuardBlock], v2 = src[i + 2 * kGuardBlock],
+                        v3 = src[i + 3 * kGuardBlock];
+            d[i] = v0;
+            d[i + kGuardBlock] = v1;
+            d[i + 2 * kGuardBlock] = v2;
+            d[i + 3 * kGuardBlock] = v3;
+        }
+        for (; i < hi; i += kGuardBlock) d[i] = src[i];
+    }
+}
+
+// The same check for operands that are not 16-B aligned (the flat buffers are 256-B aligned, so
+// only the stateless ABI reaches it): one thread per chunk compares its sampled word bytewise and
+// copies its chunk when it differs.
+__global__ __launch_bounds__(kGuardWave) void k_guard_publish_bytes(const char *__restrict__ flat,
+                                                                    char *__restrict__ payload, int64_t nbytes,
+                                                                    int32_t *__restrict__ dirty,
+                                                                    uint32_t *__restrict__ hits, int32_t gen)
 {
     const int64_t n16 = nbytes >> 4;
     const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
@@ -1332,48 +1401,26 @@ __global__ __launch_bounds__(kGuardWave) void k_guard_compare(const char *__rest
     int diff = 0;
     if (k < samples) {
         const int64_t o = guard_offset(k, samples, n16, (uint32_t)gen);
-        if (VEC) {
-            const u32x4 a = *reinterpret_cast<const u32x4 *>(flat + o);
-            const u32x4 b = *reinterpret_cast<const u32x4 *>(payload + o);
-            diff = (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
-        } else {
-            for (int j = 0; j < 16; ++j) diff |= flat[o + j] != payload[o + j];
+        for (int j = 0; j < 16; ++j) diff |= flat[o + j] != payload[o + j];
+        if (k == 0)
+            for (int j = 0; j < 16; ++j) diff |= flat[j] != payload[j];
+        if (diff) {
+            const int64_t lo = (k >= samples - 1 ? (samples > 1 ? n16 - 1 : 0) : guard_base(k, samples, n16)) << 4;
+            const int64_t hi = (k >= samples - 1 ? n16 : guard_base(k + 1, samples, n16)) << 4;
+            for (int64_t i = lo; i < hi; ++i) payload[i] = flat[i];
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x < (nbytes & 15))
-        diff |= flat[(n16 << 4) + threadIdx.x] != payload[(n16 << 4) + threadIdx.x];
-    if (blockIdx.x == 0 && threadIdx.x < 2 && n16 > 0) {   // the first and the last word, always
-        const int64_t o = threadIdx.x ? (n16 - 1) << 4 : 0;
-        if (VEC) {
-            const u32x4 a = *reinterpret_cast<const u32x4 *>(flat + o);
-            const u32x4 b = *reinterpret_cast<const u32x4 *>(payload + o);
-            diff |= (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
-        } else {
-            for (int j = 0; j < 16; ++j) diff |= flat[o + j] != payload[o + j];
+    if (blockIdx.x == 0 && threadIdx.x < (nbytes & 15)) {
+        const int64_t j = (n16 << 4) + threadIdx.x;
+        if (flat[j] != payload[j]) {
+            payload[j] = flat[j];
+            diff = 1;
         }
     }
     diff = __syncthreads_or(diff);
     if (diff && threadIdx.x == 0) {
         const int32_t old = atomicExch(dirty, gen);
         if (old != gen) atomicAdd(hits, 1u);
-    }
-}
-
-template <bool VEC>
-__global__ __launch_bounds__(kBlock) void k_copy_if(char *__restrict__ dst, const char *__restrict__ src,
-                                                    int64_t nbytes, const int32_t *__restrict__ dirty, int32_t gen)
-{
-    if (*dirty != gen) return;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    const int64_t first = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (VEC) {
-        const int64_t n16 = nbytes >> 4;
-        u32x4 *d = reinterpret_cast<u32x4 *>(dst);
-        const u32x4 *s = reinterpret_cast<const u32x4 *>(src);
-        for (int64_t i = first; i < n16; i += stride) d[i] = s[i];
-        if (blockIdx.x == 0 && threadIdx.x < (nbytes & 15)) dst[(n16 << 4) + threadIdx.x] = src[(n16 << 4) + threadIdx.x];
-    } else {
-        for (int64_t i = first; i < nbytes; i += stride) dst[i] = src[i];
     }
 }
 
@@ -1384,16 +1431,12 @@ hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes,
     const char *src = (const char *)flat;
     const int64_t n16 = nbytes >> 4;
     const int64_t samples = n16 < kGuardSamples ? n16 : kGuardSamples;
-    const uint32_t gc = (uint32_t)((samples + kGuardWave - 1) / kGuardWave + (samples == 0 ? 1 : 0));
     if (aligned16(flat) && aligned16(payload)) {
-        hipLaunchKernelGGL(k_guard_compare<true>, dim3(gc), dim3(kGuardWave), 0, s, src, payload, nbytes, dirty, hits,
-                           gen);
-        hipLaunchKernelGGL(k_copy_if<true>, dim3(kGuardCopyBlocks), dim3(kBlock), 0, s, payload, src, nbytes, dirty,
-                           gen);
+        const uint32_t g = (uint32_t)std::max<int64_t>(1, (samples + kGuardChunksPerBlock - 1) / kGuardChunksPerBlock);
+        hipLaunchKernelGGL(k_guard_publish, dim3(g), dim3(kGuardBlock), 0, s, src, payload, nbytes, dirty, hits, gen);
     } else {
-        hipLaunchKernelGGL(k_guard_compare<false>, dim3(gc), dim3(kGuardWave), 0, s, src, payload, nbytes, dirty, hits,
-                           gen);
-        hipLaunchKernelGGL(k_copy_if<false>, dim3(kGuardCopyBlocks), dim3(kBlock), 0, s, payload, src, nbytes, dirty,
+        const uint32_t g = (uint32_t)std::max<int64_t>(1, (samples + kGuardWave - 1) / kGuardWave);
+        hipLaunchKernelGGL(k_guard_publish_bytes, dim3(g), dim3(kGuardWave), 0, s, src, payload, nbytes, dirty, hits,
                            gen);
     }
     return hipGetLastError();
@@ -1403,7 +1446,7 @@ hipError_t launch_guard_payload(char *payload, const void *flat, int64_t nbytes,
 // parameters ARE the snapshot peers read; writes through `param.data` there move no version
 // counter.  One launch per publish: the payload published last time -- untouched since its
 // window closed, until the average after this publish overwrites that slot -- is compared with the
-// samples saved when it was published (k_guard_compare's offsets of that publish's generation
+// samples saved when it was published (k_guard_publish's offsets of that publish's generation
 // `gen`), then the samples of the payload published now (generation `cur_gen`, the offsets moved on
 // by one) are saved in their place.  Each lane owns one sample, so the compare and the save of a
 // sample are in one lane, in order.  `old` NULL: save only; `cur` NULL: compare only.  Layout of

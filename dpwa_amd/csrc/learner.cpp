@@ -252,7 +252,7 @@ struct Ctl {            // device control block
                         // clock[cur+2], which that publish then selects without a kernel
     dpwa_coef coef;
     int32_t guard_dirty;   // reuse guard: the generation (publish number) of the last publish that found
-                           // the parameters changed (kernels.hip k_guard_compare)
+                           // the parameters changed (kernels.hip k_guard_publish)
     uint32_t guard_hits;   // ... and how many publishes did
     int32_t window_dirty;  // window guard (resident): the generation of the last window found written
     uint32_t window_hits;  // ... and how many windows were

@@ -116,17 +116,36 @@ GUARD_SAMPLES = 4096
 
 def guard_words(n16, gen, samples=GUARD_SAMPLES):
     """The 16-B words the reuse / window guard compares at publish generation `gen` (a host
-    restatement of kernels.hip guard_offset): word base(k) + gen mod W, base(k) = k(n16-1)/(s-1),
-    W the widest gap between bases, plus the first and the last word at every generation; every
-    word is covered in any W consecutive generations."""
+    restatement of kernels.hip guard_offset): the payload is cut into min(n16, 4096) chunks,
+    chunk k = words [b(k), b(k+1)) with b(k) = k(n16-1)/(s-1) (the last chunk is the last word
+    alone), and chunk k is sampled at word b(k) + gen mod (its length); the first word is compared
+    at every generation too.  Every word is covered in any W consecutive generations."""
     s = min(n16, samples)
     if s <= 1:
         return {0, max(0, n16 - 1)}
-    widest = (n16 - 1 + s - 2) // (s - 1)
-    r = gen % widest
-    return {(k * (n16 - 1) // (s - 1) + r) % n16 for k in range(s)} | {0, n16 - 1}
+
+    def b(k):
+        return k * (n16 - 1) // (s - 1)
+    out = {b(k) + gen % (b(k + 1) - b(k)) for k in range(s - 1)}
+    return out | {0, n16 - 1}
+
+
+def guard_chunk(n16, word, samples=GUARD_SAMPLES):
+    """The chunk (index) a word belongs to, and its word range."""
+    s = min(n16, samples)
+    if s <= 1 or word >= n16 - 1:
+        return max(0, s - 1), (max(0, n16 - 1), n16)
+    k = word * (s - 1) // (n16 - 1)
+    while k * (n16 - 1) // (s - 1) > word:
+        k -= 1
+    while (k + 1) * (n16 - 1) // (s - 1) <= word:
+        k += 1
+    return k, (k * (n16 - 1) // (s - 1), (k + 1) * (n16 - 1) // (s - 1))
 
 
 def guard_period(n16, samples=GUARD_SAMPLES):
+    """W: the longest chunk, so every word is sampled within W consecutive generations."""
     s = min(n16, samples)
-    return 1 if s <= 1 else (n16 - 1 + s - 2) // (s - 1)
+    if s <= 1:
+        return 1
+    return max((k + 1) * (n16 - 1) // (s - 1) - k * (n16 - 1) // (s - 1) for k in range(s - 1))
