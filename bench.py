@@ -817,7 +817,7 @@ def parity_key(trial):
     return "%s/%s%s" % (kind or "lockstep", pull, form)
 
 
-TRAFFIC_ROUNDS = ("r05", "r04", "r03")     # profiles/traffic_<round>_<publish>[_x<learners>].json, newest first
+TRAFFIC_ROUNDS = ("r06", "r05", "r04", "r03")     # profiles/traffic_<round>_<publish>[_x<learners>].json, newest first
 
 
 def pmc_traffic(path, publish, learners, numel, dtype, basis):
