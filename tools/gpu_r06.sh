@@ -23,6 +23,8 @@ for step in "$@"; do
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 || { echo "smoke failed" >&2; tail -30 "$out/smoke.log" >&2; exit 1; } ;;
     tests)
       timeout -k 10 1100 python -u -m pytest -x -v --timeout 280 --timeout-method thread $arg > "$out/pytest_$i.log" 2>&1 || { echo "tests failed" >&2; tail -60 "$out/pytest_$i.log" >&2; exit 1; } ;;
+    ubsantests)   # the suite through build_san/libdpwa_hip.so (tools/ubsan_build.sh; take ./build_san out of .gpurunignore first)
+      DPWA_HIP_LIB=$PWD/build_san/libdpwa_hip.so timeout -k 10 1100 python -u -m pytest -x -v --timeout 280 --timeout-method thread $arg > "$out/pytest_ubsan_$i.log" 2>&1 || { echo "ubsan tests failed" >&2; tail -60 "$out/pytest_ubsan_$i.log" >&2; exit 1; } ;;
     bench)
       DPWA_BENCH_DETAIL=$out/bench_${i}_detail.json timeout -k 10 900 python -u bench.py $arg > "$out/bench_$i.json" 2> "$out/bench_$i.err" || { echo "bench failed" >&2; tail -40 "$out/bench_$i.err" >&2; exit 1; }
       python3 tools/check_line.py "$out/bench_$i.json" >&2 || exit 1 ;;
