@@ -240,3 +240,50 @@ def test_reuse_guard_rotation_catches_a_fixed_unsampled_word(tmp_path):
     first = want.index(1)
     assert 1 <= first <= W, (first, W)
     assert sum(want) >= 2                    # and again one period later
+
+
+def test_reuse_guard_on_unaligned_parameters(tmp_path):
+    """Connection level, parameters that start 4 bytes past a 16-B boundary (a view into a larger
+    tensor): the guard takes its bytewise form (k_guard_publish_bytes) -- writes to the first
+    element (always compared) and to the last one (the tail bytes) make the reusing publish copy
+    what changed, and the trajectories equal the oracle's."""
+    import ctypes
+
+    from dpwa_amd import DpwaConnection, _lib
+    n, T = 100_003, 4
+    names = ["a", "b"]
+    cfg = tmp_path / "unaligned.yaml"
+    write_cfg(cfg, names, 1.0, "constant", 0.0, 0.5)
+    rng = np.random.default_rng(8)
+    init = rng.standard_normal((2, n)).astype(np.float32)
+    group = LocalGroup()
+    conns = [DpwaConnection(names[g], str(cfg), seed=7 + g, group=group) for g in range(2)]
+    bases = [torch.zeros(n + 1, device=DEV) for _ in range(2)]
+    flats = [bases[g][1:] for g in range(2)]
+    for g in range(2):
+        flats[g].copy_(torch.from_numpy(init[g]))
+        assert flats[g].data_ptr() % 16 == 4
+    params = init.copy()
+    for r in range(T):
+        for g in range(2):
+            conns[g].update_send(flats[g], 1.0, reuse_snapshot=r > 0)
+            if r == 0:
+                _lib.call("dpwa_learner_set_reuse_guard", conns[g]._learner.handle, 1)
+        snaps = [params[g].copy() for g in range(2)]
+        for g in range(2):
+            conns[g].update_wait_average(flats[g], 1.0, write_through=True)
+            params[g] = olerp.lerp_f32(params[g], snaps[1 - g], 0.5)
+        flats[0][0] += 1.5                      # the first element: always compared
+        params[0][0] = np.float32(params[0][0] + np.float32(1.5))
+        flats[1][-1] -= 2.0                     # the last element: the tail bytes
+        params[1][-1] = np.float32(params[1][-1] - np.float32(2.0))
+    torch.cuda.synchronize()
+    for g in range(2):
+        assert olerp.bits_equal(flats[g].cpu().numpy(), params[g]), g
+    hits = []
+    for c in conns:
+        h = ctypes.c_uint32()
+        _lib.call("dpwa_learner_reuse_guard_hits", c._learner.handle, ctypes.byref(h))
+        hits.append(h.value)
+        c.close()
+    assert hits == [T - 1, T - 1], hits
