@@ -744,6 +744,17 @@ static int window_alloc(dpwa_learner *l)
     return DPWA_OK;
 }
 
+// Work on `s` that overwrites slot version % 2 -- the payload the window guard's last roll read
+// (the one published before the last publish): an average's write-through store or a relocation --
+// runs after that roll when the roll went to another stream.
+static int wait_window_roll(dpwa_learner *l, hipStream_t s)
+{
+    if (!l->resident || !l->window_stream || l->window_stream == s) return DPWA_OK;
+    HIP_TRY(hipEventRecord(l->ev_window, l->window_stream));
+    HIP_TRY(hipStreamWaitEvent(s, l->ev_window, 0));
+    return DPWA_OK;
+}
+
 // One roll on `s`: check the last window (if any), then sample `cur` (if not NULL).
 static int window_roll(dpwa_learner *l, const char *cur, hipStream_t s)
 {
@@ -1294,12 +1305,7 @@ static int average_prepare(dpwa_learner *l, void *flat, double loss, const doubl
         const int k = (int)(l->version % 2);   // slot of the next publish
         int rc = wait_slot_readers(l, k, s);
         if (rc) return rc;
-        if (l->resident && l->window_stream && l->window_stream != s) {
-            // the window guard's last roll (on the publish's stream) read the payload published
-            // before it -- slot k, which this average overwrites
-            HIP_TRY(hipEventRecord(l->ev_window, l->window_stream));
-            HIP_TRY(hipStreamWaitEvent(s, l->ev_window, 0));
-        }
+        if ((rc = wait_window_roll(l, s))) return rc;
         p.snap = slot_payload(l, k);
         p.snap_slot = k;
         if (l->cfg.method != DPWA_INTERP_LOSS && !l->header_on_publish) {   // peers never read this header's loss
@@ -1550,6 +1556,7 @@ static int relocate_impl(dpwa_learner *l, hipStream_t s)
     if (!l->resident || l->res_slot == k) return DPWA_OK;
     int rc = wait_slot_readers(l, k, s);
     if (rc) return rc;
+    if ((rc = wait_window_roll(l, s))) return rc;
     HIP_TRY(launch_copy_payload(slot_payload(l, k), slot_payload(l, l->res_slot), (int64_t)l->payload_bytes, s));
     l->res_slot = k;
     l->wt_valid = true;
