@@ -40,12 +40,12 @@ def test_fds_reach_every_peer():
     ps = [ctx.Process(target=_rank, args=(r, world, q_addr, addr_qs[r], results, chunks)) for r in range(world)]
     for p in ps:
         p.start()
-    addrs = dict(q_addr.get(timeout=60) for _ in range(world))
+    addrs = dict(q_addr.get(timeout=180) for _ in range(world))
     for q in addr_qs:
         q.put(addrs)
-    out = dict(results.get(timeout=60) for _ in range(world))
+    out = dict(results.get(timeout=180) for _ in range(world))
     for p in ps:
-        p.join(30)
+        p.join(120)
         assert p.exitcode == 0
     for rank, got in out.items():
         for r, contents in got.items():
