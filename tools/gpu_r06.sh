@@ -41,10 +41,10 @@ for step in "$@"; do
       done ;;
     rehearse)
       n=${arg%% *}; rest=${arg#"$n"}
-      timeout -k 10 900 python -u bench.py --gpus $n --dist-backend gloo --steps 20 --warmup 5 \
-          --dist-sweep-max-numel 100000000 $rest > "$out/rehearse_n$n.json" 2> "$out/rehearse_n$n.err" \
-          || { echo "rehearsal n=$n failed" >&2; tail -40 "$out/rehearse_n$n.err" >&2; exit 1; }
-      python3 tools/check_line.py "$out/rehearse_n$n.json" >&2 || exit 1 ;;
+      DPWA_BENCH_DETAIL=$out/rehearse_${i}_n${n}_detail.json timeout -k 10 900 python -u bench.py --gpus $n --dist-backend gloo --steps 20 --warmup 5 \
+          --dist-sweep-max-numel 100000000 $rest > "$out/rehearse_${i}_n$n.json" 2> "$out/rehearse_${i}_n$n.err" \
+          || { echo "rehearsal n=$n failed" >&2; tail -40 "$out/rehearse_${i}_n$n.err" >&2; exit 1; }
+      python3 tools/check_line.py "$out/rehearse_${i}_n$n.json" >&2 || exit 1 ;;
     py)
       timeout -k 10 600 python -u $arg > "$out/py_$i.log" 2>&1 || { echo "py failed" >&2; tail -40 "$out/py_$i.log" >&2; exit 1; } ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
