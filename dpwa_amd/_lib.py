@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("DPWA_HIP_LIB", os.path.join(_HERE, "libdpwa_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dpwa_hip.h")
 
 # Constants mirrored from include/dpwa_hip.h
-ABI_VERSION = 8
+ABI_VERSION = 9
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_NOMEM = 0, -1, -2, -3, -4
 F32, BF16, F64 = 0, 1, 2
 INTERP_CONSTANT, INTERP_CLOCK, INTERP_LOSS = 0, 1, 2
@@ -81,6 +81,8 @@ _pint = ctypes.POINTER(ctypes.c_int)
 SIGNATURES = {
     "dpwa_last_error": [],
     "dpwa_abi_version": [],
+    "dpwa_sched_get_state": [_vp, ctypes.POINTER(ctypes.c_uint32), _int, _pint],
+    "dpwa_sched_set_state": [_vp, ctypes.POINTER(ctypes.c_uint32), _int],
     "dpwa_trace_enabled": [],
     "dpwa_trace_push": [ctypes.c_char_p],
     "dpwa_trace_pop": [],

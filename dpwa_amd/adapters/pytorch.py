@@ -203,6 +203,14 @@ class DpwaPyTorchAdapter:
             elif wt and payload is not None:
                 a._versions = a._param_versions()
 
+    def state_dict(self):
+        """The connection's gossip state (clock, scheduler) for a checkpoint beside the model's
+        (extension: the reference checkpoints the net but restarts dpwa's clock at 0)."""
+        return self._conn.state_dict()
+
+    def load_state_dict(self, state):
+        self._conn.load_state_dict(state)
+
     @property
     def reuse_guard_hits(self):
         """Publishes whose reuse guard found the parameters changed behind the version counters

@@ -105,6 +105,21 @@ public:
     // random.randint(a, b) == randrange(a, b + 1) == a + _randbelow(b - a + 1)
     int64_t randint(int64_t a, int64_t b) { return a + (int64_t)randbelow((uint64_t)(b - a + 1)); }
 
+    // The generator's state in CPython's random.getstate() order: the 624 words, then the
+    // position (getstate()[1] == (*mt, pos)).
+    void get_state(uint32_t *out) const
+    {
+        for (int i = 0; i < N; ++i) out[i] = mt_[i];
+        out[N] = (uint32_t)idx_;
+    }
+    bool set_state(const uint32_t *in)
+    {
+        if (in[N] > (uint32_t)N) return false;     // CPython's setstate rejects pos > N too
+        for (int i = 0; i < N; ++i) mt_[i] = in[i];
+        idx_ = (int)in[N];
+        return true;
+    }
+
 private:
     void init_genrand(uint32_t s)
     {
@@ -337,6 +352,84 @@ int dpwa_sched_n_live(const dpwa_sched *s, int *n_live)
     int n = 0;
     for (const auto &p : s->peers) n += p.live ? 1 : 0;
     *n_live = n;
+    return DPWA_OK;
+}
+
+// ---- gossip-state checkpoint (SURVEY §5 checkpoint/resume).  The reference keeps no gossip state
+// across a restart (dpwa.py:59 starts the clock at 0; `random` starts from its seed again); here a
+// resumed job can continue the scheduler exactly where it stopped.  Layout, 32-bit words:
+//   magic 'DPWS', format 1, MT19937 state (624 words + position, CPython getstate() order),
+//   n_peers, per peer {score, flags: 1 connected | 2 live}, n_order, order[n_order]
+constexpr uint32_t kStateMagic = 0x53575044u;   // "DPWS" little-endian
+constexpr uint32_t kStateFormat = 1;
+
+static int state_words(const dpwa_sched *s)
+{
+    return 2 + PyMT::N + 1 + 1 + 2 * (int)s->peers.size() + 1 + (int)s->order.size();
+}
+
+int dpwa_sched_get_state(const dpwa_sched *s, uint32_t *words, int max_words, int *n_words)
+{
+    if (!s || !n_words) return set_error(DPWA_ERR_ARG, "dpwa_sched_get_state: NULL argument");
+    const int n = state_words(s);
+    *n_words = n;
+    if (!words) return DPWA_OK;                   // size query
+    if (max_words < n) return set_error(DPWA_ERR_ARG, "dpwa_sched_get_state: %d words needed, %d given", n, max_words);
+    int w = 0;
+    words[w++] = kStateMagic;
+    words[w++] = kStateFormat;
+    s->rng.get_state(words + w);
+    w += PyMT::N + 1;
+    words[w++] = (uint32_t)s->peers.size();
+    for (const PeerEntry &p : s->peers) {
+        words[w++] = (uint32_t)p.score;
+        words[w++] = (p.connected ? 1u : 0u) | (p.live ? 2u : 0u);
+    }
+    words[w++] = (uint32_t)s->order.size();
+    for (int k : s->order) words[w++] = (uint32_t)k;
+    return DPWA_OK;
+}
+
+int dpwa_sched_set_state(dpwa_sched *s, const uint32_t *words, int n_words)
+{
+    if (!s || !words) return set_error(DPWA_ERR_ARG, "dpwa_sched_set_state: NULL argument");
+    const int fixed = 2 + PyMT::N + 1 + 1;
+    if (n_words < fixed + 1 || words[0] != kStateMagic || words[1] != kStateFormat)
+        return set_error(DPWA_ERR_ARG, "dpwa_sched_set_state: not a scheduler state (format %u)", kStateFormat);
+    const uint32_t P = words[2 + PyMT::N + 1];
+    if (P != s->peers.size())
+        return set_error(DPWA_ERR_ARG, "dpwa_sched_set_state: state of %u peers, scheduler has %zu", P,
+                         s->peers.size());
+    if (n_words < fixed + 2 * (int)P + 1) return set_error(DPWA_ERR_ARG, "dpwa_sched_set_state: truncated state");
+    const uint32_t n_order = words[fixed + 2 * P];
+    if (n_words != fixed + 2 * (int)P + 1 + (int)n_order || n_order > P)
+        return set_error(DPWA_ERR_ARG, "dpwa_sched_set_state: bad peer order length");
+    // validate everything before changing anything
+    std::vector<PeerEntry> peers(P);
+    for (uint32_t k = 0; k < P; ++k) {
+        const uint32_t sc = words[fixed + 2 * k], fl = words[fixed + 2 * k + 1];
+        if (sc < (uint32_t)kFlowMin || sc > (uint32_t)kFlowMax || fl > 3)
+            return set_error(DPWA_ERR_ARG, "dpwa_sched_set_state: peer %u: score %u flags %u out of range", k, sc, fl);
+        peers[k].score = (int)sc;
+        peers[k].connected = (fl & 1u) != 0;
+        peers[k].live = (fl & 2u) != 0;
+    }
+    std::vector<int> order;
+    std::vector<char> seen(P, 0);
+    for (uint32_t j = 0; j < n_order; ++j) {
+        const uint32_t k = words[fixed + 2 * P + 1 + j];
+        if (k >= P || seen[k] || !peers[k].live)
+            return set_error(DPWA_ERR_ARG, "dpwa_sched_set_state: bad peer order entry %u", k);
+        seen[k] = 1;
+        order.push_back((int)k);
+    }
+    for (uint32_t k = 0; k < P; ++k)
+        if (peers[k].live && !seen[k]) return set_error(DPWA_ERR_ARG, "dpwa_sched_set_state: live peer %u not ordered", k);
+    PyMT rng = s->rng;
+    if (!rng.set_state(words + 2)) return set_error(DPWA_ERR_ARG, "dpwa_sched_set_state: generator position out of range");
+    s->rng = rng;
+    s->peers = peers;
+    s->order = order;
     return DPWA_OK;
 }
 

@@ -239,6 +239,7 @@ class DpwaConnection:
         _lib.call("dpwa_node_handles", self._node, None, ctypes.byref(sched))
         self._sched = Scheduler(len(self.peers), handle=sched.value)
         self._learner = None
+        self._pending_clock = None        # load_state_dict before the learner exists
         self._resident = False      # make_resident was called
         self._sent = None           # resident: (parameters tensor, its version) at update_send
         # transport of copying fetches: "copy" (hipMemcpyAsync) or "kernel[:blocks]"
@@ -477,6 +478,30 @@ class DpwaConnection:
         _lib.call("dpwa_node_set_fault", self._node, self._peer_by_name(peer_name),
                   -1 if status is None else codes[status])
 
+    def state_dict(self):
+        """Gossip state for a checkpoint (extension; the reference keeps none across a restart:
+        dpwa.py:59 starts the clock at 0 and the process's `random` starts from its seed): the
+        clock and the scheduler -- its generator, every peer's flow-control score and state, the
+        peer order -- so a resumed job continues the same peer choices and clock bookkeeping.
+        Plain data (ints, a float, strings): torch.save / json both take it."""
+        return {"format": 1, "name": self.name, "peers": [p.name for p in self.peers],
+                "clock": float(self.clock) if self._learner is not None else float(self._pending_clock or 0.0),
+                "scheduler": self._sched.get_state()}
+
+    def load_state_dict(self, state):
+        """Restores a ``state_dict()`` taken from a connection with the same name and peers
+        (before its first update_send, or between rounds)."""
+        if state.get("format") != 1:
+            raise ValueError("not a DpwaConnection state (format %r)" % state.get("format"))
+        if state.get("name") != self.name or list(state.get("peers", [])) != [p.name for p in self.peers]:
+            raise ValueError("state of node %r with peers %r does not fit node %r with peers %r"
+                             % (state.get("name"), state.get("peers"), self.name, [p.name for p in self.peers]))
+        self._sched.set_state(state["scheduler"])
+        if self._learner is not None:
+            self._learner.write_clock(float(state["clock"]))
+        else:
+            self._pending_clock = float(state["clock"])     # written once the learner exists (_bind)
+
     def flow_control_scores(self):
         return {p.name: self._sched.score(k) for k, p in enumerate(self.peers)}
 
@@ -550,6 +575,9 @@ class DpwaConnection:
         h = ctypes.c_void_p()
         _lib.call("dpwa_node_handles", self._node, ctypes.byref(h), None)
         self._learner = Learner(parameters.device, parameters.numel(), parameters.dtype, handle=h.value)
+        if self._pending_clock is not None:           # load_state_dict before the first round
+            self._learner.write_clock(self._pending_clock)
+            self._pending_clock = None
         if self._pull.partition(":")[0] in RELAY_PULLS:
             if not hasattr(self._group, "relay_blocks"):
                 raise ValueError("the relay pull needs a DistGroup (one learner per rank)")

@@ -114,6 +114,19 @@ class Scheduler:
         _lib.call("dpwa_sched_n_live", self._h, ctypes.byref(out))
         return out.value
 
+    def get_state(self):
+        """The scheduler's whole state as a list of 32-bit words (include/dpwa_hip.h
+        dpwa_sched_get_state): words 2..626 are CPython's random.getstate()[1]."""
+        n = ctypes.c_int()
+        _lib.call("dpwa_sched_get_state", self._h, None, 0, ctypes.byref(n))
+        buf = (ctypes.c_uint32 * n.value)()
+        _lib.call("dpwa_sched_get_state", self._h, buf, n.value, ctypes.byref(n))
+        return list(buf)
+
+    def set_state(self, words):
+        buf = (ctypes.c_uint32 * len(words))(*[int(w) for w in words])
+        _lib.call("dpwa_sched_set_state", self._h, buf, len(words))
+
     def random(self):
         out = ctypes.c_double()
         _lib.call("dpwa_sched_random", self._h, ctypes.byref(out))

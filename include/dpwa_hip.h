@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DPWA_ABI_VERSION 8
+#define DPWA_ABI_VERSION 9
 
 #define DPWA_OK 0
 #define DPWA_ERR_ARG (-1)     /* bad argument (API misuse)                          */
@@ -472,6 +472,13 @@ int dpwa_sched_remove(dpwa_sched *s, int peer);
 int dpwa_sched_add(dpwa_sched *s, int peer);
 int dpwa_sched_n_live(const dpwa_sched *s, int *n_live);
 /* raw CPython-equivalent draws, for tests: random.random(), random.randint(a, b) */
+/* Gossip-state checkpoint (SURVEY §5 checkpoint/resume; the reference keeps none across a
+ * restart, dpwa.py:59): the scheduler's generator (CPython getstate() order), every peer's
+ * flow-control score and connected/live flags, and TxThread's peer order, as 32-bit words.
+ * get_state with words == NULL returns the size in *n_words; set_state validates the whole state
+ * (format, peer count, score bounds, order) before changing anything.  ABI version 9. */
+int dpwa_sched_get_state(const dpwa_sched *s, uint32_t *words, int max_words, int *n_words);
+int dpwa_sched_set_state(dpwa_sched *s, const uint32_t *words, int n_words);
 int dpwa_sched_random(dpwa_sched *s, double *out);
 int dpwa_sched_randint(dpwa_sched *s, int64_t a, int64_t b, int64_t *out);
 

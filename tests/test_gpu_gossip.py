@@ -470,3 +470,60 @@ def test_prefetching_local_group_matches_oracle(tmp_path, zero_copy, pull):
             assert conns[g].clock == exp["clocks"][r, g]
     for c in conns:
         c.close()
+
+
+def test_resumed_gossip_continues_the_uninterrupted_one(tmp_path):
+    """Gossip-state checkpoint (DpwaConnection.state_dict / load_state_dict, extension): three
+    learners (clock interpolation, fetch_probability 0.7) run 12 rounds; the same learners run 6,
+    are checkpointed (gossip state + parameters), closed, and new connections with other seeds
+    resume from the checkpoint for 6 more.  Rounds 7-12 -- peers, clocks and parameters -- equal
+    the uninterrupted run's bit for bit."""
+    names = ["r0", "r1", "r2"]
+    cfg = tmp_path / "resume.yaml"
+    write_cfg(cfg, names, 0.7, "clock", 0.0, None)
+    rng = np.random.default_rng(13)
+    n, T, cut = 10_007, 12, 6
+    init = rng.standard_normal((3, n)).astype(np.float32)
+    deltas = (0.01 * rng.standard_normal((T, 3, n))).astype(np.float32)
+
+    def run(conns, flats, rounds):
+        rec = []
+        for r in rounds:
+            for c, f in zip(conns, flats):
+                c.update_send(f, 1.0 + r)
+            peers = []
+            for c, f in zip(conns, flats):
+                payload, _ = c.update_wait_average(f, 2.0 + r)
+                peers.append(payload.peer if payload is not None else None)
+            for g, f in enumerate(flats):
+                f.add_(torch.from_numpy(deltas[r, g]).to(DEV))
+            torch.cuda.synchronize()
+            rec.append((peers, [c.clock for c in conns], [f.cpu().numpy().copy() for f in flats]))
+        return rec
+
+    group = LocalGroup()
+    conns = [DpwaConnection(nm, str(cfg), seed=200 + g, group=group) for g, nm in enumerate(names)]
+    flats = [torch.from_numpy(init[g].copy()).to(DEV) for g in range(3)]
+    full = run(conns, flats, range(T))
+    for c in conns:
+        c.close()
+
+    group = LocalGroup()
+    conns = [DpwaConnection(nm, str(cfg), seed=200 + g, group=group) for g, nm in enumerate(names)]
+    flats = [torch.from_numpy(init[g].copy()).to(DEV) for g in range(3)]
+    first = run(conns, flats, range(cut))
+    states = [c.state_dict() for c in conns]
+    saved = [f.clone() for f in flats]
+    for c in conns:
+        c.close()
+    group = LocalGroup()
+    conns = [DpwaConnection(nm, str(cfg), seed=900 + g, group=group) for g, nm in enumerate(names)]
+    for c, st in zip(conns, states):
+        c.load_state_dict(st)
+    second = run(conns, saved, range(cut, T))
+    for c in conns:
+        c.close()
+    for r, (a, b) in enumerate(zip(full, first + second)):
+        assert a[0] == b[0] and a[1] == b[1], (r, a[:2], b[:2])
+        for g in range(3):
+            assert olerp.bits_equal(a[2][g], b[2][g]), (r, g)

@@ -189,3 +189,59 @@ def test_oracle_add_peer_matches_reference():
             assert (payload is not None) == r["data"]
             assert L.scores(case["peers"]) == r["scores"]
             assert list(L.peers) == r["order"]
+
+
+def test_state_is_cpython_getstate_and_round_trips():
+    """Gossip-state checkpoint (dpwa_sched_get_state / _set_state): words 2..626 are CPython's
+    random.getstate()[1] after the same draws; a second scheduler given the state continues the
+    first one's peer choices, scores and gate draws exactly, through removals and faults."""
+    s = Scheduler(5, seed=1234, fetch_probability=0.7)
+    r = random.Random(1234)
+    for _ in range(37):
+        assert s.random() == r.random()
+    st = s.get_state()
+    assert st[:2] == [0x53575044, 1] and tuple(st[2:2 + 625]) == r.getstate()[1]
+    rng = random.Random(77)
+
+    def rounds(sched, n, seed):
+        g = random.Random(seed)           # the same scripted transport outcomes for both
+        out = []
+        for _ in range(n):
+            status = [g.choice([0, 0, 0, 1, 2, 3]) for _ in range(5)]
+            out.append((sched.bernoulli(), sched.fetch(status), sched.scores()))
+        return out
+
+    rounds(s, 40, 5)
+    live = [k for k, sc in enumerate(s.scores()) if sc is not None]
+    if len(live) > 1:
+        s.remove(live[-1])                # remove_peer (conn.py:215-222) on top of the faults' removals
+    s.add(0)                              # and put a peer back (add_peer), if it was gone
+    rounds(s, 10, 6)
+    saved = s.get_state()
+    ahead = rounds(s, 60, 7)
+    t = Scheduler(5, seed=rng.randrange(1 << 30), fetch_probability=0.7)
+    t.set_state(saved)
+    assert t.get_state() == saved
+    assert rounds(t, 60, 7) == ahead
+
+
+def test_state_is_validated_before_it_is_applied():
+    s = Scheduler(3, seed=9)
+    good = s.get_state()
+    t = Scheduler(4, seed=9)
+    with pytest.raises(_lib.DpwaError, match="peers"):
+        t.set_state(good)                                   # another peer count
+    bad = list(good)
+    bad[2 + 625 + 1] = 5000                                 # peer 0's score out of [10, 1000]
+    before = s.get_state()
+    with pytest.raises(_lib.DpwaError, match="out of range"):
+        s.set_state(bad)
+    assert s.get_state() == before                          # nothing changed
+    bad = list(good)
+    bad[0] = 0
+    with pytest.raises(_lib.DpwaError, match="not a scheduler state"):
+        s.set_state(bad)
+    bad = list(good)
+    bad[2 + 624] = 625                                      # generator position past N
+    with pytest.raises(_lib.DpwaError, match="position"):
+        s.set_state(bad)
