@@ -1176,14 +1176,19 @@ def round_sweep(device, cfg_dir, steps=20, warmup=3, rows=None, publish="write-t
     return rows
 
 
+VMM_MIN_BYTES = 3 << 29     # learner.cpp kVmmMinBytes: slots from here up are fd-shared hipMemCreate chunks
+
+
 def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, watchdog, min_steps=3, warmup=2,
-                     max_numel=None, rows=None, resident=False):
+                     max_numel=None, rows=None, resident=False, vmm_ok=True):
     """N > 1: whole gossip rounds at every north_star size (configs[1..4] sizes and dtypes), one
     learner per rank, on the transport the trials chose (`pull`: "<mode>" lock-step or
     "async/<mode>[+wt]"), constant 0.5, fetch_probability 1 -- the GB/s and rounds/s table of
     BASELINE's north_star at 2/4/8 GPUs.  A size that fails on any rank is reported with its
     error and the sweep goes on.  max_numel: skip larger sizes (rehearsals with several ranks
-    on one GPU)."""
+    on one GPU).  vmm_ok False (a `+vmm` parity transport failed on this node's devices): the
+    sizes whose slots would be fd-shared hipMemCreate chunks are reported as not run instead of
+    mapping memory that failed its check."""
     from dpwa_amd import DpwaConnection
     names = ["w%d" % (r + 1) for r in range(world)]
     cfg = os.path.join(cfg_dir, "dist_sweep.yaml")     # every rank its own copy (cfg_dir is per rank)
@@ -1202,6 +1207,12 @@ def dist_round_sweep(world, rank, device, cfg_dir, pull, write_through, ctl, wat
         # parameters, two snapshot slots, staging (two under the board), relay buffer + margin:
         # checked on every rank before anything is allocated, so no rank fails alone inside the
         # binding collectives
+        if not vmm_ok and numel * esize >= VMM_MIN_BYTES:
+            rows.append({"numel": numel, "dtype": dt, "transport": pull,
+                         "error": "not run: its snapshot slots are fd-shared hipMemCreate chunks, and a +vmm parity "
+                                  "transport failed on these devices"})
+            progress("dist sweep %d %s skipped: %s" % (numel, dt, rows[-1]["error"]))
+            continue
         need = 6 * numel * esize + (2 << 30)
         free = torch.cuda.mem_get_info(device)[0]
         if not _agree(free >= need * share, world, ctl):
@@ -2295,8 +2306,9 @@ def main(argv=None):
         learners[:] = []
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+        vmm_ok = parity is None or all(v for k, v in parity.items() if "+vmm" in k)
         dist_round_sweep(world, rank, device, tmp, pull, wt_main, ctl, wd, max_numel=args.dist_sweep_max_numel,
-                         rows=round_rows, resident=resident_main)
+                         rows=round_rows, resident=resident_main, vmm_ok=vmm_ok)
     wd.enter("result", 60.0)
     if out is not None:
         emit_result(out, detail_path(world))

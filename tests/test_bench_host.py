@@ -249,3 +249,15 @@ def test_result_line_from_the_committed_round5_line():
     assert d["value"] == full["value"] and d["roofline"]["frac"] == full["roofline"]["frac"]
     assert d["cpu_baseline"]["value"] == full["cpu_baseline"]["value"]
     assert d["value_cold"] == full["value_cold"]["value"]
+
+
+def test_vmm_threshold_matches_the_learner():
+    """bench.VMM_MIN_BYTES (which N>1 sweep sizes use fd-shared slots, skipped when a +vmm parity
+    transport failed) is learner.cpp's kVmmMinBytes."""
+    import re
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    src = open(os.path.join(ROOT, "dpwa_amd", "csrc", "learner.cpp")).read()
+    m = re.search(r"kVmmMinBytes = \(size_t\)(\d+) << (\d+);", src)
+    assert m and bench.VMM_MIN_BYTES == int(m.group(1)) << int(m.group(2))
