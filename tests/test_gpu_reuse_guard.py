@@ -287,3 +287,51 @@ def test_reuse_guard_on_unaligned_parameters(tmp_path):
         hits.append(h.value)
         c.close()
     assert hits == [T - 1, T - 1], hits
+
+
+def test_reuse_guard_copies_the_chunks_whose_sample_differs(tmp_path):
+    """The one-launch guard copies per chunk (kernels.hip k_guard_publish): learner a writes two
+    elements through param.data -- one in a word its next publish samples, one in another chunk's
+    unsampled word.  Learner b averages with constant 1.0, so its parameters become the snapshot a
+    served: the sampled write reaches b, the unsampled one is not in that snapshot (it would be
+    once its chunk's rotating sample reaches it, tests above)."""
+    from tests.helpers import guard_chunk
+    n = 100_032
+    n16 = n * 4 // 16
+    gen = 2                                          # a's second publish is the guarded one
+    words = sorted(guard_words(n16, gen))
+    x = words[len(words) // 2]                       # sampled at gen 2
+    cx = guard_chunk(n16, x)[0]
+    y = next(w for w in range(n16 // 4, n16) if w not in guard_words(n16, gen) and guard_chunk(n16, w)[0] != cx)
+    kx, ky = x * 4 + 2, y * 4 + 1
+    rng = np.random.default_rng(41)
+    init = rng.standard_normal((2, n)).astype(np.float32)
+    cfg = tmp_path / "chunks.yaml"
+    write_cfg(cfg, ["a", "b"], 1.0, "constant", 0.0, 1.0)
+    group = LocalGroup()
+    nets, ads = [], []
+    for g, nm in enumerate(("a", "b")):
+        net = Net([(n,)]).to(DEV)
+        load_flat(net, init[g])
+        nets.append(net)
+        ads.append(DpwaPyTorchAdapter(net, nm, str(cfg), seed=50 + g, group=group, write_through=True))
+    for ad in ads:
+        ad.update_send(1.0)
+    for ad in ads:
+        ad.update_wait(1.0)
+    before_y = float(nets[0].p0.detach()[ky].item())
+    with torch.no_grad():
+        nets[0].p0.data[kx] = 77.5
+        nets[0].p0.data[ky] = -33.25
+    for ad in ads:
+        ad.update_send(1.0)
+    for ad in ads:
+        ad.update_wait(1.0)
+    got_x = float(nets[1].p0.detach()[kx].item())
+    got_y = float(nets[1].p0.detach()[ky].item())
+    hits = ads[0].reuse_guard_hits
+    for ad in ads:
+        ad.connection.close()
+    assert hits == 1
+    assert got_x == 77.5
+    assert got_y == before_y and got_y != -33.25
