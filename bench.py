@@ -185,6 +185,9 @@ _XGMI = ("bytes_per_pull", "avg_pull_us", "achieved_gbs_per_pull", "peak_gbs", "
 _SCALAR = (int, float, bool, str, type(None))
 
 
+_SIZE_TAG = {11_173_962: "11m", 100_000_000: "100m", 1_000_000_000: "1b", 7_000_000_000: "7b"}
+
+
 def _pick(d, keys, maxlen=160):
     """The scalar entries of `d` named in `keys` (strings cut to maxlen)."""
     out = {}
@@ -205,6 +208,14 @@ def compact_line(full, detail=None):
     if isinstance(cfg, dict):
         out["config"] = {k: (v[:200] if isinstance(v, str) else v) for k, v in cfg.items()
                          if isinstance(v, _SCALAR) and k not in ("loop_order", "peer")}
+        # north_star's table (GB/s and rounds/s at 11M / 100M / 1B / 7B) as scalars of `config`,
+        # which the driver keeps: whole rounds at each size on the line's transport
+        for row in full.get("round_sweep") or []:
+            if isinstance(row, dict) and isinstance(row.get("value"), (int, float)):
+                tag = _SIZE_TAG.get(row.get("numel"), str(row.get("numel")))
+                out["config"]["sweep_%s_gbs" % tag] = row["value"]
+                if isinstance(row.get("gossip_rounds_per_s"), (int, float)):
+                    out["config"]["sweep_%s_rounds_per_s" % tag] = row["gossip_rounds_per_s"]
     vc = full.get("value_cold")
     out["value_cold"] = vc.get("value") if isinstance(vc, dict) else vc if isinstance(vc, _SCALAR) else None
     rl = full.get("roofline")
