@@ -52,3 +52,21 @@ def test_state_of_another_node_is_refused(tmp_path):
         b.load_state_dict({"format": 0})
     a.close()
     b.close()
+
+
+def test_state_goes_through_torch_save_and_the_safe_loader(tmp_path):
+    """The INTEGRATION recipe: torch.save beside the model, torch.load(weights_only=True)."""
+    import torch
+    names = ["a", "b", "c"]
+    cfg = tmp_path / "c.yaml"
+    _cfg(cfg, names)
+    a = DpwaConnection("c", str(cfg), seed=5, group=LocalGroup())
+    for _ in range(9):
+        a._sched.fetch([0, 1])
+    torch.save({"gossip": a.state_dict()}, tmp_path / "ck.pt")
+    st = torch.load(tmp_path / "ck.pt", weights_only=True)["gossip"]
+    b = DpwaConnection("c", str(cfg), seed=6, group=LocalGroup())
+    b.load_state_dict(st)
+    assert b._sched.get_state() == a._sched.get_state()
+    a.close()
+    b.close()
