@@ -335,3 +335,13 @@ def test_reuse_guard_copies_the_chunks_whose_sample_differs(tmp_path):
     assert hits == 1
     assert got_x == 77.5
     assert got_y == before_y and got_y != -33.25
+
+
+@pytest.mark.parametrize("n", [3, 5, 64, 1000])
+def test_reuse_guard_on_tiny_models(tmp_path, n):
+    """Models below one 16-B word, at a few words and below 4,096 words (every word its own
+    chunk): dense writes through param.data are caught at every reusing publish and the
+    trajectories equal the oracle's."""
+    same, hits, T = _run(tmp_path, "dense", n=n, T=4)
+    assert all(same), same
+    assert hits == [T - 1, T - 1], hits
