@@ -345,3 +345,84 @@ def test_reuse_guard_on_tiny_models(tmp_path, n):
     same, hits, T = _run(tmp_path, "dense", n=n, T=4)
     assert all(same), same
     assert hits == [T - 1, T - 1], hits
+
+
+@pytest.mark.parametrize("mode", ["dense", "sampled", "unsampled"])
+def test_reuse_guard_bf16(tmp_path, mode):
+    """bf16 parameters (100,003 elements, padded by the flat buffer to 256 B) through the
+    write-through adapter with the guard on, two learners at constant 0.5: dense writes through
+    param.data every round give the torch-eager bf16 oracle's trajectories; a write to a word the
+    next publish samples reaches the peer at once (its chunk is copied); a write to a word it
+    does not sample is not in that publish's snapshot (its chunk's sampled word is elsewhere), and
+    the peer averages the old value -- bit for bit as the oracle given that snapshot."""
+    from tests.test_gpu_kernels import from_u16, to_u16
+    n = 100_003
+    rng = np.random.default_rng(17)
+    init = olerp.f32_to_bf16(rng.standard_normal((2, n)).astype(np.float32))
+    cfg = tmp_path / ("bf16_%s.yaml" % mode)
+    write_cfg(cfg, ["a", "b"], 1.0, "constant", 0.0, 0.5)
+    group = LocalGroup()
+    nets, ads = [], []
+    for g, nm in enumerate(("a", "b")):
+        net = Net([(n,)], dtype=torch.bfloat16).to(DEV)
+        with torch.no_grad():
+            net.p0.copy_(from_u16(init[g]))
+        nets.append(net)
+        ads.append(DpwaPyTorchAdapter(net, nm, str(cfg), seed=60 + g, group=group, write_through=True))
+    n16 = ads[0].flat.numel * 2 // 16          # the flat buffer pads the parameter to 256 B
+    params = [init[0].copy(), init[1].copy()]
+    T = 4
+    for r in range(T):
+        for ad in ads:
+            ad.update_send(1.0)
+        snaps = [params[0].copy(), params[1].copy()]
+        for g, ad in enumerate(ads):
+            ad.update_wait(1.0)
+            params[g] = olerp.lerp_bf16(params[g], snaps[1 - g], 0.5)
+        torch.cuda.synchronize()
+        for g in range(2):
+            assert olerp.bits_equal(to_u16(nets[g].p0.detach()), params[g]), (mode, r, g)
+        if mode == "dense":
+            bump = olerp.f32_to_bf16((0.25 * rng.standard_normal((2, n))).astype(np.float32))
+            for g in range(2):
+                new = olerp.f32_to_bf16(olerp.bf16_to_f32(params[g]) + olerp.bf16_to_f32(bump[g]))
+                with torch.no_grad():
+                    nets[g].p0.data.copy_(from_u16(new))        # through .data: no version counter moves
+                params[g] = new
+        elif r == 0:
+            gen = 2                                              # a's next (guarded) publish
+            words = guard_words(n16, gen)
+            w = (sorted(words)[len(words) // 2] if mode == "sampled"
+                 else next(x for x in range(n16 // 2, n16) if x not in words))
+            k = w * 8 + 3
+            old = float(nets[0].p0.detach()[k].item())
+            with torch.no_grad():
+                nets[0].p0.data[k] = 64.0
+            new = params[0].copy()
+            new[k] = olerp.f32_to_bf16(np.array([64.0], np.float32))[0]
+            if mode == "sampled":
+                params[0] = new                                  # the publish takes it: b sees it
+            else:
+                # a's own parameters hold the write; its snapshot does not (b averages the old value)
+                ads_snapshot_old = params[0].copy()
+                params[0] = new
+                for ad in ads:
+                    ad.update_send(1.0)
+                snaps = [ads_snapshot_old, params[1].copy()]
+                for g, ad in enumerate(ads):
+                    ad.update_wait(1.0)
+                    params[g] = olerp.lerp_bf16(params[g], snaps[1 - g], 0.5)
+                torch.cuda.synchronize()
+                for g in range(2):
+                    assert olerp.bits_equal(to_u16(nets[g].p0.detach()), params[g]), (mode, "after", g)
+                assert old != 64.0
+                break
+    hits = ads[0].reuse_guard_hits
+    for ad in ads:
+        ad.connection.close()
+    if mode == "dense":
+        assert hits == T - 1
+    elif mode == "sampled":
+        assert hits == 1
+    else:
+        assert hits == 0
