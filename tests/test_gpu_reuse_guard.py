@@ -393,7 +393,7 @@ def test_reuse_guard_bf16(tmp_path, mode):
             gen = 2                                              # a's next (guarded) publish
             words = guard_words(n16, gen)
             w = (sorted(words)[len(words) // 2] if mode == "sampled"
-                 else next(x for x in range(n16 // 2, n16) if x not in words))
+                 else next(x for x in range(n16 // 2, n // 8) if x not in words))
             k = w * 8 + 3
             old = float(nets[0].p0.detach()[k].item())
             with torch.no_grad():
