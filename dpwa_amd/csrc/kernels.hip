@@ -1309,9 +1309,15 @@ constexpr int kGuardWave = 64;
 constexpr int kGuardChunksPerBlock = 16;     // chunks sampled by one workgroup (lanes 0..15 of wave 0)
 constexpr int kGuardBlock = 256;             // 4 waves copy a dirty chunk
 
+// b(k) = k (n16-1) / (samples-1).  samples = min(n16, kGuardSamples): below kGuardSamples words it
+// is k itself, otherwise the divisor is the constant kGuardSamples-1, which compiles to a
+// multiply-high -- the sampling lanes' addresses wait on this, and a 64-bit division by a
+// variable is a long emulated sequence on the VALU.
 __device__ __forceinline__ int64_t guard_base(int64_t k, int64_t samples, int64_t n16)
 {
-    return samples > 1 ? k * (n16 - 1) / (samples - 1) : 0;
+    if (samples <= 1) return 0;
+    if (samples < kGuardSamples) return k;
+    return (int64_t)((uint64_t)k * (uint64_t)(n16 - 1) / (uint64_t)(kGuardSamples - 1));
 }
 
 // Byte offset of the word sampled in chunk k (of `samples`) over n16 16-B words at generation `gen`.
@@ -1320,7 +1326,8 @@ __device__ __forceinline__ int64_t guard_offset(int64_t k, int64_t samples, int6
     if (samples <= 1 || k >= samples - 1) return (samples > 1 ? n16 - 1 : 0) << 4;
     const int64_t b = guard_base(k, samples, n16);
     const int64_t len = guard_base(k + 1, samples, n16) - b;        // >= 1
-    return (b + (int64_t)(gen % (uint64_t)len)) << 4;
+    const int64_t r = len <= (int64_t)UINT32_MAX ? (int64_t)(gen % (uint32_t)len) : (int64_t)(gen % (uint64_t)len);
+    return (b + r) << 4;
 }
 
 __global__ __launch_bounds__(kGuardBlock) void k_guard_publish(const char *__restrict__ flat,
