@@ -53,7 +53,7 @@ int main(int argc, char **argv)
         CHECK(dpwa_sched_create(&s, n, key.data(), (int)key.size(), fp) == DPWA_OK && s);
         std::vector<char> removed((size_t)n, 0);
         for (int step = 0; step < 300; ++step) {
-            switch (uni(0, 6)) {
+            switch (uni(0, 7)) {
             case 0: {   // one whole fetch loop against a random static status
                 std::vector<int32_t> st((size_t)(n > 0 ? n : 1));
                 for (auto &x : st) x = uni(DPWA_PEER_READY, DPWA_PEER_DEAD);
@@ -119,6 +119,51 @@ int main(int argc, char **argv)
                 const int64_t a = uni(-5, 5), b = a + uni(0, 2000);
                 int64_t v = 0;
                 CHECK(dpwa_sched_randint(s, a, b, &v) == DPWA_OK && v >= a && v <= b);
+                break;
+            }
+            case 6: {   // checkpoint: a twin restored from the state continues identically; damaged
+                        // or truncated states fail without changing the scheduler they were given to
+                int nw = 0;
+                CHECK(dpwa_sched_get_state(s, nullptr, 0, &nw) == DPWA_OK && nw > 0);
+                std::vector<uint32_t> st((size_t)nw);
+                CHECK(dpwa_sched_get_state(s, st.data(), nw - 1, &nw) != DPWA_OK);
+                CHECK(dpwa_sched_get_state(s, st.data(), nw, &nw) == DPWA_OK);
+                dpwa_sched *t = nullptr;
+                const uint32_t other = (uint32_t)rng();
+                CHECK(dpwa_sched_create(&t, n, &other, 1, fp) == DPWA_OK && t);
+                int tw = 0;    // t's own size: all its peers are live, s's may not be
+                CHECK(dpwa_sched_get_state(t, nullptr, 0, &tw) == DPWA_OK);
+                std::vector<uint32_t> before((size_t)tw), after((size_t)tw);
+                CHECK(dpwa_sched_get_state(t, before.data(), tw, &tw) == DPWA_OK);
+                std::vector<uint32_t> bad = st;
+                const int cut = uni(0, nw - 1);
+                if (uni(0, 1)) {
+                    bad.resize((size_t)cut);           // truncated
+                } else {                               // one word damaged
+                    bad[(size_t)cut] ^= (uint32_t)uni(1, 0x7fffffff);
+                }
+                const int rc = dpwa_sched_set_state(t, bad.data(), (int)bad.size());
+                if (rc != DPWA_OK) {
+                    int aw = 0;
+                    CHECK(dpwa_sched_get_state(t, after.data(), tw, &aw) == DPWA_OK && aw == tw);
+                    CHECK(after == before);
+                }
+                CHECK(dpwa_sched_set_state(t, st.data(), nw) == DPWA_OK);
+                for (int j = 0; j < 20; ++j) {
+                    int pa = -2, pb = -2, ca = -1, cb = -1;
+                    CHECK(dpwa_sched_pick(s, &pa, &ca) == DPWA_OK && dpwa_sched_pick(t, &pb, &cb) == DPWA_OK);
+                    CHECK(pa == pb && ca == cb);
+                    if (pa >= 0) {
+                        const int r = uni(DPWA_REPLY_PAYLOAD, DPWA_REPLY_TIMEOUT);
+                        int d1 = 0, d2 = 0, x1 = 0, x2 = 0;
+                        CHECK(dpwa_sched_report(s, pa, r, &d1, &x1) == DPWA_OK);
+                        CHECK(dpwa_sched_report(t, pb, r, &d2, &x2) == DPWA_OK);
+                        CHECK(d1 == d2 && x1 == x2);
+                    }
+                    double xa = 0, xb = 1;
+                    CHECK(dpwa_sched_random(s, &xa) == DPWA_OK && dpwa_sched_random(t, &xb) == DPWA_OK && xa == xb);
+                }
+                CHECK(dpwa_sched_destroy(t) == DPWA_OK);
                 break;
             }
             default: {   // malformed calls fail cleanly
