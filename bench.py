@@ -372,6 +372,7 @@ class Watchdog:
         self.parity = {}
         self.transport = None
         self.held, self.held_rc = None, None   # hold(): the finished line and the run's exit status
+        self.fired = self.disarmed = False
         self._lock = threading.Lock()
         t = threading.Thread(target=self._run, name="bench-watchdog", daemon=True)
         t.start()
@@ -393,12 +394,21 @@ class Watchdog:
         with self._lock:
             self.deadline = None
 
+    def disarm(self):
+        """Stops the watchdog for good; False when it has already fired (it prints and exits)."""
+        with self._lock:
+            if self.fired:
+                return False
+            self.deadline, self.disarmed = None, True
+            return True
+
     def _run(self):
         import faulthandler
         while True:
             time.sleep(1.0)
             with self._lock:
-                late = self.deadline is not None and time.monotonic() > self.deadline
+                late = not self.disarmed and self.deadline is not None and time.monotonic() > self.deadline
+                self.fired = self.fired or late
                 phase, transport = self.phase, self.transport
                 held, held_rc = self.held, self.held_rc
             if not late:
@@ -409,6 +419,10 @@ class Watchdog:
                     out = dict(held)
                     out["error"] = "watchdog: phase '%s' overran its budget (the line up to it)" % phase
                     out["phase"] = phase
+                    if transport is not None and isinstance(out.get("parity"), dict):   # a late parity check
+                        out["parity"] = dict(out["parity"], **{transport: False})
+                        out["parity_failed"] = sorted(k for k, v in out["parity"].items()
+                                                      if k != "workload" and not v)
                     emit_result(out, detail_path(self.world))
                 faulthandler.dump_traceback(all_threads=True)
                 sys.stderr.flush()
@@ -617,7 +631,8 @@ PARITY_PHASE_S = 180.0          # watchdog budget of one parity transport
 def parity_transports(world, gossip="auto"):
     """Every transport the run can time, plus the fd-shared (hipMemCreate, DPWA_VMM=1) slot
     path that configs[3]/[4] use above 1.5 GiB, through the lock-step fused relay (slots and
-    relay buffers fd-imported) and the free-running board."""
+    relay buffers fd-imported) and the free-running board.  main() checks the `+vmm` ones at N>1
+    only after the measured line is held (no timed transport uses them)."""
     if world == 1:
         return ["self", "local", "local+res"]
     t = []
@@ -1574,10 +1589,16 @@ def main(argv=None):
     # The parity leg runs first: at N>1 a transport that fails it on this node's devices is
     # reported (parity: false) and left out of the trials, so the timed run always uses a
     # transport whose results matched the oracle; at N=1 it checks both local forms (and gives
-    # the GPU a second of work between the CPU baseline and the timed rounds).
+    # the GPU a second of work between the CPU baseline and the timed rounds).  At N>1 the
+    # fd-shared (+vmm) forms are checked after the line is held (late_parity): no timed transport
+    # uses them (they only gate the sweep's sizes above VMM_MIN_BYTES), so a hang in an import
+    # path the line does not depend on costs the watchdog's phase, not the measured line.
     parity = None
+    late_parity = []
     if not args.no_parity:
-        parity = parity_leg(world, rank, local_rank, device, tmp, parity_transports(world, args.gossip),
+        transports = parity_transports(world, args.gossip)
+        late_parity = [t for t in transports if "+vmm" in t] if world > 1 else []
+        parity = parity_leg(world, rank, local_rank, device, tmp, [t for t in transports if t not in late_parity],
                             args.dist_backend, ctl=ctl, watchdog=wd)
 
     # rehearsals run several ranks on one GPU: their pulls never cross an xGMI link
@@ -2303,33 +2324,60 @@ def main(argv=None):
         if world == 1:
             out["roofline"]["size_sweep"] = size_rows
         out["round_sweep"] = round_rows
-    wd.hold(out, 1 if parity_failed else 0)
-    if world == 1 and not args.no_sweep:
-        wd.enter("size sweep", 900.0)
-        size_sweep(device, rows=size_rows)
-        wd.enter("round sweep", 900.0)
-        round_sweep(device, tmp, rows=round_rows, publish=form)
-    elif world > 1 and not args.no_sweep:
-        # the timed learners' buffers go first: the sweep's 7B learner needs ~80 GB per GPU
+    code = 1 if parity_failed else 0
+    wd.hold(out, code)
+    # Everything after this point runs with the measurement done: an exception in it (a rank that
+    # left a collective, a sweep size that does not fit) ends the job with the measured line
+    # and the run's status, as a watchdog overrun does, never with a traceback in its place.
+    printed = False
+    try:
+        if world == 1 and not args.no_sweep:
+            wd.enter("size sweep", 900.0)
+            size_sweep(device, rows=size_rows)
+            wd.enter("round sweep", 900.0)
+            round_sweep(device, tmp, rows=round_rows, publish=form)
+        elif world > 1 and (late_parity or not args.no_sweep):
+            # the timed learners' buffers go first: the sweep's 7B learner needs ~80 GB per GPU, and
+            # the late parity transports build groups of their own
+            for conn, _ in lockstep_learners + async_learners:
+                conn.close()
+            lockstep_learners, async_learners = [], []
+            learners[:] = []
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            if late_parity:
+                hbarrier()
+                parity.update(parity_leg(world, rank, local_rank, device, tmp, late_parity, args.dist_backend, ctl=ctl,
+                                         watchdog=wd))
+                if out is not None:
+                    out["parity_failed"] = sorted(k for k, v in parity.items() if k != "workload" and not v)
+            if not args.no_sweep:
+                vmm_ok = parity is None or all(v for k, v in parity.items() if "+vmm" in k)
+                dist_round_sweep(world, rank, device, tmp, pull, wt_main, ctl, wd, max_numel=args.dist_sweep_max_numel,
+                                 rows=round_rows, resident=resident_main, vmm_ok=vmm_ok)
+        wd.enter("result", 60.0)
+        if out is not None:
+            emit_result(out, detail_path(world))
+        printed = True
+        wd.hold(None, code)      # the line is out: an overrun now only exits
+        wd.enter("shutdown", 300.0)
         for conn, _ in lockstep_learners + async_learners:
             conn.close()
-        lockstep_learners, async_learners = [], []
-        learners[:] = []
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-        vmm_ok = parity is None or all(v for k, v in parity.items() if "+vmm" in k)
-        dist_round_sweep(world, rank, device, tmp, pull, wt_main, ctl, wd, max_numel=args.dist_sweep_max_numel,
-                         rows=round_rows, resident=resident_main, vmm_ok=vmm_ok)
-    wd.enter("result", 60.0)
-    if out is not None:
-        emit_result(out, detail_path(world))
-    wd.hold(None, 1 if parity_failed else 0)      # the line is out: an overrun now only exits
-    wd.enter("shutdown", 300.0)
-    for conn, _ in lockstep_learners + async_learners:
-        conn.close()
-    if world > 1:
-        hbarrier()
-        dist.destroy_process_group()
+        if world > 1:
+            hbarrier()
+            dist.destroy_process_group()
+    except Exception as e:   # noqa: BLE001
+        import traceback
+        traceback.print_exc()
+        progress("after the measured line, phase '%s': %s: %s" % (wd.phase, type(e).__name__, e))
+        if not wd.disarm():      # the watchdog fired first: it prints the line and exits
+            time.sleep(600)
+        if out is not None and not printed:
+            out["error"] = "after the measurement, phase '%s': %s: %s" % (wd.phase, type(e).__name__, e)
+            out["phase"] = wd.phase
+            emit_result(out, detail_path(world))
+        sys.stderr.flush()
+        os._exit(code)
     wd.idle()
     progress("done")
     if parity is not None:

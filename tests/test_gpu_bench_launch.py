@@ -120,6 +120,20 @@ def test_injected_transport_failure_is_isolated(tmp_path):
     assert out["value"] > 0 and not any(k.startswith("kernel") for k in _detail(out)["pull_trials_gbs"])
 
 
+def test_hang_in_a_late_parity_transport_keeps_the_measured_line(tmp_path):
+    """At N>1 the fd-shared (+vmm) transports are checked after the line is held: a hang in one
+    (here rank 1 raises at its start, so rank 0 blocks in the transport's first collective) ends
+    the job through the watchdog with the measured line, that transport false, exit status 0."""
+    t = "lockstep/relay-avg:32+vmm"
+    rc, lines, err = _bench(tmp_path, {"DPWA_BENCH_INJECT": "%s@1:start" % t}, args=ARGS + ["--phase-scale", "0.1"])
+    assert rc == 0, err[-3000:]
+    out = _line(lines)
+    assert out["value"] > 0 and out["parity_of_timed_transport"]["ok"]
+    assert out["parity"][t] is False and t in out["parity_failed"]
+    assert "watchdog" in out["error"] and out["phase"] == "parity %s" % t
+    assert all(v for k, v in out["parity"].items() if "+vmm" not in k)
+
+
 def test_resident_parity_failure_falls_back_to_write_through(tmp_path):
     """If no resident transport passes the parity check (here injected failures in every lock-step
     `+res` transport of a --publish resident run), the timed run uses the verified write-through
