@@ -276,8 +276,8 @@ def detail_path(world):
     return os.environ.get("DPWA_BENCH_DETAIL") or os.path.join(ROOT, "gpurun_out", "bench_detail_n%d.json" % world)
 
 
-def emit_result(full, path):
-    """Writes the full result to `path` (best effort) and prints the compact line."""
+def result_line(full, path):
+    """Writes the full result to `path` (best effort) and returns the compact line naming it."""
     try:
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
         with open(path + ".tmp", "w") as f:
@@ -288,7 +288,24 @@ def emit_result(full, path):
     except OSError as e:
         progress("detail file not written: %s" % e)
         where = None
-    emit(json.dumps(compact_line(full, where)))
+    return json.dumps(compact_line(full, where))
+
+
+def emit_result(full, path):
+    """Writes the full result to `path` (best effort) and prints the compact line."""
+    emit(result_line(full, path))
+
+
+def set_last_words(full, path):
+    """The held line as a signal would leave it (include/dpwa_hip.h dpwa_last_words_set): if the
+    process is stopped from outside (torch.distributed.run stops every rank when one dies; a time
+    limit) or dies in the runtime (a GPU fault ends in abort()) after the measurement, the line
+    up to that phase is still written to stdout.  `full` None clears it."""
+    from dpwa_amd import _lib
+    try:
+        _lib.last_words(_RESULT_FD, result_line(full, path) + "\n" if full is not None else "")
+    except Exception as e:   # noqa: BLE001 -- best effort: the normal paths print the line anyway
+        progress("last words not registered: %s" % e)
 
 
 # ---------------------------------------------------------------- robustness of the N>1 run
@@ -382,13 +399,38 @@ class Watchdog:
             self.phase = phase
             self.transport = transport
             self.deadline = time.monotonic() + seconds * self.args.phase_scale
+            held = self.held
         progress(phase)
+        if held is not None:
+            self._last_words(held, phase, transport)
 
     def hold(self, result, rc):
         """From here on an overrun prints `result` (rank 0's finished line; None on other ranks)
-        with the phase and the error added, and exits with `rc`; hold(None, None) undoes it."""
+        with the phase and the error added, and exits with `rc`; hold(None, None) undoes it.
+        While a line is held it is also registered as the process's last words (set_last_words),
+        refreshed at every phase; hold(None, ...) clears them."""
         with self._lock:
             self.held, self.held_rc = result, rc
+            phase, transport = self.phase, self.transport
+        if self.rank == 0 and (result is not None or self._words):
+            self._last_words(result, phase, transport)
+
+    _words = False
+
+    def _last_words(self, held, phase, transport):
+        if self.rank != 0:
+            return
+        if held is None:
+            set_last_words(None, None)
+            self._words = False
+            return
+        out = dict(held)
+        out["error"] = "ended by a signal in phase '%s', after the measurement (the line up to it)" % phase
+        out["phase"] = phase
+        if transport is not None and isinstance(out.get("parity"), dict):
+            out["parity"] = dict(out["parity"], **{transport: False})
+        set_last_words(out, detail_path(self.world))
+        self._words = True
 
     def idle(self):
         with self._lock:
@@ -414,6 +456,8 @@ class Watchdog:
             if not late:
                 continue
             progress("WATCHDOG: phase '%s' overran its budget; exiting" % phase)
+            if self._words:              # this print replaces them
+                set_last_words(None, None)
             if held_rc is not None:      # the measurement is complete: the line as it stands
                 if held is not None:
                     out = dict(held)
@@ -442,10 +486,11 @@ class Watchdog:
 
 
 def injected(transport, rank, where):
-    """DPWA_BENCH_INJECT="<transport>@<rank>[:start|:end]" (test hook): raise inside that
+    """DPWA_BENCH_INJECT="<transport>@<rank>[:start|:end|:die]" (test hook): raise inside that
     parity transport on that rank, at its start (before its first collective: the other ranks
     then block in one, and the watchdog ends the job) or at its end (after its rounds: the
-    transport's isolation turns it into parity false)."""
+    transport's isolation turns it into parity false); `die`: that rank exits at the transport's
+    start (torch.distributed.run then stops the others with SIGTERM)."""
     spec = os.environ.get("DPWA_BENCH_INJECT", "")
     for item in filter(None, spec.split(",")):
         t, _, rest = item.partition("@")
@@ -927,6 +972,9 @@ def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backen
         conns, err, rec, check = [], None, None, None
         try:
             with _Env(DPWA_VMM="1") if vmm else _Env():
+                if injected(t, rank, "die"):
+                    progress("injected exit (DPWA_BENCH_INJECT, die)")
+                    os._exit(7)
                 if injected(t, rank, "start"):
                     raise RuntimeError("injected failure (DPWA_BENCH_INJECT, start)")
                 if kind == "self":                    # the N=1 timed form: one learner, its own snapshot
@@ -2356,10 +2404,10 @@ def main(argv=None):
                 dist_round_sweep(world, rank, device, tmp, pull, wt_main, ctl, wd, max_numel=args.dist_sweep_max_numel,
                                  rows=round_rows, resident=resident_main, vmm_ok=vmm_ok)
         wd.enter("result", 60.0)
+        wd.hold(None, code)      # the line goes out now: an overrun from here only exits
         if out is not None:
             emit_result(out, detail_path(world))
         printed = True
-        wd.hold(None, code)      # the line is out: an overrun now only exits
         wd.enter("shutdown", 300.0)
         for conn, _ in lockstep_learners + async_learners:
             conn.close()
@@ -2372,9 +2420,13 @@ def main(argv=None):
         progress("after the measured line, phase '%s': %s: %s" % (wd.phase, type(e).__name__, e))
         if not wd.disarm():      # the watchdog fired first: it prints the line and exits
             time.sleep(600)
+        wd.hold(None, code)      # no last words: the line is printed here (or was)
         if out is not None and not printed:
             out["error"] = "after the measurement, phase '%s': %s: %s" % (wd.phase, type(e).__name__, e)
             out["phase"] = wd.phase
+            if wd.transport is not None and isinstance(out.get("parity"), dict):   # a late parity check
+                out["parity"][wd.transport] = False
+                out["parity_failed"] = sorted(k for k, v in out["parity"].items() if k != "workload" and not v)
             emit_result(out, detail_path(world))
         sys.stderr.flush()
         os._exit(code)

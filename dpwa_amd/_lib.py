@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("DPWA_HIP_LIB", os.path.join(_HERE, "libdpwa_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dpwa_hip.h")
 
 # Constants mirrored from include/dpwa_hip.h
-ABI_VERSION = 9
+ABI_VERSION = 10
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_NOMEM = 0, -1, -2, -3, -4
 F32, BF16, F64 = 0, 1, 2
 INTERP_CONSTANT, INTERP_CLOCK, INTERP_LOSS = 0, 1, 2
@@ -86,6 +86,8 @@ SIGNATURES = {
     "dpwa_trace_enabled": [],
     "dpwa_trace_push": [ctypes.c_char_p],
     "dpwa_trace_pop": [],
+    "dpwa_last_words_set": [ctypes.c_int, ctypes.c_char_p, ctypes.c_int64],
+    "dpwa_last_words_written": [ctypes.POINTER(ctypes.c_int)],
     "dpwa_lerp_f32": [_vp, _vp, _i64, _vp, _vp],
     "dpwa_lerp_bf16": [_vp, _vp, _i64, _vp, _vp],
     "dpwa_lerp_f32_host": [_vp, _vp, _i64, _dbl, _vp],
@@ -243,6 +245,19 @@ class trace_range:
     def __exit__(self, *exc):
         load().dpwa_trace_pop()
         return False
+
+
+def last_words(fd, line):
+    """Registers `line` (str; "" clears it) to be written to `fd` if the process is ended by a
+    signal or dies by one (include/dpwa_hip.h dpwa_last_words_set)."""
+    data = line.encode() if line else b""
+    call("dpwa_last_words_set", int(fd) if data else -1, data or None, len(data))
+
+
+def last_words_written():
+    w = ctypes.c_int()
+    call("dpwa_last_words_written", ctypes.byref(w))
+    return bool(w.value)
 
 
 def call(name, *args):

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DPWA_ABI_VERSION 9
+#define DPWA_ABI_VERSION 10
 
 #define DPWA_OK 0
 #define DPWA_ERR_ARG (-1)     /* bad argument (API misuse)                          */
@@ -100,6 +100,13 @@ int dpwa_abi_version(void);
 int dpwa_trace_enabled(void);
 int dpwa_trace_push(const char *name);
 int dpwa_trace_pop(void);
+
+/* Last words (bench.py's held result line): registers `line` (len bytes, at most 16 KiB; len 0
+ * clears it) to be written to `fd` with write(2), once, if the process is ended by SIGTERM,
+ * SIGINT, SIGHUP, SIGABRT, SIGSEGV, SIGBUS, SIGFPE or SIGILL; the handler then restores the
+ * previous handler and re-raises.  The first call installs the handlers.  ABI version 10. */
+int dpwa_last_words_set(int fd, const char *line, int64_t len);
+int dpwa_last_words_written(int *written);
 
 /* ------------------------------------------------------------------------------------
  * Stateless kernels (the fused replacements of the ATen mul/mul/add behind pytorch.py:68)

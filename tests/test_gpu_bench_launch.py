@@ -123,15 +123,35 @@ def test_injected_transport_failure_is_isolated(tmp_path):
 def test_hang_in_a_late_parity_transport_keeps_the_measured_line(tmp_path):
     """At N>1 the fd-shared (+vmm) transports are checked after the line is held: a hang in one
     (here rank 1 raises at its start, so rank 0 blocks in the transport's first collective) ends
-    the job through the watchdog with the measured line, that transport false, exit status 0."""
+    the job through the watchdog with the measured line, that transport false, exit status 0.
+    Whichever rank's watchdog fires first, rank 0 keeps the line: by its own watchdog, or by the
+    post-measurement guard when rank 1's exit breaks the collective it is blocked in."""
     t = "lockstep/relay-avg:32+vmm"
     rc, lines, err = _bench(tmp_path, {"DPWA_BENCH_INJECT": "%s@1:start" % t}, args=ARGS + ["--phase-scale", "0.1"])
     assert rc == 0, err[-3000:]
     out = _line(lines)
     assert out["value"] > 0 and out["parity_of_timed_transport"]["ok"]
     assert out["parity"][t] is False and t in out["parity_failed"]
-    assert "watchdog" in out["error"] and out["phase"] == "parity %s" % t
+    assert ("watchdog" in out["error"] or "after the measurement" in out["error"]), out["error"]
+    assert out["phase"] == "parity %s" % t
     assert all(v for k, v in out["parity"].items() if "+vmm" not in k)
+
+
+def test_rank_lost_after_the_measurement_keeps_the_measured_line(tmp_path):
+    """A rank that dies after the line is held (here rank 1 exits at a late parity transport):
+    torch.distributed.run stops rank 0 with SIGTERM or rank 0's collective fails first; either
+    way rank 0 leaves the measured line on stdout (its last words, or the exception path), with
+    the phase it reached; the job's status is the launcher's.  The SIGTERM can arrive while rank 0
+    is still registering the transport's phase: the line written is then the previous phase's,
+    complete (the library keeps two buffers)."""
+    t = "lockstep/relay-avg:32+vmm"
+    rc, lines, err = _bench(tmp_path, {"DPWA_BENCH_INJECT": "%s@1:die" % t}, args=ARGS + ["--phase-scale", "0.2"])
+    out = _line(lines)
+    assert out["value"] > 0 and out["parity_of_timed_transport"]["ok"], err[-3000:]
+    assert "ended by a signal" in out["error"] or "after the measurement" in out["error"], out["error"]
+    assert out["phase"] in ("parity %s" % t, "report"), out["phase"]
+    if out["phase"] != "report":
+        assert out["parity"][t] is False
 
 
 def test_resident_parity_failure_falls_back_to_write_through(tmp_path):
