@@ -296,6 +296,20 @@ def emit_result(full, path):
     emit(result_line(full, path))
 
 
+def emit_final(full, path):
+    """Prints the held line exactly once: registered as the last words and flushed through the
+    library, so a signal arriving now either finds it written or writes it itself, never both."""
+    line = result_line(full, path)
+    from dpwa_amd import _lib
+    try:
+        _lib.last_words(_RESULT_FD, line + "\n")
+        _lib.last_words_flush()
+        return
+    except Exception as e:   # noqa: BLE001 -- the line goes out directly then
+        progress("last words unavailable (%s): printing directly" % e)
+    emit(line)
+
+
 def set_last_words(full, path):
     """The held line as a signal would leave it (include/dpwa_hip.h dpwa_last_words_set): if the
     process is stopped from outside (torch.distributed.run stops every rank when one dies; a time
@@ -456,8 +470,6 @@ class Watchdog:
             if not late:
                 continue
             progress("WATCHDOG: phase '%s' overran its budget; exiting" % phase)
-            if self._words:              # this print replaces them
-                set_last_words(None, None)
             if held_rc is not None:      # the measurement is complete: the line as it stands
                 if held is not None:
                     out = dict(held)
@@ -467,7 +479,7 @@ class Watchdog:
                         out["parity"] = dict(out["parity"], **{transport: False})
                         out["parity_failed"] = sorted(k for k, v in out["parity"].items()
                                                       if k != "workload" and not v)
-                    emit_result(out, detail_path(self.world))
+                    emit_final(out, detail_path(self.world))
                 faulthandler.dump_traceback(all_threads=True)
                 sys.stderr.flush()
                 os._exit(held_rc)
@@ -2404,10 +2416,10 @@ def main(argv=None):
                 dist_round_sweep(world, rank, device, tmp, pull, wt_main, ctl, wd, max_numel=args.dist_sweep_max_numel,
                                  rows=round_rows, resident=resident_main, vmm_ok=vmm_ok)
         wd.enter("result", 60.0)
-        wd.hold(None, code)      # the line goes out now: an overrun from here only exits
         if out is not None:
-            emit_result(out, detail_path(world))
+            emit_final(out, detail_path(world))
         printed = True
+        wd.hold(None, code)      # the line is out: an overrun from here only exits
         wd.enter("shutdown", 300.0)
         for conn, _ in lockstep_learners + async_learners:
             conn.close()
@@ -2420,14 +2432,13 @@ def main(argv=None):
         progress("after the measured line, phase '%s': %s: %s" % (wd.phase, type(e).__name__, e))
         if not wd.disarm():      # the watchdog fired first: it prints the line and exits
             time.sleep(600)
-        wd.hold(None, code)      # no last words: the line is printed here (or was)
         if out is not None and not printed:
             out["error"] = "after the measurement, phase '%s': %s: %s" % (wd.phase, type(e).__name__, e)
             out["phase"] = wd.phase
             if wd.transport is not None and isinstance(out.get("parity"), dict):   # a late parity check
                 out["parity"][wd.transport] = False
                 out["parity_failed"] = sorted(k for k, v in out["parity"].items() if k != "workload" and not v)
-            emit_result(out, detail_path(world))
+            emit_final(out, detail_path(world))
         sys.stderr.flush()
         os._exit(code)
     wd.idle()

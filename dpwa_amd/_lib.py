@@ -87,6 +87,7 @@ SIGNATURES = {
     "dpwa_trace_push": [ctypes.c_char_p],
     "dpwa_trace_pop": [],
     "dpwa_last_words_set": [ctypes.c_int, ctypes.c_char_p, ctypes.c_int64],
+    "dpwa_last_words_flush": [ctypes.POINTER(ctypes.c_int)],
     "dpwa_last_words_written": [ctypes.POINTER(ctypes.c_int)],
     "dpwa_lerp_f32": [_vp, _vp, _i64, _vp, _vp],
     "dpwa_lerp_bf16": [_vp, _vp, _i64, _vp, _vp],
@@ -252,6 +253,13 @@ def last_words(fd, line):
     signal or dies by one (include/dpwa_hip.h dpwa_last_words_set)."""
     data = line.encode() if line else b""
     call("dpwa_last_words_set", int(fd) if data else -1, data or None, len(data))
+
+
+def last_words_flush():
+    """Writes the registered line now, unless a signal already did; True when this call wrote it."""
+    w = ctypes.c_int()
+    call("dpwa_last_words_flush", ctypes.byref(w))
+    return bool(w.value)
 
 
 def last_words_written():

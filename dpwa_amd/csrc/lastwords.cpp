@@ -8,8 +8,13 @@
 // re-raises, so faulthandler's dump and the default action still follow.
 //
 // Two static line buffers: dpwa_last_words_set fills the inactive one and then publishes it with
-// one atomic store, so a signal arriving mid-update writes the previous, complete line.
+// one atomic store, so a signal arriving mid-update writes the previous, complete line.  The
+// normal end prints the line through dpwa_last_words_flush: the line is written exactly once,
+// by whichever of the flush and a signal claims it first (a handler that finds the flush writing
+// on another thread waits for it, up to 2 s, before the process goes).
+#include <pthread.h>
 #include <signal.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -33,7 +38,7 @@ struct Line {
 Line g_lines[2];
 std::atomic<Line *> g_active{nullptr};      // nullptr: nothing to write
 std::atomic<int> g_fd{-1};
-std::atomic<int> g_written{0};
+std::atomic<int> g_state{0};                // 0 armed, 1 being written (by the flush), 2 written
 int g_next = 0;                             // the buffer the next set fills (setter side only)
 std::mutex g_set_mu;
 bool g_installed = false;
@@ -46,20 +51,40 @@ int slot_of(int sig)
     return -1;
 }
 
+void write_all(int fd, const Line *l)
+{
+    const char *p = l->buf;
+    size_t left = l->len;
+    while (left) {
+        const ssize_t w = write(fd, p, left);
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) break;
+        p += w;
+        left -= (size_t)w;
+    }
+}
+
+// Claims the line (state 0 -> 1), writes it, marks it written; false when it was claimed before.
+bool write_once()
+{
+    Line *l = g_active.load(std::memory_order_acquire);
+    const int fd = g_fd.load(std::memory_order_relaxed);
+    int armed = 0;
+    if (!l || fd < 0 || !g_state.compare_exchange_strong(armed, 1)) return false;
+    write_all(fd, l);
+    g_state.store(2);
+    return true;
+}
+
 void on_signal(int sig)
 {
     const int saved = errno;
-    Line *l = g_active.load(std::memory_order_acquire);
-    const int fd = g_fd.load(std::memory_order_relaxed);
-    if (l && fd >= 0 && !g_written.exchange(1)) {
-        const char *p = l->buf;
-        size_t left = l->len;
-        while (left) {
-            const ssize_t w = write(fd, p, left);
-            if (w < 0 && errno == EINTR) continue;
-            if (w <= 0) break;
-            p += w;
-            left -= (size_t)w;
+    if (!write_once()) {
+        // the flush may be writing on another thread (it blocks these signals on its own): let it
+        // finish before the previous handler ends the process
+        for (int i = 0; i < 2000 && g_state.load() == 1; ++i) {
+            struct timespec ts = {0, 1000000};
+            nanosleep(&ts, nullptr);
         }
     }
     const int i = slot_of(sig);
@@ -106,9 +131,21 @@ extern "C" int dpwa_last_words_set(int fd, const char *line, int64_t len)
     return DPWA_OK;
 }
 
+extern "C" int dpwa_last_words_flush(int *wrote)
+{
+    sigset_t block, old;
+    sigemptyset(&block);
+    for (int sig : kSignals) sigaddset(&block, sig);
+    pthread_sigmask(SIG_BLOCK, &block, &old);      // no handler on this thread mid-write
+    const bool w = write_once();
+    pthread_sigmask(SIG_SETMASK, &old, nullptr);
+    if (wrote) *wrote = w ? 1 : 0;
+    return DPWA_OK;
+}
+
 extern "C" int dpwa_last_words_written(int *written)
 {
     if (!written) return dpwa::set_error(DPWA_ERR_ARG, "dpwa_last_words_written: NULL argument");
-    *written = g_written.load();
+    *written = g_state.load() == 2 ? 1 : 0;
     return DPWA_OK;
 }

@@ -102,10 +102,13 @@ int dpwa_trace_push(const char *name);
 int dpwa_trace_pop(void);
 
 /* Last words (bench.py's held result line): registers `line` (len bytes, at most 16 KiB; len 0
- * clears it) to be written to `fd` with write(2), once, if the process is ended by SIGTERM,
- * SIGINT, SIGHUP, SIGABRT, SIGSEGV, SIGBUS, SIGFPE or SIGILL; the handler then restores the
- * previous handler and re-raises.  The first call installs the handlers.  ABI version 10. */
+ * clears it) to be written to `fd` with write(2) if the process is ended by SIGTERM, SIGINT,
+ * SIGHUP, SIGABRT, SIGSEGV, SIGBUS, SIGFPE or SIGILL; the handler then restores the previous
+ * handler and re-raises.  The first call installs the handlers.  dpwa_last_words_flush writes
+ * the registered line now; the line is written at most once, by the flush or by a signal,
+ * whichever claims it first (*wrote = 1 when the flush did).  ABI version 10. */
 int dpwa_last_words_set(int fd, const char *line, int64_t len);
+int dpwa_last_words_flush(int *wrote);
 int dpwa_last_words_written(int *written);
 
 /* ------------------------------------------------------------------------------------

@@ -62,6 +62,20 @@ time.sleep(30)
     assert rc == -signal.SIGTERM and out == ""
 
 
+def test_flush_writes_once_and_a_later_signal_writes_nothing():
+    _lib_or_skip()
+    rc, out, _ = _run("""
+_lib.last_words(1, '{"value": 4}\\n')
+assert _lib.last_words_flush() is True
+assert _lib.last_words_flush() is False and _lib.last_words_written() is True
+_lib.last_words(1, '{"value": 5}\\n')
+assert _lib.last_words_flush() is False
+os.kill(os.getpid(), signal.SIGTERM)
+time.sleep(30)
+""")
+    assert rc == -signal.SIGTERM and out == '{"value": 4}\n'
+
+
 def test_previous_handler_still_runs():
     """faulthandler registered before (as bench.py does for SIGTERM) still dumps the threads."""
     _lib_or_skip()
