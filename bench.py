@@ -72,6 +72,7 @@ MIX_CEILING_11M = {"mix": "2R:2W", "frac": 0.759, "source": "profiles/r02_stream
 
 _T0 = time.perf_counter()
 _RESULT_FD = 1       # where the one result line goes (main() moves everything else off stdout)
+_WATCHDOG = None     # main()'s, for the exception guard under __main__
 
 
 def emit(line):
@@ -146,6 +147,8 @@ def parse(argv=None):
                     help="N>1: leave sizes above this out of the round sweep (rehearsals with ranks sharing a GPU)")
     ap.add_argument("--compute-us", type=float, default=1000.0,
                     help="per-learner synthetic training step (bf16 GEMM loop) for the 'overlap' field; 0 = skip")
+    ap.add_argument("--no-provisional", action="store_true",
+                    help="N>1: no provisional lock-step copy measurement before the other transports are checked")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the parity leg (a short gossip through every transport, checked against the oracle)")
     ap.add_argument("--traffic", default=None,
@@ -176,7 +179,7 @@ def base_line(args, world):
 LINE_MAX = 6144
 _TOP = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "gossip_rounds_per_s", "gossip_rounds_per_s_per_learner", "averagings",
-        "publish_fallback", "error", "phase")
+        "publish_fallback", "error", "phase", "provisional")
 _ROOFLINE = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_x", "bytes_per_launch",
              "metric_bytes_per_averaging", "avg_launch_us", "kernel", "in_loop_frac", "in_loop_avg_launch_us",
              "mix_ceiling_frac", "kernel_over_mix_ceiling", "learners_per_launch")
@@ -439,7 +442,8 @@ class Watchdog:
             self._words = False
             return
         out = dict(held)
-        out["error"] = "ended by a signal in phase '%s', after the measurement (the line up to it)" % phase
+        out["error"] = ("ended by a signal in phase '%s', %s" % (phase, "before the full measurement (the provisional line)"
+                        if held.get("provisional") else "after the measurement (the line up to it)"))
         out["phase"] = phase
         if transport is not None and isinstance(out.get("parity"), dict):
             out["parity"] = dict(out["parity"], **{transport: False})
@@ -952,6 +956,91 @@ class _Env:
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+
+
+def provisional_line(args, world, rank, device, cfg, mine, dtype, ctl, watchdog, parity):
+    """N>1 insurance for the driver's multi-GPU run: right after `lockstep/copy` (the plainest
+    transport: a copy-engine pull from an IPC-mapped slot) passed its parity check, the line's
+    rounds are timed once on it -- --warmup untimed and --steps timed lock-step rounds,
+    write-through, barrier + synchronize on both sides, max over ranks -- before any other
+    transport runs on this node's devices.  Rank 0 gets the provisional line (the others None);
+    main() holds it, so a hang, a fault or a stop in what follows still leaves a verified,
+    measured line (marked `provisional`).  The learners are closed before the parity leg goes on.
+    Returns (ok, line): ok agreed over the ranks; line on rank 0 only."""
+    from dpwa_amd import DpwaConnection
+    watchdog.enter("provisional measurement (lockstep/copy)", 300.0)
+    esize = 4 if dtype == torch.float32 else 2
+    conns, err, el, averaged = [], None, None, 0
+    try:
+        for name, seed in mine:
+            g = torch.Generator(device=device).manual_seed(seed)
+            flat = torch.randn(args.numel, device=device, generator=g, dtype=torch.float32).to(dtype)
+            conns.append((DpwaConnection(name, cfg, seed=1000 + seed, group="lockstep", pull="copy"), flat))
+
+        def step():
+            done = 0
+            for conn, flat in conns:
+                conn.update_send(flat, 1.0, reuse_snapshot=True)
+            for conn, flat in conns:
+                done += conn.update_wait_average(flat, 1.0, write_through=True)[0] is not None
+            return done
+
+        for _ in range(max(1, args.warmup)):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier(group=ctl)
+        t0 = time.perf_counter()
+        averaged = sum(step() for _ in range(args.steps))
+        torch.cuda.synchronize()
+        dist.barrier(group=ctl)
+        el = time.perf_counter() - t0
+    except Exception as e:   # noqa: BLE001 -- no provisional line; the run goes on as before
+        err = "%s: %s" % (type(e).__name__, e)
+        progress("provisional measurement FAILED: %s" % err)
+    finally:
+        for conn, _ in conns:
+            try:
+                conn.close()
+            except Exception as e:   # noqa: BLE001
+                progress("provisional close: %s" % e)
+        conns = []
+        torch.cuda.synchronize()
+    ok = _agree(err is None, world, ctl)
+    got = [None] * world
+    dist.all_gather_object(got, (el, averaged), group=ctl)
+    dist.barrier(group=ctl)
+    watchdog.idle()
+    if not ok or rank != 0:
+        return ok, None
+    el_max = max(g[0] for g in got)
+    av = sum(g[1] for g in got)
+    out = base_line(args, world)
+    value = round(av * 3 * args.numel * esize / el_max / 1e9, 2)
+    rps = round(world * args.steps / el_max, 1)
+    out.update({
+        "value": value,
+        "ms_per_step": round(1e3 * el_max / args.steps, 4),
+        "gossip_rounds_per_s": rps,
+        "averagings": int(av),
+        "provisional": True,
+        # the kernel is not timed on its own in this pass: the roofline block names it and its bytes
+        "roofline": {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                     "traffic": None, "bytes_per_launch": 4 * args.numel * esize, "avg_launch_us": None,
+                     "metric_bytes_per_averaging": 3 * args.numel * esize,
+                     "kernel": "dpwa::k_lerp<Ops%s, COEF_FUSED, true> (not timed alone in the provisional pass)"
+                               % args.dtype.upper()},
+        "scaling_basis": {"n_gpus": world, "learners_per_gpu": len(mine), "publish": "write-through",
+                          "raw": {"gossip_rounds_per_s": rps, "value": value}, "weak": {}},
+        "config": {"workload": "north_star on-node gossip, one learner per GPU (provisional: lockstep/copy)",
+                   "numel": args.numel, "pull": "lockstep/copy", "publish": "write-through",
+                   "interpolation": args.interpolation, "fetch_probability": args.fetch_probability,
+                   "learners_per_gpu": len(mine)},
+        "parity": parity,
+        "parity_of_timed_transport": {"transport": "lockstep/copy", "ok": True},
+        "note": "measured before the other transports were checked and timed, so that the line survives them",
+    })
+    progress("provisional: %.1f GB/s (%.4f ms/step)" % (out["value"], out["ms_per_step"]))
+    return ok, out
 
 
 def parity_leg(world, rank, local_rank, device, cfg_dir, transports, dist_backend, ctl=None, watchdog=None):
@@ -1603,7 +1692,8 @@ def main(argv=None):
         raise SystemExit("--publish resident at N=1: the line's learner averages with its own snapshot "
                          "(configs[1]'s self-peer), which resident parameters would read twice from one slot; "
                          "the resident co-resident pair is the line's `co_resident_pair` block")
-    wd = Watchdog(args, world, rank)
+    global _WATCHDOG
+    wd = _WATCHDOG = Watchdog(args, world, rank)
     # the CPU baseline first, before anything touches the GPU (its learners are child processes)
     wd.enter("start: world %d, numel %d %s" % (world, args.numel, args.dtype), 600.0)
     cpu = None
@@ -1653,13 +1743,24 @@ def main(argv=None):
     # fd-shared (+vmm) forms are checked after the line is held (late_parity): no timed transport
     # uses them (they only gate the sweep's sizes above VMM_MIN_BYTES), so a hang in an import
     # path the line does not depend on costs the watchdog's phase, not the measured line.
+    # Before the others, at N>1, lockstep/copy alone: once it passed, a provisional line is
+    # measured on it and held (provisional_line), so the driver's multi-GPU run keeps a verified
+    # measurement whatever the less plain transports do on its devices.
     parity = None
     late_parity = []
     if not args.no_parity:
         transports = parity_transports(world, args.gossip)
         late_parity = [t for t in transports if "+vmm" in t] if world > 1 else []
-        parity = parity_leg(world, rank, local_rank, device, tmp, [t for t in transports if t not in late_parity],
-                            args.dist_backend, ctl=ctl, watchdog=wd)
+        early = [t for t in transports if t not in late_parity]
+        first = early[:1] if world > 1 and early[:1] == ["lockstep/copy"] else []
+        parity = parity_leg(world, rank, local_rank, device, tmp, first, args.dist_backend, ctl=ctl,
+                            watchdog=wd) if first else {}
+        if first and parity.get("lockstep/copy") and not args.no_provisional:
+            ok, prov = provisional_line(args, world, rank, device, cfg, mine, dtype, ctl, wd, parity)
+            if ok:
+                wd.hold(prov, 0)
+        parity.update(parity_leg(world, rank, local_rank, device, tmp, early[len(first):], args.dist_backend,
+                                 ctl=ctl, watchdog=wd))
 
     # rehearsals run several ranks on one GPU: their pulls never cross an xGMI link
     shared_device = world > 1 and world > torch.cuda.device_count()
@@ -1988,11 +2089,11 @@ def main(argv=None):
         if not medians:
             wd.idle()
             if rank == 0:
-                out = base_line(args, world)
+                out = dict(wd.held) if wd.held is not None else base_line(args, world)   # the provisional line
                 out["error"] = "no transport passed the parity check and its trials"
                 out["parity"] = parity
                 out["trial_errors"] = trial_errors
-                emit_result(out, detail_path(world))
+                emit_final(out, detail_path(world))
             sys.exit(1)
         pull = max(medians, key=medians.get)
         if pull.startswith("async/"):
@@ -2453,4 +2554,22 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as e:   # noqa: BLE001 -- a held line (provisional or final) still goes out
+        wd = _WATCHDOG
+        if wd is None or wd.held_rc is None:
+            raise
+        if not wd.disarm():      # the watchdog fired first: it prints the line and exits
+            time.sleep(600)
+        import traceback
+        traceback.print_exc()
+        if wd.held is not None:
+            out = dict(wd.held)
+            out["error"] = "phase '%s': %s: %s (the held line)" % (wd.phase, type(e).__name__, e)
+            out["phase"] = wd.phase
+            if wd.transport is not None and isinstance(out.get("parity"), dict):
+                out["parity"] = dict(out["parity"], **{wd.transport: False})
+            emit_final(out, detail_path(wd.world))
+        sys.stderr.flush()
+        os._exit(wd.held_rc)     # as the watchdog would have exited

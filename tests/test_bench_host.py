@@ -33,6 +33,9 @@ def test_parity_transports_cover_every_trial_and_the_fd_shared_path():
     t = bench.parity_transports(8)
     assert "lockstep/relay-avg:32+vmm" in t and "async/copy+vmm" in t
     assert "lockstep/relay-avg:32+res+vmm" in t and "async/copy+res+vmm" in t
+    # the provisional N>1 line is measured right after the first transport, which must be the plain
+    # copy-engine pull (main() checks it alone, then the rest)
+    assert t[0] == "lockstep/copy" and bench.parity_transports(8, "lockstep")[0] == "lockstep/copy"
     lockstep = ["copy", "kernel:256", "kernel:1024", "relay:32", "relay:128", "relay:512", "relay-avg:32",
                 "relay-avg:128", "relay-avg:512"]
     trials = lockstep + ["async/%s%s" % (m, wt) for m in lockstep if not m.startswith("relay") for wt in ("", "+wt")]

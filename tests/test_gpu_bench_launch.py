@@ -69,6 +69,7 @@ def test_self_launched_two_ranks_print_one_line(tmp_path):
     import bench
     assert set(parity) == set(bench.parity_transports(2)) and all(parity.values()), parity
     assert out["parity_of_timed_transport"]["ok"]
+    assert "provisional" not in out and "error" not in out     # the final line replaced the provisional one
 
 
 def _scaling_schema(out):
@@ -135,6 +136,21 @@ def test_hang_in_a_late_parity_transport_keeps_the_measured_line(tmp_path):
     assert ("watchdog" in out["error"] or "after the measurement" in out["error"]), out["error"]
     assert out["phase"] == "parity %s" % t
     assert all(v for k, v in out["parity"].items() if "+vmm" not in k)
+
+
+def test_hang_before_the_final_measurement_leaves_the_provisional_line(tmp_path):
+    """At N>1 lockstep/copy is checked first and the line's rounds are timed on it at once (the
+    provisional line, held): a hang in a later transport (rank 1 raises at the start of
+    lockstep/kernel:256, rank 0 blocks in its first collective) ends the job with that line --
+    marked provisional, measured on the verified copy transport -- and that transport false."""
+    t = "lockstep/kernel:256"
+    rc, lines, err = _bench(tmp_path, {"DPWA_BENCH_INJECT": "%s@1:start" % t}, args=ARGS + ["--phase-scale", "0.1"])
+    assert rc == 0, err[-3000:]
+    out = _line(lines)
+    assert out["provisional"] is True and out["value"] > 0 and out["ms_per_step"] > 0, out
+    assert out["parity_of_timed_transport"] == {"transport": "lockstep/copy", "ok": True}
+    assert out["parity"]["lockstep/copy"] is True and out["parity"][t] is False
+    assert out["phase"] == "parity %s" % t, out["phase"]
 
 
 def test_rank_lost_after_the_measurement_keeps_the_measured_line(tmp_path):
