@@ -102,6 +102,10 @@ bool install()
         sigemptyset(&sa.sa_mask);
         sa.sa_flags = SA_RESTART;
         if (sigaction(kSignals[i], &sa, &g_prev[i]) != 0) return false;
+        // an ignored signal (SIGHUP under nohup) does not end the process: it stays ignored, or
+        // the line would be written for a run that goes on
+        if (!(g_prev[i].sa_flags & SA_SIGINFO) && g_prev[i].sa_handler == SIG_IGN)
+            sigaction(kSignals[i], &g_prev[i], nullptr);
     }
     return true;
 }

@@ -76,6 +76,20 @@ time.sleep(30)
     assert rc == -signal.SIGTERM and out == '{"value": 4}\n'
 
 
+def test_an_ignored_signal_stays_ignored():
+    """SIGHUP ignored before (nohup): it neither writes the line nor ends the run."""
+    _lib_or_skip()
+    rc, out, _ = _run("""
+signal.signal(signal.SIGHUP, signal.SIG_IGN)
+_lib.last_words(1, '{"value": 6}\\n')
+os.kill(os.getpid(), signal.SIGHUP)
+time.sleep(0.2)
+assert _lib.last_words_written() is False
+assert _lib.last_words_flush() is True
+""")
+    assert rc == 0 and out == '{"value": 6}\n'
+
+
 def test_previous_handler_still_runs():
     """faulthandler registered before (as bench.py does for SIGTERM) still dumps the threads."""
     _lib_or_skip()
