@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Checks a bench.py stdout capture the way the driver reads it: exactly one non-empty line, at
-most bench.LINE_MAX bytes, json.loads succeeds, the contract keys present, scalar blocks only.
+most bench.LINE_MAX bytes, json.loads succeeds, the contract keys present, scalar blocks only,
+and a completed run (no `error`, not the provisional N>1 line).
 Prints a one-line summary.  Usage: tools/check_line.py <stdout file>"""
 import json
 import os
@@ -24,6 +25,9 @@ def main(path):
     for block in ("roofline", "config", "cpu_baseline", "parity", "xgmi"):
         if isinstance(d.get(block), dict):
             assert not any(isinstance(v, (dict, list)) for v in d[block].values()), block
+    # a held line printed after a failure (watchdog, exception, signal) or the provisional one is
+    # still a parseable line, but not a completed run
+    assert "error" not in d and not d.get("provisional"), "not a completed run: %s" % d.get("error", "provisional")
     print("%s: %d bytes, n_gpus %s, value %s, ms_per_step %s, frac %s, pull %s, parity %s, weak %s" % (
         path, n, d["n_gpus"], d["value"], d["ms_per_step"], d["roofline"].get("frac"), d.get("pull"),
         "all true" if all((d.get("parity") or {"-": False}).values()) else d.get("parity"),
