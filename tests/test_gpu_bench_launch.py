@@ -253,7 +253,7 @@ def test_driver_command_prints_one_bounded_line(tmp_path):
     assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] in ("port", "reference") and cpu["ms_per_round"] > 0
     assert 0 < out["value_cold"] <= 8000.0 and out["value"] > 0 and out["ms_per_step"] > 0
     assert set(out["scaling_basis"]) >= {"raw", "weak"} and out["parity_of_timed_transport"]["ok"]
-    assert all(out["parity"].values())
+    assert all(out["parity"].values()) and "error" not in out and "provisional" not in out
     det = _detail(out)
     assert det["value"] == out["value"] and det["cpu_baseline"]["restatement_rows"]
     assert det["roofline"]["size_sweep"] and det["round_sweep"]
