@@ -237,6 +237,36 @@ def test_result_line_is_bounded_scalar_and_keeps_the_headline():
         assert "round_sweep" not in d and "adapter_loop" not in d
 
 
+def test_provisional_line_is_a_bounded_contract_line():
+    """The N>1 provisional line (bench.provisional_line's shape): the contract keys, `provisional`
+    and its verified transport kept in the compact line, and an error added when it is printed."""
+    import json
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+
+    class A:
+        steps, warmup, dtype, numel, interpolation, fetch_probability = 20, 5, "f32", 11_173_962, "constant", 1.0
+
+    out = bench.base_line(A, 8)
+    parity = {t: True for t in bench.parity_transports(8)}
+    out.update({"value": 900.0, "ms_per_step": 1.2, "gossip_rounds_per_s": 6666.7, "averagings": 160,
+                "provisional": True,
+                "roofline": {"bound": "hbm", "achieved": None, "peak": 8000.0, "unit": "GB/s", "frac": None,
+                             "traffic": None, "bytes_per_launch": 4 * A.numel * 4, "avg_launch_us": None,
+                             "kernel": "k"},
+                "scaling_basis": {"n_gpus": 8, "raw": {"gossip_rounds_per_s": 6666.7, "value": 900.0}, "weak": {}},
+                "config": {"workload": "w", "pull": "lockstep/copy", "numel": A.numel},
+                "parity": parity, "parity_of_timed_transport": {"transport": "lockstep/copy", "ok": True},
+                "error": "watchdog: phase 'parity lockstep/kernel:256' overran its budget (the line up to it)",
+                "phase": "parity lockstep/kernel:256"})
+    d = json.loads(json.dumps(bench.compact_line(out, "gpurun_out/bench_detail_n8.json")))
+    assert len(json.dumps(d)) <= bench.LINE_MAX
+    assert d["provisional"] is True and d["value"] == 900.0 and d["error"].startswith("watchdog")
+    assert d["parity_of_timed_transport"] == {"transport": "lockstep/copy", "ok": True}
+    assert d["config"]["pull"] == "lockstep/copy" and d["roofline"]["bytes_per_launch"] == 4 * A.numel * 4
+
+
 def test_result_line_from_the_committed_round5_line():
     """Round 5's own 21.7 KB line (profiles/r05q_bench.json), compacted: within the bound."""
     import json
